@@ -1,0 +1,192 @@
+/*
+ * mgp_hip.h -- C-ABI of the MI355X (gfx950) SMGP ELBO hot path.
+ *
+ * libmgp_hip.so replaces the TensorFlow C++ ops that GPflow 2.7 dispatches for
+ * the sparse-variational mixture-of-GP-experts ELBO of LouieMiddle/ModulatedGPs
+ * (MixtureGPs/models.py:69-79).  The reference has no native code or FFI of its
+ * own: its operator boundary is the GPflow posterior plugin
+ * IndependentPosteriorSingleOutputModified._conditional_fused
+ * (MixtureGPs/models.py:129-144), the likelihood protocol
+ * (MixtureGPs/likelihoods.py:31-32,39-41 via broadcasting_lik.py:39-46) and the
+ * model hook SMGP._build_likelihood (models.py:69-79).  Each entry point below
+ * names the reference call site it replaces.
+ *
+ * Conventions
+ *  - float32 in HBM, row-major, leading dimensions in ELEMENTS.  Every leading
+ *    dimension of a matrix whose rows are read as float4 must be a multiple of
+ *    4 and every base pointer 16-byte aligned (MGP_ERR_ALIGN otherwise).
+ *  - Hyper-parameters (kernel variance, lengthscales, likelihood variances) are
+ *    DEVICE pointers, so a call never synchronises with the host and can be
+ *    captured in a hipGraph.
+ *  - The caller allocates every buffer, including workspaces sized by the
+ *    *_workspace_bytes queries.  The library never allocates, frees or keeps
+ *    pointers after returning.
+ *  - Every call is asynchronous and ordered on `stream` (a hipStream_t; NULL =
+ *    the legacy default stream) and acts on the current device.
+ *  - Return value: MGP_OK (0); < 0: the (1-based) index of the first invalid
+ *    argument, negated; > 0: an MGP_ERR_* code or MGP_ERR_HIP_BASE + hipError_t.
+ */
+#ifndef MGP_HIP_H
+#define MGP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* mgp_stream_t; /* hipStream_t */
+
+enum {
+  MGP_OK = 0,
+  MGP_ERR_WORKSPACE = 1,   /* workspace pointer NULL or too small */
+  MGP_ERR_ALIGN = 2,       /* leading dimension / pointer alignment */
+  MGP_ERR_UNSUPPORTED = 3, /* size outside the supported range (e.g. D > 64, K > 32) */
+  MGP_ERR_HIP_BASE = 1000
+};
+
+/* Library identity: "mgp_hip <version> gfx950". */
+const char* mgp_version(void);
+const char* mgp_status_string(int status);
+
+/* ---------------------------------------------------------------- K1 / K2
+ * RBF (SquaredExponential) cross-covariance
+ *   Kuf[m, n] = var * exp(-0.5 * sum_d ((Z[m,d] - X[n,d]) / ls[d])^2)
+ * Replaces Kmn = self.kernel.K(self.X_data.Z, Xnew) (models.py:139; GPflow
+ * SquaredExponential.K -> square_distance + K_r2).  n_ls = 1 (isotropic) or D
+ * (ARD).  X: [N, D] (ld ldx), Z: [M, D] (ld ldz), Kuf: [M, N] (ld ldk % 4 == 0). */
+int mgp_rbf_kuf(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                float* Kuf, int64_t ldk, mgp_stream_t stream);
+
+/* Kuu[i, j] = K(Z, Z)[i, j] + jitter * (i == j).
+ * Replaces covariances.Kuu(self.X_data, self.kernel, jitter=default_jitter())
+ * (models.py:135).  Kuu: [M, M] (ld ldk % 4 == 0). */
+int mgp_rbf_kuu(const float* Z, int64_t ldz, int64_t M, int32_t D, const float* variance,
+                const float* lengthscales, int32_t n_ls, float jitter, float* Kuu, int64_t ldk,
+                mgp_stream_t stream);
+
+/* ---------------------------------------------------------------- K3
+ * Batched blocked Cholesky with the triangular inverse fused in, computed in
+ * float64 (the M x M work is M^3/3 flops; float32 would lose cond(L) * eps32 on
+ * the badly conditioned Kuu of real inducing-point sets):
+ *   L = chol(A) (lower, zeros above), LinvT = (L^-1)^T (upper, zeros below),
+ * both rounded to float32.  Replaces Lm = tf.linalg.cholesky(Kmm) inside GPflow
+ * base_conditional (models.py:141) and supplies L^-1 for its
+ * triangular_solve.  `batch` matrices at element strides strideA / strideL
+ * (the two SVGP layers of one ELBO share every launch).  info[b] = 0, or the
+ * 1-based column of the first non-positive pivot (LAPACK potrf convention);
+ * the factor then carries NaN.  L may be NULL.  lda, ldl % 4 == 0. */
+size_t mgp_chol_workspace_bytes(int64_t M, int32_t batch);
+int mgp_potrf_trtri(const float* A, int64_t lda, int64_t strideA, int64_t M, int32_t batch,
+                    float* L, float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                    void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+
+/* Same, with Kuu = var_b exp(-0.5 |(z_i - z_j)/l_b|^2) + jitter I built in
+ * float64 from Z_b inside the factorisation (fuses K2 into K3; replaces
+ * covariances.Kuu at models.py:135 for the ELBO path).  Z, variance,
+ * lengthscales: HOST arrays of `batch` (<= 8) DEVICE pointers; n_ls: host
+ * array (1 or D per entry).  Every Z_b is [M, D] with leading dimension ldz. */
+int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                        const float* const* variance, const float* const* lengthscales,
+                        const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                        float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                        void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+
+/* ---------------------------------------------------------------- K4
+ * Whitened projection A = L^-1 Kuf (as the triangular GEMM LinvT^T . Kuf) plus
+ * per-row-tile column statistics for the conditional:
+ *   stats[t][0][n]   = sum_{m in row tile t} A[m,n]^2
+ *   stats[t][1+k][n] = sum_{m in row tile t} A[m,n] * q_mu[m,k]
+ * Replaces A = tf.linalg.triangular_solve(Lm, Kmn), sum(square(A), -2) and
+ * fmean = matmul(A, f, transpose_a=True) in GPflow base_conditional
+ * (models.py:141-143).  q_mu: [M, K] (ld ldq).  stats: [T][K+1][lds] with
+ * T = mgp_stats_tiles(M); lds % 4 == 0, lds >= N. */
+int mgp_stats_tiles(int64_t M);
+int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M,
+                   int64_t N, const float* q_mu, int64_t ldq, int32_t K, float* A, int64_t lda,
+                   float* stats, int64_t lds, mgp_stream_t stream);
+
+/* ---------------------------------------------------------------- K5
+ * K-expert whitened conditional, finalised:
+ *   fmean[k][n] = sum_t stats[t][1+k][n]
+ *   fvar[k][n]  = var - sum_t stats[t][0][n] + sum_{m'} (sum_{m>=m'} L_k[m,m'] A[m,n])^2
+ * with L_k = band_part(q_sqrt[k], -1, 0) (the upper triangle is ignored).
+ * Replaces the LTA = matmul(L, A_tiled, transpose_a=True) / reduce_sum(square)
+ * tail of GPflow base_conditional (models.py:141-143; Knn = var from
+ * models.py:133).  q_sqrt: [K][M][ldqs] at element stride strideq.
+ * fmean, fvar: [K][ldf] (expert-major; ldf >= N). */
+int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
+                           int64_t strideq, const float* stats, int64_t lds,
+                           const float* variance, int64_t M, int64_t N, int32_t K, float* fmean,
+                           float* fvar, int64_t ldf, mgp_stream_t stream);
+
+/* ---------------------------------------------------------------- K7
+ * Whitened Gaussian KL (GPflow gauss_kl(q_mu, q_sqrt, K=None), reached through
+ * SVGP.prior_kl at models.py:79):
+ *   kl = 0.5 * (sum q_mu^2 - M*K - sum_k sum_m log(L_k[m,m]^2) + sum_k ||tril L_k||_F^2)
+ * Written as one double to kl_out (device).  Workspace: mgp_kl_workspace_bytes. */
+size_t mgp_kl_workspace_bytes(int64_t M, int32_t K);
+int mgp_gauss_kl_white(const float* q_mu, int64_t ldq, const float* q_sqrt, int64_t ldqs,
+                       int64_t strideq, int64_t M, int32_t K, double* kl_out, void* workspace,
+                       size_t workspace_bytes, mgp_stream_t stream);
+
+/* ---------------------------------------------------------------- K6
+ * Monte-Carlo data term of the SMGP ELBO for the local data points:
+ *   data_sum = sum_n [ logsumexp_s( sum_k W[s,n,k] ve[n,k] ) - log S ]
+ *   logits = mu_a + z * sqrt(var_a + 1e-6)              (models.py:57-58, utils.py:26-27)
+ *   W = softmax_k((-log(-log u) + logits) / tau)         (models.py:59-60,73-74; TFP 0.18)
+ *   ve = -0.5 log 2pi - 0.5 log s2_k - 0.5((y - mu_f)^2 + var_f)/s2_k  (likelihoods.py:39-41)
+ * Replaces SMGP.W_dist / E_log_p_Y / the batch sum of models.py:55-76.
+ * mu_*, var_*: [K][ldf]; Y: [N]; lik_var: [K] (device).  Noise: explicit
+ * noise_z / noise_u [S][N][K] when both non-NULL (parity mode), else in-kernel
+ * Philox4x32-10 keyed by (seed, global n = n_offset + n, s, k).  data_sum: one
+ * double (device).  Workspace: mgp_elbo_workspace_bytes(N). */
+size_t mgp_elbo_workspace_bytes(int64_t N);
+int mgp_elbo_terms(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
+                   int64_t ldf, const float* Y, const float* lik_var, int64_t N, int32_t K,
+                   int32_t S, float tau, const float* noise_z, const float* noise_u,
+                   uint64_t seed, int64_t n_offset, double* data_sum, void* workspace,
+                   size_t workspace_bytes, mgp_stream_t stream);
+
+/* elbo = data_sum / n_batch - (kl_f + kl_a) / num_data   (models.py:76,79)
+ * All pointers device; elbo_out float32 and elbo_out64 (nullable) double. */
+int mgp_elbo_combine(const double* data_sum, const double* kl_f, const double* kl_a,
+                     double n_batch, double num_data, float* elbo_out, double* elbo_out64,
+                     mgp_stream_t stream);
+
+/* Predictive epilogue (SGP.predict_y, models.py:38-41 -> likelihoods.py:31-32;
+ * SMGP.predict_assign, models.py:85-89):
+ *   y_mean[n][k] = fmean[k][n]; y_var[n][k] = fvar[k][n] + lik_var[k]
+ *   assign[n][k] = softmax_k(amean[k][n])
+ * Any output may be NULL.  Outputs are [N][K] row-major (the reference layout). */
+int mgp_predict_epilogue(const float* fmean, const float* fvar, const float* amean, int64_t ldf,
+                         const float* lik_var, int64_t N, int32_t K, float* y_mean, float* y_var,
+                         float* assign, mgp_stream_t stream);
+
+/* SMGP.predict_samples (models.py:91-103): a fresh assignment sample W (as in
+ * mgp_elbo_terms) and one normal draw z shared by the y- and f-samples:
+ *   samples_y[s][n] = sum_k W (mu_f + z sqrt(var_f + lik_var_k + 1e-6))
+ *   samples_f[s][n] = sum_k W (mu_f + z sqrt(var_f + 1e-6))
+ * Explicit noise (all three [S][N][K], parity mode) or Philox (streams 0/1 for
+ * W, stream 2 for z).  Outputs [S][N]; either may be NULL. */
+int mgp_predict_samples(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
+                        int64_t ldf, const float* lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                        const float* noise_zw, const float* noise_uw, const float* noise_zy,
+                        uint64_t seed, int64_t n_offset, float* samples_y, float* samples_f,
+                        mgp_stream_t stream);
+
+/* Raw noise stream (for tests and for SMGP.predict_samples): writes
+ * z[s][n][k] (normals) and/or u[s][n][k] (uniforms in (0,1)) exactly as
+ * mgp_elbo_terms draws them in Philox mode.  Either pointer may be NULL. */
+int mgp_philox_noise(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S, float* z,
+                     float* u, mgp_stream_t stream);
+/* Same, stream-2 normals (the z of mgp_predict_samples). */
+int mgp_philox_normal2(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S, float* z,
+                       mgp_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGP_HIP_H */

@@ -1,0 +1,77 @@
+"""Build libmgp_hip.so (gfx950) in-tree with hipcc.
+
+    python -m modulatedgps_amd.build [-v]
+
+The shared library has a plain C ABI (include/mgp_hip.h) and no torch
+dependency; it links only the HIP runtime.  Objects are compiled in parallel
+and the library is relinked only when a source or header is newer.
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+BUILD = os.path.join(PKG, "_build")
+LIB = os.path.join(PKG, "libmgp_hip.so")
+ARCH = os.environ.get("MGP_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+CXXFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-I", INCLUDE, "-I", CSRC,
+            "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+
+
+def _sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def _headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    return hs
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else -1.0
+
+
+def _compile(src, hdr_time, verbose, extra):
+    obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
+    if _mtime(obj) >= max(_mtime(src), hdr_time) and not extra:
+        return obj
+    cmd = [HIPCC, *CXXFLAGS, *extra, "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    if verbose and r.stderr.strip():
+        print(r.stderr, flush=True)
+    return obj
+
+
+def build(verbose=False, extra_flags=()):
+    """Compile every csrc/*.hip for gfx950 and link modulatedgps_amd/libmgp_hip.so."""
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    hdr_time = max([_mtime(h) for h in _headers()] + [0.0])
+    extra = list(extra_flags)
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr_time, verbose, extra), srcs))
+    if _mtime(LIB) < max(_mtime(o) for o in objs) or extra:
+        tmp = LIB + ".tmp"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

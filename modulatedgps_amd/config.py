@@ -1,0 +1,32 @@
+"""Global configuration mirroring the GPflow globals the reference relies on
+(MixtureGPs/models.py:16-17: default_float / default_jitter), plus the device.
+
+The compute dtype of this build is float32 (the MI355X path); the reference's
+float64 semantics are the parity target (tolerances in tests/)."""
+import torch
+
+_CFG = {"jitter": 1e-6, "device": None}
+
+
+def default_jitter():
+    return _CFG["jitter"]
+
+
+def set_default_jitter(v):
+    _CFG["jitter"] = float(v)
+
+
+def default_float():
+    return torch.float32
+
+
+def default_device():
+    if _CFG["device"] is not None:
+        return _CFG["device"]
+    if not torch.cuda.is_available():
+        raise RuntimeError("modulatedgps_amd needs a HIP device (MI355X); none is visible")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def set_default_device(dev):
+    _CFG["device"] = torch.device(dev)

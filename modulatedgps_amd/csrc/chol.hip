@@ -1,0 +1,432 @@
+// K3: batched blocked Cholesky of Kuu with the triangular inverse fused in,
+// computed in float64 (optionally with Kuu itself built in float64 from Z).
+//
+// Reference: Lm = tf.linalg.cholesky(Kmm) inside GPflow base_conditional,
+// reached from MixtureGPs/models.py:141, with Kmm = covariances.Kuu(Z, kernel,
+// jitter) from models.py:135; the inverse replaces the S-batched
+// tf.linalg.triangular_solve(Lm, Kmn) by one triangular GEMM (trigemm.hip).
+//
+// Precision design: the reference runs in float64.  Kuu is often badly
+// conditioned (cond 1e4..1e7 for inducing points drawn from the data), and a
+// float32 factorisation (LAPACK spotrf included) loses cond(L) * eps32 -- up to
+// 1e-3 normwise on the conditional at BASELINE config 2.  The M x M work here is
+// M^3/3 flops (0.36 GFLOP at M = 1024, a few microseconds of the chip), so it
+// runs in float64 (v_mfma_f64_16x16x4_f64 + f64 VALU) and only the N-scaled
+// GEMMs (K4/K5) run in float32.  Outputs L and (L^-1)^T are rounded to float32.
+//
+// Algorithm (block CB = 64, nb = ceil(M/64), matrix padded with identity to
+// nb*64): a right-looking blocked Cholesky that carries the forward
+// substitution of L X = I along ("augmented" sweep):
+//   step j:  P_i = W_ij D_j^T                    (= L_ij, D_j = L_jj^-1)
+//            W_il -= P_i P_l^T        j < l <= i (trailing update, f64 MFMA)
+//            X_jc  = D_j B_jc         c <= j     (row block j of X = L^-1)
+//            B_ic -= P_i X_jc         i > j      (forward-substitution update)
+//            the workgroup that owns tile (j+1, j+1) factors it right after its
+//            update (look-ahead), producing L_{j+1,j+1} and D_{j+1}.
+// One launch per step; every tile of a step is independent (each workgroup
+// recomputes the 64^3 panels it needs); every launch carries all `batch`
+// matrices (blockIdx.y).  nb + 1 launches per factorisation.
+#include <math.h>
+
+#include "mgp_common.hpp"
+
+namespace mgp {
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
+constexpr int CB = 64;        // Cholesky block
+constexpr int LDT = CB + 2;   // LDS leading dimension (doubles): conflict-free b64 reads
+constexpr int kCholThreads = 256;
+constexpr int kMaxBatch = 8;
+
+struct CholArgs {
+  // input: either a float32 matrix A (per batch at A + b*strideA) ...
+  const float* A; int64_t lda, strideA;
+  // ... or Kuu built from Z (float64 arithmetic): Kuu = var exp(-0.5 |(zi-zj)/l|^2) + jitter I
+  const float* Z[kMaxBatch]; const float* var[kMaxBatch]; const float* ls[kMaxBatch];
+  int n_ls[kMaxBatch]; int64_t ldz; int D; double jitter;
+  float* L; float* LinvT; int64_t ldl, strideL;   // L may be NULL
+  int32_t* info;
+  double* ws; int64_t strideWS;                   // per batch: W, B [Mp][Mp], D [nb][64][64]
+  int64_t M, Mp; int nb;
+};
+
+__device__ __forceinline__ double* ws_W(const CholArgs& a, int b) { return a.ws + (int64_t)b * a.strideWS; }
+__device__ __forceinline__ double* ws_B(const CholArgs& a, int b) { return ws_W(a, b) + a.Mp * a.Mp; }
+__device__ __forceinline__ double* ws_D(const CholArgs& a, int b, int j) {
+  return ws_W(a, b) + 2 * a.Mp * a.Mp + (int64_t)j * CB * CB;
+}
+
+// Element (gr, gc) of the padded input matrix, in float64.
+__device__ __forceinline__ double input_elem(const CholArgs& a, int b, int64_t gr, int64_t gc) {
+  if (gr >= a.M || gc >= a.M) return gr == gc ? 1.0 : 0.0;
+  if (a.A) return (double)a.A[(int64_t)b * a.strideA + gr * a.lda + gc];
+  const float* Z = a.Z[b];
+  const float* ls = a.ls[b];
+  double s = 0.0;
+  for (int d = 0; d < a.D; ++d) {
+    const double l = (double)ls[a.n_ls[b] == 1 ? 0 : d];
+    const double diff = ((double)Z[gr * a.ldz + d] - (double)Z[gc * a.ldz + d]) / l;
+    s = fma(diff, diff, s);
+  }
+  double v = (double)a.var[b][0] * exp(-0.5 * s);
+  if (gr == gc) v += a.jitter;
+  return v;
+}
+
+// 64x64 tile (row-major f64, ld) -> LDS (ld LDT).
+__device__ __forceinline__ void tile_load(double* __restrict__ s, const double* __restrict__ g, int64_t ld) {
+  for (int idx = threadIdx.x; idx < CB * CB / 2; idx += kCholThreads) {
+    const int r = idx >> 5, c = (idx & 31) * 2;
+    const double2 v = *reinterpret_cast<const double2*>(g + (int64_t)r * ld + c);
+    s[r * LDT + c] = v.x;
+    s[r * LDT + c + 1] = v.y;
+  }
+}
+
+// LDS tile -> float32 global, optionally transposed (dst[c][r] = s[r][c]),
+// guarded to rows < nr, cols < nc of the destination block.
+__device__ __forceinline__ void tile_store_f32(float* __restrict__ g, int64_t ld, const double* __restrict__ s,
+                                               bool transpose, int nr, int nc) {
+  for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+    const int r = idx >> 6, c = idx & 63;
+    if (r < nr && c < nc) g[(int64_t)r * ld + c] = (float)(transpose ? s[c * LDT + r] : s[r * LDT + c]);
+  }
+}
+
+__device__ __forceinline__ void tile_store_f64(double* __restrict__ g, int64_t ld, const double* __restrict__ s) {
+  for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+    const int r = idx >> 6, c = idx & 63;
+    g[(int64_t)r * ld + c] = s[r * LDT + c];
+  }
+}
+
+// Wave quadrant (32x32 of the 64x64 tile) as 2x2 accumulators of the f64
+// 16x16x4 MFMA.  Lane l supplies A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15];
+// result register r holds D[row = (l >> 4) + 4 r][col = l & 15].
+struct Quad {
+  doublex4 c[2][2];
+};
+
+__device__ __forceinline__ Quad quad_zero() {
+  Quad q;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) q.c[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+  return q;
+}
+
+// q += sign * opA(sa) . opB(sb); opA(X)[i][k] = TA ? X[k][i] : X[i][k]; opB(X)[k][j] = TB ? X[j][k] : X[k][j].
+template <bool TA, bool TB>
+__device__ __forceinline__ void tile_mma(Quad& q, const double* __restrict__ sa, const double* __restrict__ sb,
+                                         double sign) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qi = (w >> 1) * 32, qj = (w & 1) * 32;
+  const int l16 = lane & 15, kq = lane >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+    const int k = k0 + kq;
+    double a[2], b[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int i = qi + 16 * t + l16, j = qj + 16 * t + l16;
+      a[t] = sign * (TA ? sa[k * LDT + i] : sa[i * LDT + k]);
+      b[t] = TB ? sb[j * LDT + k] : sb[k * LDT + j];
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+        q.c[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], q.c[ti][tj], 0, 0, 0);
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void quad_foreach(F f) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qi = (w >> 1) * 32, qj = (w & 1) * 32;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) f(ti, tj, r, qi + 16 * ti + (lane >> 4) + 4 * r, qj + 16 * tj + (lane & 15));
+}
+
+__device__ __forceinline__ void quad_to_lds(double* __restrict__ s, const Quad& q) {
+  quad_foreach([&](int ti, int tj, int r, int row, int col) { s[row * LDT + col] = q.c[ti][tj][r]; });
+}
+__device__ __forceinline__ void quad_from_global(Quad& q, const double* __restrict__ g, int64_t ld) {
+  quad_foreach([&](int ti, int tj, int r, int row, int col) { q.c[ti][tj][r] = g[(int64_t)row * ld + col]; });
+}
+__device__ __forceinline__ void quad_to_global(double* __restrict__ g, int64_t ld, const Quad& q) {
+  quad_foreach([&](int ti, int tj, int r, int row, int col) { g[(int64_t)row * ld + col] = q.c[ti][tj][r]; });
+}
+
+// Factor the symmetric 64x64 tile in sF (lower part used) in place: sF <- L
+// (zeros above), sX <- L^-1.  Wave 0 only (lane r owns row r for the factor,
+// column r for the inverse).  Records the first non-positive pivot.
+__device__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX, double* __restrict__ col,
+                                 int32_t* info, int64_t gcol0) {
+  if (threadIdx.x >= 64) return;
+  const int r = threadIdx.x;
+  double a[CB];
+#pragma unroll
+  for (int t = 0; t < CB; ++t) a[t] = sF[r * LDT + t];
+  int bad = 0;
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const double piv = __shfl(a[c], c, 64);
+    if (!(piv > 0.0) && bad == 0) bad = c + 1;
+    const double d = sqrt(piv);
+    const double lc = (r > c) ? a[c] / d : (r == c ? d : 0.0);
+    a[c] = lc;
+    col[r] = lc;
+#pragma unroll
+    for (int s = c + 1; s < CB; ++s) a[s] = fma(-lc, col[s], a[s]);
+  }
+  if (bad && r == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
+#pragma unroll
+  for (int t = 0; t < CB; ++t) sF[r * LDT + t] = (t <= r) ? a[t] : 0.0;
+  // inverse: lane c owns column c of X = L^-1 (forward substitution over rows)
+  const int c = r;
+  double x[CB];
+#pragma unroll
+  for (int i = 0; i < CB; ++i) {
+    double s = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int t = 0; t < i; ++t) s = fma(-sF[i * LDT + t], x[t], s);
+    x[i] = s / sF[i * LDT + i];
+  }
+#pragma unroll
+  for (int i = 0; i < CB; ++i) sX[i * LDT + c] = x[i];
+}
+
+// Write the factored diagonal tile j: L block (f32, guarded to M; optional) and D_j (f64).
+__device__ void write_diag(const CholArgs& a, int b, int j, const double* sF, const double* sX) {
+  const int64_t g0 = (int64_t)j * CB;
+  const int nr = (int)min<int64_t>(CB, a.M - g0);
+  if (a.L) tile_store_f32(a.L + (int64_t)b * a.strideL + g0 * a.ldl + g0, a.ldl, sF, false, nr, nr);
+  tile_store_f64(ws_D(a, b, j), CB, sX);
+}
+
+// ------------------------------------------------------------------ prep launch
+__global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
+  __shared__ double s1[CB * LDT], s2[CB * LDT], col[CB];
+  const int b = blockIdx.y;
+  const int ntiles = a.nb * a.nb;
+  if ((int)blockIdx.x == ntiles) {  // factor tile (0, 0) straight from the input
+    if (threadIdx.x == 0) a.info[b] = 0;
+    for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+      const int r = idx >> 6, c = idx & 63;
+      s1[r * LDT + c] = input_elem(a, b, r, c);
+    }
+    __syncthreads();
+    factor_diag_tile(s1, s2, col, a.info + b, 0);
+    __syncthreads();
+    write_diag(a, b, 0, s1, s2);
+    return;
+  }
+  const int bi = blockIdx.x / a.nb, bl = blockIdx.x % a.nb;
+  const int64_t r0 = (int64_t)bi * CB, c0 = (int64_t)bl * CB;
+  if (bl <= bi) {
+    double* W = ws_W(a, b) + r0 * a.Mp + c0;
+    for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+      const int r = idx >> 6, c = idx & 63;
+      W[(int64_t)r * a.Mp + c] = input_elem(a, b, r0 + r, c0 + c);
+    }
+  }
+  // zero L above / LinvT below the block diagonal (within M x M)
+  if (bl != bi && (bl < bi || a.L)) {
+    float* dst = (bl > bi ? a.L : a.LinvT) + (int64_t)b * a.strideL;
+    for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+      const int r = idx >> 6, c = idx & 63;
+      const int64_t gr = r0 + r, gc = c0 + c;
+      if (gr < a.M && gc < a.M) dst[gr * a.ldl + gc] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ step launch j
+__global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
+  __shared__ double s1[CB * LDT], s2[CB * LDT], sD[CB * LDT], col[CB];
+  const int b = blockIdx.y;
+  const int T = a.nb - j - 1;
+  const int nU = T * (T + 1) / 2;
+  const int idx = blockIdx.x;
+  double* W = ws_W(a, b);
+  double* Bm = ws_B(a, b);
+  float* LinvT = a.LinvT + (int64_t)b * a.strideL;
+  const int64_t Mp = a.Mp;
+  auto Wt = [&](int bi, int bl) { return W + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
+  auto Bt = [&](int bi, int bl) { return Bm + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
+  auto store_linvT = [&](int c, const double* sx) {  // X_jc -> LinvT block (c, j)
+    const int64_t gr = (int64_t)c * CB, gc = (int64_t)j * CB;
+    tile_store_f32(LinvT + gr * a.ldl + gc, a.ldl, sx, true, (int)min<int64_t>(CB, a.M - gr),
+                   (int)min<int64_t>(CB, a.M - gc));
+  };
+
+  if (T == 0) {  // last step: row block j of X only
+    const int c = idx;
+    tile_load(sD, ws_D(a, b, j), CB);
+    if (c < j) tile_load(s1, Bt(j, c), Mp);
+    __syncthreads();
+    if (c < j) {
+      Quad x = quad_zero();
+      tile_mma<false, false>(x, sD, s1, 1.0);
+      __syncthreads();
+      quad_to_lds(s1, x);
+      __syncthreads();
+      store_linvT(c, s1);
+    } else {
+      store_linvT(c, sD);
+    }
+    return;
+  }
+
+  if (idx < nU) {  // ---------------- trailing update tile (i, l), j < l <= i
+    int ai = 0;
+    while ((ai + 1) * (ai + 2) / 2 <= idx) ++ai;
+    const int bl_ = idx - ai * (ai + 1) / 2;
+    const int i = j + 1 + ai, l = j + 1 + bl_;
+    tile_load(s1, Wt(i, j), Mp);
+    tile_load(sD, ws_D(a, b, j), CB);
+    if (l != i) tile_load(s2, Wt(l, j), Mp);
+    __syncthreads();
+    Quad pi = quad_zero(), pl = quad_zero();
+    tile_mma<false, true>(pi, s1, sD, 1.0);                 // P_i = W_ij D_j^T
+    if (l != i) tile_mma<false, true>(pl, s2, sD, 1.0);     // P_l
+    __syncthreads();
+    quad_to_lds(s1, pi);
+    if (l != i) quad_to_lds(s2, pl);
+    __syncthreads();
+    if (l == i && a.L) {
+      const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
+      tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
+                     (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
+    }
+    Quad u;
+    quad_from_global(u, Wt(i, l), Mp);
+    tile_mma<false, true>(u, s1, (l == i) ? s1 : s2, -1.0);  // W_il -= P_i P_l^T
+    if (ai == 0 && bl_ == 0) {  // look-ahead: factor the next diagonal tile
+      __syncthreads();
+      quad_to_lds(s1, u);
+      __syncthreads();
+      factor_diag_tile(s1, s2, col, a.info + b, (int64_t)(j + 1) * CB);
+      __syncthreads();
+      write_diag(a, b, j + 1, s1, s2);
+    } else {
+      quad_to_global(Wt(i, l), Mp, u);
+    }
+    return;
+  }
+
+  // ------------------ forward-substitution tile (i, c), i > j, c <= j
+  const int x = idx - nU;
+  const int i = j + 1 + x / (j + 1), c = x % (j + 1);
+  tile_load(s1, Wt(i, j), Mp);
+  tile_load(sD, ws_D(a, b, j), CB);
+  if (c < j) tile_load(s2, Bt(j, c), Mp);
+  __syncthreads();
+  Quad pi = quad_zero(), xq = quad_zero();
+  tile_mma<false, true>(pi, s1, sD, 1.0);                   // P_i
+  if (c < j) tile_mma<false, false>(xq, sD, s2, 1.0);       // X_jc = D_j B_jc
+  __syncthreads();
+  quad_to_lds(s1, pi);
+  if (c < j) quad_to_lds(s2, xq);
+  __syncthreads();
+  const double* sx = (c < j) ? s2 : sD;                     // X_jj = D_j
+  if (i == j + 1) store_linvT(c, sx);
+  Quad u = quad_zero();
+  if (c < j) quad_from_global(u, Bt(i, c), Mp);
+  tile_mma<false, false>(u, s1, sx, -1.0);                  // B_ic -= P_i X_jc
+  quad_to_global(Bt(i, c), Mp, u);
+}
+
+}  // namespace mgp
+
+using namespace mgp;
+
+static int64_t chol_mp(int64_t M) { return (M + CB - 1) / CB * CB; }
+static int64_t chol_ws_doubles_per_batch(int64_t M) {
+  const int64_t Mp = chol_mp(M);
+  return 2 * Mp * Mp + (Mp / CB) * CB * CB;
+}
+
+extern "C" size_t mgp_chol_workspace_bytes(int64_t M, int32_t batch) {
+  if (M <= 0 || batch <= 0) return 0;
+  return (size_t)chol_ws_doubles_per_batch(M) * (size_t)batch * sizeof(double);
+}
+
+static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  if (!workspace || workspace_bytes < mgp_chol_workspace_bytes(a.M, batch)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(workspace)) return MGP_ERR_ALIGN;
+  a.Mp = chol_mp(a.M);
+  a.nb = (int)(a.Mp / CB);
+  a.strideWS = chol_ws_doubles_per_batch(a.M);
+  a.ws = (double*)workspace;
+  const dim3 block(kCholThreads);
+  hipLaunchKernelGGL(chol_prep, dim3(a.nb * a.nb + 1, batch), block, 0, s, a);
+  int st = launch_status();
+  if (st) return st;
+  for (int j = 0; j < a.nb; ++j) {
+    const int T = a.nb - j - 1;
+    const int n = (T == 0) ? a.nb : T * (T + 1) / 2 + T * (j + 1);
+    hipLaunchKernelGGL(chol_step, dim3(n, batch), block, 0, s, a, j);
+    st = launch_status();
+    if (st) return st;
+  }
+  return MGP_OK;
+}
+
+extern "C" int mgp_potrf_trtri(const float* A, int64_t lda, int64_t strideA, int64_t M, int32_t batch,
+                               float* L, float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                               void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  if (!A) return -1;
+  if (lda < M) return -2;
+  if (batch > 1 && strideA < lda * M) return -3;
+  if (M < 0) return -4;
+  if (batch < 0) return -5;
+  if (!LinvT) return -7;
+  if (ldl < M) return -8;
+  if (batch > 1 && strideL < ldl * M) return -9;
+  if (!info) return -10;
+  if (M == 0 || batch == 0) return MGP_OK;
+  CholArgs a = {};
+  a.A = A; a.lda = lda; a.strideA = strideA;
+  a.L = L; a.LinvT = LinvT; a.ldl = ldl; a.strideL = strideL;
+  a.info = info; a.M = M;
+  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                                   const float* const* variance, const float* const* lengthscales,
+                                   const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                                   float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                                   void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  if (!Z) return -1;
+  if (ldz < D) return -2;
+  if (M < 0) return -3;
+  if (D < 1) return -4;
+  if (!variance) return -5;
+  if (!lengthscales) return -6;
+  if (!n_ls) return -7;
+  if (!(jitter >= 0.f)) return -8;
+  if (batch < 0 || batch > kMaxBatch) return -9;
+  if (!LinvT) return -11;
+  if (ldl < M) return -12;
+  if (batch > 1 && strideL < ldl * M) return -13;
+  if (!info) return -14;
+  if (M == 0 || batch == 0) return MGP_OK;
+  CholArgs a = {};
+  for (int b = 0; b < batch; ++b) {
+    if (!Z[b] || !variance[b] || !lengthscales[b]) return -1;
+    if (n_ls[b] != 1 && n_ls[b] != D) return -7;
+    a.Z[b] = Z[b]; a.var[b] = variance[b]; a.ls[b] = lengthscales[b]; a.n_ls[b] = n_ls[b];
+  }
+  a.ldz = ldz; a.D = D; a.jitter = (double)jitter;
+  a.L = L; a.LinvT = LinvT; a.ldl = ldl; a.strideL = strideL;
+  a.info = info; a.M = M;
+  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream);
+}

@@ -1,0 +1,495 @@
+// K6 / K7 and the small epilogues of the SMGP ELBO.
+//
+// K6  mgp_elbo_terms: the Monte-Carlo data term.  Reference:
+//       SMGP.W_dist (models.py:55-61), reparameterize (utils.py:26-27),
+//       RelaxedOneHotCategorical(1e-2).sample (models.py:60,73-74; TFP 0.18
+//       ExpRelaxedOneHotCategorical._sample_n + Exp bijector),
+//       GaussianModified._variational_expectations (likelihoods.py:39-41) via
+//       BroadcastingLikelihood (broadcasting_lik.py:23-24,39-42),
+//       E_log_p_Y (models.py:63-67) and the batch mean (models.py:76).
+//     One thread per data point n: the K expert var-exps are S-invariant and
+//     computed once; the S samples are a running (online) logsumexp, so
+//     neither W [S,N,K] nor the logits are ever materialised.  Noise is drawn
+//     in-register from Philox4x32-10 keyed by the GLOBAL index (shard
+//     invariant) or read from explicit arrays (parity mode).
+//     Reduction: wave shuffles -> one partial per workgroup -> one-block
+//     double-precision final sum (deterministic, no atomics).
+// K7  mgp_gauss_kl_white: GPflow gauss_kl(q_mu, q_sqrt) whitened (models.py:79),
+//     a streaming reduction over the packed lower triangle of each L_k.
+#include <math.h>
+
+#include "mgp_common.hpp"
+
+namespace mgp {
+
+constexpr int kElboThreads = 256;
+
+template <int KMAX>
+__global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
+    const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
+    const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
+    const float* __restrict__ lik_var, int64_t N, int K, int S, float inv_tau,
+    const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
+    uint32_t key1, int64_t n_offset, double* __restrict__ partials) {
+  __shared__ double scratch[16];
+  const int64_t n = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
+  float val = 0.f;
+  if (n < N) {
+    const float kHalfLog2Pi = 0.91893853320467274f;
+    float ve[KMAX], ma[KMAX], sa[KMAX];
+    const float y = Y[n];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        const float s2 = lik_var[k];
+        const float d = y - mu_f[(int64_t)k * ldf + n];
+        ve[k] = -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + n]) / s2;
+        ma[k] = mu_a[(int64_t)k * ldf + n];
+        sa[k] = sqrtf(var_a[(int64_t)k * ldf + n] + 1e-6f);
+      } else {
+        ve[k] = 0.f; ma[k] = 0.f; sa[k] = 0.f;
+      }
+    }
+    const uint32_t ng = (uint32_t)(n + n_offset);
+    float run_max = -INFINITY, run_sum = 0.f;
+    for (int s = 0; s < S; ++s) {
+      float z[KMAX], u[KMAX];
+      if (noise_z != nullptr) {
+        const float* pz = noise_z + ((int64_t)s * N + n) * K;
+        const float* pu = noise_u + ((int64_t)s * N + n) * K;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+          z[k] = (k < K) ? pz[k] : 0.f;
+          u[k] = (k < K) ? pu[k] : 0.5f;
+        }
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < (KMAX + 3) / 4; ++kb) {
+          if (4 * kb >= K) break;
+          const u32x4 wz = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 0u}, key0, key1);
+          const u32x4 wu = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 1u}, key0, key1);
+          float zz[4];
+          box_muller4(wz, zz);
+          const uint32_t uw[4] = {wu.x, wu.y, wu.z, wu.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (4 * kb + e < KMAX) {
+              z[4 * kb + e] = zz[e];
+              u[4 * kb + e] = u01(uw[e]);
+            }
+          }
+        }
+      }
+      float x[KMAX], xm = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {
+          const float g = -logf(-logf(u[k]));
+          x[k] = (g + fmaf(z[k], sa[k], ma[k])) * inv_tau;
+          xm = fmaxf(xm, x[k]);
+        }
+      }
+      float den = 0.f, num = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {
+          const float e = __expf(x[k] - xm);
+          den += e;
+          num = fmaf(e, ve[k], num);
+        }
+      }
+      const float l = num / den;
+      if (l > run_max) {
+        run_sum = run_sum * __expf(run_max - l) + 1.f;
+        run_max = l;
+      } else {
+        run_sum += __expf(l - run_max);
+      }
+    }
+    val = run_max + logf(run_sum) - logf((float)S);
+  }
+  const double bs = block_sum<double>((double)val, scratch);
+  if (threadIdx.x == 0) partials[blockIdx.x] = bs;
+}
+
+__global__ __launch_bounds__(1024) void sum_partials_kernel(const double* __restrict__ p, int n,
+                                                            double* __restrict__ out) {
+  __shared__ double scratch[16];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) v += p[i];
+  v = block_sum<double>(v, scratch);
+  if (threadIdx.x == 0) *out = v;
+}
+
+// ------------------------------------------------------------------ K7
+constexpr int kKlRows = 16;
+
+__global__ __launch_bounds__(256) void kl_partials_kernel(const float* __restrict__ q_mu, int64_t ldq,
+                                                          const float* __restrict__ q_sqrt,
+                                                          int64_t ldqs, int64_t strideq, int64_t M,
+                                                          int K, int nRowBlocks,
+                                                          double* __restrict__ partials) {
+  __shared__ double scratch[16];
+  const int blk = blockIdx.x;
+  float tr = 0.f, ld = 0.f, mh = 0.f;
+  if (blk < K * nRowBlocks) {
+    const int k = blk / nRowBlocks;
+    const int64_t r0 = (int64_t)(blk % nRowBlocks) * kKlRows;
+    const float* L = q_sqrt + (int64_t)k * strideq;
+    for (int64_t i = r0; i < r0 + kKlRows && i < M; ++i) {
+      const float* row = L + i * ldqs;
+      for (int64_t j = threadIdx.x; j <= i; j += blockDim.x) {
+        const float v = row[j];
+        tr = fmaf(v, v, tr);
+        if (j == i) ld += logf(v * v);
+      }
+    }
+  } else {  // the last block: Mahalanobis term sum q_mu^2
+    for (int64_t idx = threadIdx.x; idx < M * K; idx += blockDim.x) {
+      const float v = q_mu[(idx / K) * ldq + (idx % K)];
+      mh = fmaf(v, v, mh);
+    }
+  }
+  const double a = block_sum<double>((double)tr, scratch);
+  const double b = block_sum<double>((double)ld, scratch);
+  const double c = block_sum<double>((double)mh, scratch);
+  if (threadIdx.x == 0) {
+    partials[3 * blk + 0] = a;
+    partials[3 * blk + 1] = b;
+    partials[3 * blk + 2] = c;
+  }
+}
+
+__global__ __launch_bounds__(1024) void kl_final_kernel(const double* __restrict__ p, int nblk,
+                                                        double MK, double* __restrict__ out) {
+  __shared__ double scratch[16];
+  double tr = 0.0, ld = 0.0, mh = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+    tr += p[3 * i];
+    ld += p[3 * i + 1];
+    mh += p[3 * i + 2];
+  }
+  tr = block_sum<double>(tr, scratch);
+  ld = block_sum<double>(ld, scratch);
+  mh = block_sum<double>(mh, scratch);
+  if (threadIdx.x == 0) *out = 0.5 * (mh - MK - ld + tr);
+}
+
+__global__ void elbo_combine_kernel(const double* data_sum, const double* kl_f, const double* kl_a,
+                                    double n_batch, double num_data, float* out, double* out64) {
+  const double e = *data_sum / n_batch - (*kl_f + *kl_a) / num_data;
+  if (out) *out = (float)e;
+  if (out64) *out64 = e;
+}
+
+__global__ __launch_bounds__(256) void predict_epilogue_kernel(
+    const float* __restrict__ fmean, const float* __restrict__ fvar, const float* __restrict__ amean,
+    int64_t ldf, const float* __restrict__ lik_var, int64_t N, int K, float* __restrict__ y_mean,
+    float* __restrict__ y_var, float* __restrict__ assign) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  for (int k = 0; k < K; ++k) {
+    if (y_mean) y_mean[n * K + k] = fmean[(int64_t)k * ldf + n];
+    if (y_var) y_var[n * K + k] = fvar[(int64_t)k * ldf + n] + lik_var[k];
+  }
+  if (assign) {
+    float m = -INFINITY;
+    for (int k = 0; k < K; ++k) m = fmaxf(m, amean[(int64_t)k * ldf + n]);
+    float den = 0.f;
+    for (int k = 0; k < K; ++k) den += __expf(amean[(int64_t)k * ldf + n] - m);
+    for (int k = 0; k < K; ++k) assign[n * K + k] = __expf(amean[(int64_t)k * ldf + n] - m) / den;
+  }
+}
+
+__global__ __launch_bounds__(256) void philox_noise_kernel(uint32_t key0, uint32_t key1,
+                                                           int64_t n_offset, int64_t N, int K, int S,
+                                                           float* __restrict__ z,
+                                                           float* __restrict__ u) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * (int64_t)S) return;
+  const int s = (int)(idx / N);
+  const int64_t n = idx % N;
+  const uint32_t ng = (uint32_t)(n + n_offset);
+  for (int kb = 0; 4 * kb < K; ++kb) {
+    const u32x4 wz = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 0u}, key0, key1);
+    const u32x4 wu = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 1u}, key0, key1);
+    float zz[4];
+    box_muller4(wz, zz);
+    const uint32_t uw[4] = {wu.x, wu.y, wu.z, wu.w};
+    for (int e = 0; e < 4 && 4 * kb + e < K; ++e) {
+      const int64_t o = ((int64_t)s * N + n) * K + 4 * kb + e;
+      if (z) z[o] = zz[e];
+      if (u) u[o] = u01(uw[e]);
+    }
+  }
+}
+
+// SMGP.predict_samples (models.py:91-103).  One thread per (s, n).
+template <int KMAX>
+__global__ __launch_bounds__(256) void predict_samples_kernel(
+    const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
+    const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ lik_var, int64_t N, int K,
+    int S, float inv_tau, const float* __restrict__ zw_in, const float* __restrict__ uw_in,
+    const float* __restrict__ zy_in, uint32_t key0, uint32_t key1, int64_t n_offset,
+    float* __restrict__ sy, float* __restrict__ sf) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * (int64_t)S) return;
+  const int s = (int)(idx / N);
+  const int64_t n = idx % N;
+  const uint32_t ng = (uint32_t)(n + n_offset);
+  float zw[KMAX], uw[KMAX], zy[KMAX];
+  if (zw_in != nullptr) {
+    const int64_t o = ((int64_t)s * N + n) * K;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      zw[k] = (k < K) ? zw_in[o + k] : 0.f;
+      uw[k] = (k < K) ? uw_in[o + k] : 0.5f;
+      zy[k] = (k < K) ? zy_in[o + k] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int kb = 0; kb < (KMAX + 3) / 4; ++kb) {
+      if (4 * kb >= K) break;
+      const u32x4 a = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 0u}, key0, key1);
+      const u32x4 b = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 1u}, key0, key1);
+      const u32x4 c = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 2u}, key0, key1);
+      float za[4], zc[4];
+      box_muller4(a, za);
+      box_muller4(c, zc);
+      const uint32_t bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * kb + e < KMAX) {
+          zw[4 * kb + e] = za[e];
+          uw[4 * kb + e] = u01(bw[e]);
+          zy[4 * kb + e] = zc[e];
+        }
+    }
+  }
+  float x[KMAX], xm = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < K) {
+      const float logit = fmaf(zw[k], sqrtf(var_a[(int64_t)k * ldf + n] + 1e-6f), mu_a[(int64_t)k * ldf + n]);
+      x[k] = (-logf(-logf(uw[k])) + logit) * inv_tau;
+      xm = fmaxf(xm, x[k]);
+    }
+  float den = 0.f, ay = 0.f, af = 0.f;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < K) {
+      const float e = __expf(x[k] - xm);
+      const float m = mu_f[(int64_t)k * ldf + n], v = var_f[(int64_t)k * ldf + n];
+      den += e;
+      ay = fmaf(e, fmaf(zy[k], sqrtf(v + lik_var[k] + 1e-6f), m), ay);
+      af = fmaf(e, fmaf(zy[k], sqrtf(v + 1e-6f), m), af);
+    }
+  if (sy) sy[(int64_t)s * N + n] = ay / den;
+  if (sf) sf[(int64_t)s * N + n] = af / den;
+}
+
+__global__ __launch_bounds__(256) void philox_normal2_kernel(uint32_t key0, uint32_t key1,
+                                                             int64_t n_offset, int64_t N, int K,
+                                                             int S, float* __restrict__ z) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * (int64_t)S) return;
+  const int s = (int)(idx / N);
+  const int64_t n = idx % N;
+  for (int kb = 0; 4 * kb < K; ++kb) {
+    const u32x4 w = philox4x32_10(u32x4{(uint32_t)(n + n_offset), (uint32_t)s, (uint32_t)kb, 2u}, key0, key1);
+    float zz[4];
+    box_muller4(w, zz);
+    for (int e = 0; e < 4 && 4 * kb + e < K; ++e) z[((int64_t)s * N + n) * K + 4 * kb + e] = zz[e];
+  }
+}
+
+}  // namespace mgp
+
+using namespace mgp;
+
+extern "C" int mgp_predict_samples(const float* mu_f, const float* var_f, const float* mu_a,
+                                   const float* var_a, int64_t ldf, const float* lik_var, int64_t N,
+                                   int32_t K, int32_t S, float tau, const float* noise_zw,
+                                   const float* noise_uw, const float* noise_zy, uint64_t seed,
+                                   int64_t n_offset, float* samples_y, float* samples_f,
+                                   mgp_stream_t stream) {
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (!mu_a) return -3;
+  if (!var_a) return -4;
+  if (ldf < N) return -5;
+  if (!lik_var) return -6;
+  if (N < 0) return -7;
+  if (K < 1) return -8;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -9;
+  if (!(tau > 0.f)) return -10;
+  const bool any = noise_zw || noise_uw || noise_zy, all = noise_zw && noise_uw && noise_zy;
+  if (any && !all) return -11;
+  if (n_offset < 0) return -15;
+  if (N == 0) return MGP_OK;
+  const int64_t total = N * (int64_t)S;
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+#define MGP_PS_CASE(KM)                                                                              \
+  if (K <= KM) {                                                                                      \
+    hipLaunchKernelGGL(predict_samples_kernel<KM>, grid, block, 0, s, mu_f, var_f, mu_a, var_a, ldf,  \
+                       lik_var, N, K, S, 1.f / tau, noise_zw, noise_uw, noise_zy, k0, k1, n_offset,   \
+                       samples_y, samples_f);                                                         \
+  } else
+  MGP_PS_CASE(4) MGP_PS_CASE(8) MGP_PS_CASE(16) MGP_PS_CASE(32) {}
+#undef MGP_PS_CASE
+  return launch_status();
+}
+
+extern "C" int mgp_philox_normal2(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S,
+                                  float* z, mgp_stream_t stream) {
+  if (n_offset < 0) return -2;
+  if (N < 0) return -3;
+  if (K < 1) return -4;
+  if (S < 1) return -5;
+  if (!z) return -6;
+  if (N == 0) return MGP_OK;
+  const int64_t total = N * (int64_t)S;
+  hipLaunchKernelGGL(philox_normal2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32),
+                     n_offset, N, K, S, z);
+  return launch_status();
+}
+
+static int64_t elbo_blocks(int64_t N) { return (N + kElboThreads - 1) / kElboThreads; }
+
+extern "C" size_t mgp_elbo_workspace_bytes(int64_t N) {
+  return (size_t)(elbo_blocks(N) > 0 ? elbo_blocks(N) : 1) * sizeof(double);
+}
+
+extern "C" int mgp_elbo_terms(const float* mu_f, const float* var_f, const float* mu_a,
+                              const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
+                              int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
+                              const float* noise_u, uint64_t seed, int64_t n_offset,
+                              double* data_sum, void* workspace, size_t workspace_bytes,
+                              mgp_stream_t stream) {
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (!mu_a) return -3;
+  if (!var_a) return -4;
+  if (ldf < N) return -5;
+  if (!Y) return -6;
+  if (!lik_var) return -7;
+  if (N < 0) return -8;
+  if (K < 1) return -9;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -10;
+  if (!(tau > 0.f)) return -11;
+  if ((noise_z == nullptr) != (noise_u == nullptr)) return -12;
+  if (n_offset < 0) return -15;
+  if (!data_sum) return -16;
+  if (!workspace || workspace_bytes < mgp_elbo_workspace_bytes(N)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  double* partials = (double*)workspace;
+  const int nb = (int)elbo_blocks(N);
+  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+  if (nb > 0) {
+#define MGP_ELBO_CASE(KM)                                                                            \
+  if (K <= KM) {                                                                                      \
+    hipLaunchKernelGGL(elbo_terms_kernel<KM>, dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a, \
+                       var_a, ldf, Y, lik_var, N, K, S, 1.f / tau, noise_z, noise_u, k0, k1,         \
+                       n_offset, partials);                                                           \
+  } else
+    MGP_ELBO_CASE(1) MGP_ELBO_CASE(2) MGP_ELBO_CASE(4) MGP_ELBO_CASE(8) MGP_ELBO_CASE(16)
+    MGP_ELBO_CASE(32) {}
+#undef MGP_ELBO_CASE
+    int st = launch_status();
+    if (st) return st;
+  }
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, nb, data_sum);
+  return launch_status();
+}
+
+extern "C" int mgp_elbo_combine(const double* data_sum, const double* kl_f, const double* kl_a,
+                                double n_batch, double num_data, float* elbo_out, double* elbo_out64,
+                                mgp_stream_t stream) {
+  if (!data_sum) return -1;
+  if (!kl_f) return -2;
+  if (!kl_a) return -3;
+  if (!(n_batch > 0)) return -4;
+  if (!(num_data > 0)) return -5;
+  if (!elbo_out && !elbo_out64) return -6;
+  hipLaunchKernelGGL(elbo_combine_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, data_sum, kl_f,
+                     kl_a, n_batch, num_data, elbo_out, elbo_out64);
+  return launch_status();
+}
+
+static int kl_row_blocks(int64_t M) { return (int)((M + kKlRows - 1) / kKlRows); }
+
+extern "C" size_t mgp_kl_workspace_bytes(int64_t M, int32_t K) {
+  return (size_t)(K * kl_row_blocks(M) + 1) * 3 * sizeof(double);
+}
+
+extern "C" int mgp_gauss_kl_white(const float* q_mu, int64_t ldq, const float* q_sqrt, int64_t ldqs,
+                                  int64_t strideq, int64_t M, int32_t K, double* kl_out,
+                                  void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  if (!q_mu) return -1;
+  if (ldq < K) return -2;
+  if (!q_sqrt) return -3;
+  if (ldqs < M) return -4;
+  if (K > 1 && strideq < ldqs * M) return -5;
+  if (M < 1) return -6;
+  if (K < 1) return -7;
+  if (!kl_out) return -8;
+  if (!workspace || workspace_bytes < mgp_kl_workspace_bytes(M, K)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int nrb = kl_row_blocks(M);
+  const int nblk = K * nrb + 1;
+  double* p = (double*)workspace;
+  hipLaunchKernelGGL(kl_partials_kernel, dim3(nblk), dim3(256), 0, s, q_mu, ldq, q_sqrt, ldqs,
+                     strideq, M, K, nrb, p);
+  int st = launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(kl_final_kernel, dim3(1), dim3(1024), 0, s, p, nblk, (double)M * (double)K,
+                     kl_out);
+  return launch_status();
+}
+
+extern "C" int mgp_predict_epilogue(const float* fmean, const float* fvar, const float* amean,
+                                    int64_t ldf, const float* lik_var, int64_t N, int32_t K,
+                                    float* y_mean, float* y_var, float* assign, mgp_stream_t stream) {
+  if ((y_mean || y_var) && !fmean) return -1;
+  if (y_var && !fvar) return -2;
+  if (assign && !amean) return -3;
+  if (ldf < N) return -4;
+  if (y_var && !lik_var) return -5;
+  if (N < 0) return -6;
+  if (K < 1) return -7;
+  if (N == 0) return MGP_OK;
+  hipLaunchKernelGGL(predict_epilogue_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, fmean, fvar, amean, ldf, lik_var, N, K, y_mean, y_var, assign);
+  return launch_status();
+}
+
+extern "C" int mgp_philox_noise(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S,
+                                float* z, float* u, mgp_stream_t stream) {
+  if (n_offset < 0) return -2;
+  if (N < 0) return -3;
+  if (K < 1) return -4;
+  if (S < 1) return -5;
+  if (N == 0) return MGP_OK;
+  const int64_t total = N * (int64_t)S;
+  hipLaunchKernelGGL(philox_noise_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32),
+                     n_offset, N, K, S, z, u);
+  return launch_status();
+}
+
+extern "C" const char* mgp_version(void) { return "mgp_hip 0.1.0 gfx950"; }
+
+extern "C" const char* mgp_status_string(int status) {
+  if (status == MGP_OK) return "ok";
+  if (status < 0) return "invalid argument (index = -status)";
+  if (status == MGP_ERR_WORKSPACE) return "workspace missing or too small";
+  if (status == MGP_ERR_ALIGN) return "leading dimension or pointer not 16-byte aligned";
+  if (status == MGP_ERR_UNSUPPORTED) return "size outside the supported range";
+  if (status >= MGP_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(status - MGP_ERR_HIP_BASE));
+  return "unknown status";
+}

@@ -1,0 +1,109 @@
+// Shared device helpers for the gfx950 SMGP kernels (MFMA fragments, wave
+// reductions, guarded vector loads, Philox noise).  CDNA4 only: wave64,
+// f32-input MFMA v_mfma_f32_32x32x2_f32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mgp_hip.h"
+
+namespace mgp {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------ errors
+inline int hip_status(hipError_t e) { return e == hipSuccess ? MGP_OK : MGP_ERR_HIP_BASE + (int)e; }
+inline int launch_status() { return hip_status(hipGetLastError()); }
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ------------------------------------------------------------------ MFMA
+// D(32x32) += A(32x2) * B(2x32), exact f32 (fmaf chain).  Lane l supplies
+// A[i = l & 31][k = l >> 5] and B[k = l >> 5][j = l & 31].  Result register r of
+// lane l holds D[row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)][col = l & 31].
+__device__ __forceinline__ floatx16 mfma32x32x2(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ------------------------------------------------------------------ reductions
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// Block-wide sum (blockDim.x multiple of 64, <= 1024).  Result valid in thread 0.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* scratch /* >= 16 entries */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  T r = 0;
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    for (int i = 0; i < nw; ++i) r += scratch[i];
+  }
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------------ guarded loads
+// Load 4 consecutive floats of row `row` starting at column `col` (col % 4 == 0)
+// with zero fill outside [0, nrows) x [0, ncols).  Requires ld % 4 == 0 and a
+// 16-byte aligned base.
+__device__ __forceinline__ floatx4 load4_guarded(const float* __restrict__ base, int64_t ld,
+                                                 int64_t row, int64_t col, int64_t nrows,
+                                                 int64_t ncols) {
+  floatx4 v = {0.f, 0.f, 0.f, 0.f};
+  if (row < nrows) {
+    const float* p = base + row * ld + col;
+    if (col + 3 < ncols) {
+      v = *reinterpret_cast<const floatx4*>(p);
+    } else {
+      if (col + 0 < ncols) v.x = p[0];
+      if (col + 1 < ncols) v.y = p[1];
+      if (col + 2 < ncols) v.z = p[2];
+    }
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+// Salmon et al. SC'11; constants from Random123.  Must match oracle/philox.py.
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// uint32 -> (0,1): ((w >> 9) + 0.5) * 2^-23 (exact in fp32).
+__device__ __forceinline__ float u01(uint32_t w) { return ((float)(w >> 9) + 0.5f) * 1.1920928955078125e-07f; }
+
+// Four normals from one stream-0 block (Box-Muller on word pairs (x,y), (z,w)).
+__device__ __forceinline__ void box_muller4(u32x4 w, float out[4]) {
+  // Precise logf/sincosf (not the __ intrinsics): parity with the float64 oracle.
+  const float r0 = sqrtf(-2.f * logf(u01(w.x)));
+  const float r1 = sqrtf(-2.f * logf(u01(w.z)));
+  float s0, c0, s1, c1;
+  sincosf(6.283185307179586f * u01(w.y), &s0, &c0);
+  sincosf(6.283185307179586f * u01(w.w), &s1, &c1);
+  out[0] = r0 * c0;
+  out[1] = r0 * s0;
+  out[2] = r1 * c1;
+  out[3] = r1 * s1;
+}
+
+}  // namespace mgp

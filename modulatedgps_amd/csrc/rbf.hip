@@ -1,0 +1,145 @@
+// K1 / K2: RBF (SquaredExponential) covariance blocks Kuf = K(Z, X) and
+// Kuu = K(Z, Z) + jitter I.
+//
+// Reference: MixtureGPs/models.py:135 (covariances.Kuu) and :139
+// (self.kernel.K(Z, Xnew)); GPflow 2.7 SquaredExponential.K_r2(r2) =
+// var * exp(-0.5 r2), r2 = square_distance(X / l, X2 / l).
+//
+// Roofline: HBM-write bound.  Algorithmic bytes = 4 * (N*D + M*D + M*N); per
+// output element the kernel does D subtracts + D FMAs + 1 exp2, far below the
+// f32 VALU ridge.  Layout: Kuf [M][ldk] row-major (N contiguous); each thread
+// owns 4 consecutive columns (one float4 store per row), a wave writes 1 KiB
+// contiguous per row.  The scaled Z rows of the tile are staged once in LDS
+// and read as wave-uniform broadcasts.
+//
+// Numerics: direct-difference form sum_d (z_d - x_d)^2 * c_d^2 (exact symmetric,
+// never negative) instead of GPflow's |a|^2 + |b|^2 - 2ab expansion; the
+// exp(-0.5 r2) is evaluated as exp2(-r2') with c_d = sqrt(0.5 log2 e) / l_d.
+#include "mgp_common.hpp"
+
+namespace mgp {
+
+constexpr int kRbfThreads = 256;
+constexpr int kRbfCols = 4;                       // columns per thread
+constexpr int kRbfTileN = kRbfThreads * kRbfCols; // 1024 columns per workgroup
+constexpr int kRbfTileM = 16;                     // rows per workgroup
+
+template <int DMAX>
+__global__ __launch_bounds__(kRbfThreads) void rbf_kernel(
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ Z, int64_t ldz, int64_t N,
+    int64_t M, int D, const float* __restrict__ variance, const float* __restrict__ ls, int n_ls,
+    float jitter, float* __restrict__ out, int64_t ldo) {
+  __shared__ float zs[kRbfTileM][DMAX];
+  __shared__ float cs[DMAX];
+  const int t = threadIdx.x;
+  const int64_t n0 = (int64_t)blockIdx.x * kRbfTileN + (int64_t)t * kRbfCols;
+  const int64_t m0 = (int64_t)blockIdx.y * kRbfTileM;
+  const float kHalfLog2e = 0.8493218002880191f;  // sqrt(0.5 * log2(e))
+
+  if (t < DMAX) cs[t] = (t < D) ? kHalfLog2e / ls[n_ls == 1 ? 0 : t] : 0.f;
+  __syncthreads();
+  for (int i = t; i < kRbfTileM * DMAX; i += kRbfThreads) {
+    const int r = i / DMAX, d = i % DMAX;
+    const int64_t m = m0 + r;
+    zs[r][d] = (m < M && d < D) ? Z[m * ldz + d] * cs[d] : 0.f;
+  }
+  float xs[kRbfCols][DMAX];
+#pragma unroll
+  for (int j = 0; j < kRbfCols; ++j) {
+    const int64_t n = n0 + j;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) xs[j][d] = (n < N && d < D) ? X[n * ldx + d] * cs[d] : 0.f;
+  }
+  const float var = variance[0];
+  __syncthreads();
+
+  const int rows = (int)((M - m0) < kRbfTileM ? (M - m0) : kRbfTileM);
+  for (int r = 0; r < rows; ++r) {
+    const int64_t m = m0 + r;
+    float v[kRbfCols];
+#pragma unroll
+    for (int j = 0; j < kRbfCols; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        const float diff = zs[r][d] - xs[j][d];
+        acc = fmaf(diff, diff, acc);
+      }
+      v[j] = var * exp2f(-acc);
+      if (jitter != 0.f && m == n0 + j) v[j] += jitter;
+    }
+    float* o = out + m * ldo + n0;
+    if (n0 + kRbfCols <= N) {
+      *reinterpret_cast<floatx4*>(o) = floatx4{v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < kRbfCols; ++j)
+        if (n0 + j < N) o[j] = v[j];
+    }
+  }
+}
+
+static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                      int D, const float* variance, const float* ls, int n_ls, float jitter, float* out,
+                      int64_t ldo, hipStream_t stream) {
+  if (N <= 0 || M <= 0) return MGP_OK;
+  dim3 grid((unsigned)((N + kRbfTileN - 1) / kRbfTileN), (unsigned)((M + kRbfTileM - 1) / kRbfTileM));
+  dim3 block(kRbfThreads);
+#define MGP_RBF_CASE(DM)                                                                            \
+  if (D <= DM) {                                                                                     \
+    hipLaunchKernelGGL(rbf_kernel<DM>, grid, block, 0, stream, X, ldx, Z, ldz, N, M, D, variance, ls, \
+                       n_ls, jitter, out, ldo);                                                      \
+    return launch_status();                                                                          \
+  }
+  MGP_RBF_CASE(1)
+  MGP_RBF_CASE(2)
+  MGP_RBF_CASE(4)
+  MGP_RBF_CASE(8)
+  MGP_RBF_CASE(16)
+  MGP_RBF_CASE(32)
+#undef MGP_RBF_CASE
+  return MGP_ERR_UNSUPPORTED;
+}
+
+}  // namespace mgp
+
+using namespace mgp;
+
+extern "C" int mgp_rbf_kuf(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N,
+                           int64_t M, int32_t D, const float* variance, const float* lengthscales,
+                           int32_t n_ls, float* Kuf, int64_t ldk, mgp_stream_t stream) {
+  if (!X) return -1;
+  if (ldx < D) return -2;
+  if (!Z) return -3;
+  if (ldz < D) return -4;
+  if (N < 0) return -5;
+  if (M < 0) return -6;
+  if (D < 1) return -7;
+  if (D > 32) return MGP_ERR_UNSUPPORTED;
+  if (!variance) return -8;
+  if (!lengthscales) return -9;
+  if (n_ls != 1 && n_ls != D) return -10;
+  if (!Kuf) return -11;
+  if (ldk < N) return -12;
+  if (ldk % 4 || !aligned16(Kuf)) return MGP_ERR_ALIGN;
+  return rbf_launch(X, ldx, Z, ldz, N, M, D, variance, lengthscales, n_ls, 0.f, Kuf, ldk,
+                    (hipStream_t)stream);
+}
+
+extern "C" int mgp_rbf_kuu(const float* Z, int64_t ldz, int64_t M, int32_t D, const float* variance,
+                           const float* lengthscales, int32_t n_ls, float jitter, float* Kuu,
+                           int64_t ldk, mgp_stream_t stream) {
+  if (!Z) return -1;
+  if (ldz < D) return -2;
+  if (M < 0) return -3;
+  if (D < 1) return -4;
+  if (D > 32) return MGP_ERR_UNSUPPORTED;
+  if (!variance) return -5;
+  if (!lengthscales) return -6;
+  if (n_ls != 1 && n_ls != D) return -7;
+  if (!Kuu) return -9;
+  if (ldk < M) return -10;
+  if (ldk % 4 || !aligned16(Kuu)) return MGP_ERR_ALIGN;
+  return rbf_launch(Z, ldz, Z, ldz, M, M, D, variance, lengthscales, n_ls, jitter, Kuu, ldk,
+                    (hipStream_t)stream);
+}

@@ -1,0 +1,344 @@
+"""SGP / SMGP / SMGPModified / SVGPModified on the MI355X kernels.
+
+Drop-in counterparts of MixtureGPs/models.py (same class names, constructor
+arguments and method names).  The SMGP ELBO hot path
+(SMGP._build_likelihood, models.py:69-79) runs as:
+
+  per layer (pred, assign):                         reference call site
+    K2 mgp_rbf_kuu          Kuu + jitter I          models.py:135
+    K3 mgp_potrf_trtri      L, L^-1 (both layers    models.py:141 (cholesky)
+                            batched in one sweep)
+    K1 mgp_rbf_kuf          Kuf [M, N]              models.py:139
+    K4 mgp_trsm_stats       A = L^-1 Kuf + stats    models.py:141-143 (triangular_solve, A^T q_mu)
+    K5 mgp_expert_conditional  fmean, fvar [K, N]   models.py:141-143 (LTA, fvar)
+    K7 mgp_gauss_kl_white   KL                      models.py:79 (prior_kl)
+  K6 mgp_elbo_terms         sum_n lse_s(...)        models.py:55-67,73-76
+  mgp_elbo_combine          ELBO scalar             models.py:76,79
+
+The reference evaluates every conditional on S tiled copies of X
+(SGP.integrate, models.py:35-36); the copies are identical, so the conditional
+is computed once per data point and S only enters the Monte-Carlo term.
+Outputs that the reference returns with a leading S axis (predict_f on tiled
+inputs, predict_y) are returned as broadcast views of that single result.
+
+Compute dtype is float32 on the device; the parity tolerances against the
+float64 reference semantics are stated in tests/.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from .broadcasting_lik import BroadcastingLikelihood
+from .config import default_device, default_jitter
+from .kernels import SquaredExponential
+
+TAU = 1e-2  # RelaxedOneHotCategorical temperature, models.py:60
+
+
+def _splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+def _to_dev(x, device, dtype=torch.float32):
+    t = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x)
+    return t.to(device=device, dtype=dtype)
+
+
+class SVGPModified:
+    """Whitened SVGP layer with K latent GPs sharing one kernel and one Z
+    (GPflow SVGP(kernel, likelihood, Z, num_latent_gps=K, whiten=True) with the
+    posterior plugin IndependentPosteriorSingleOutputModified, models.py:126-160).
+
+    Variational state: q_mu [M, K] (init zeros) and q_sqrt [K, M, M] lower
+    triangular (init identity), as GPflow's SVGP initialises them."""
+
+    def __init__(self, kernel, likelihood, inducing_variable, num_latent_gps=1, whiten=True,
+                 q_mu=None, q_sqrt=None, q_diag=False, mean_function=None, device=None):
+        if not whiten:
+            raise NotImplementedError("only the whitened SVGP (whiten=True) is on the hot path")
+        if q_diag:
+            raise NotImplementedError("q_diag=True is not used by the reference models")
+        if mean_function is not None:
+            raise NotImplementedError("the reference layers use the Zero mean function")
+        if not isinstance(kernel, SquaredExponential):
+            raise TypeError("kernel must be modulatedgps_amd.kernels.SquaredExponential")
+        self.device = torch.device(device or kernel.device or default_device())
+        self.kernel = kernel
+        self.likelihood = likelihood
+        self.whiten = True
+        Z = _to_dev(inducing_variable, self.device)
+        if Z.dim() == 1:
+            Z = Z[:, None]
+        self.Z = Z.contiguous()
+        M = self.Z.shape[0]
+        self.num_latent_gps = int(num_latent_gps)
+        K = self.num_latent_gps
+        self.q_mu = torch.zeros(M, K, dtype=torch.float32, device=self.device)
+        self.q_sqrt = ops.padded(M, M, self.device, batch=K, zero=True)
+        self.q_sqrt.copy_(torch.eye(M, device=self.device).expand(K, M, M))
+        if q_mu is not None or q_sqrt is not None:
+            self.set_variational(q_mu if q_mu is not None else self.q_mu,
+                                 q_sqrt if q_sqrt is not None else self.q_sqrt)
+
+    # ------------------------------------------------------------------ state
+    @property
+    def inducing_variable(self):
+        return self.Z
+
+    @property
+    def num_inducing(self):
+        return self.Z.shape[0]
+
+    def set_variational(self, q_mu, q_sqrt):
+        """Set q_mu [M, K] and q_sqrt [K, M, M] (band_part(-1, 0) is applied)."""
+        q_mu = _to_dev(q_mu, self.device)
+        q_sqrt = _to_dev(q_sqrt, self.device)
+        M, K = self.num_inducing, self.num_latent_gps
+        if tuple(q_mu.shape) != (M, K) or tuple(q_sqrt.shape) != (K, M, M):
+            raise ValueError(f"expected q_mu [{M},{K}] and q_sqrt [{K},{M},{M}]")
+        self.q_mu.copy_(q_mu)
+        self.q_sqrt.copy_(torch.tril(q_sqrt))
+
+    def parameters(self):
+        return {"Z": self.Z, "q_mu": self.q_mu, "q_sqrt": self.q_sqrt, **self.kernel.parameters()}
+
+    # ------------------------------------------------------------------ ops
+    def Kuu(self, out=None):
+        return ops.rbf_kuu(self.Z, self.kernel.variance, self.kernel.lengthscales, default_jitter(),
+                           out=out)
+
+    def factorise(self, want_L=False):
+        """Kuu (float64) -> L, (L^-1)^T (float32 [1, M, M]) and info (models.py:135,141)."""
+        return ops.kuu_potrf_trtri([self.Z], [self.kernel.variance], [self.kernel.lengthscales],
+                                   default_jitter(), want_L=want_L)
+
+    def prior_kl(self, out=None):
+        """GPflow SVGP.prior_kl -> gauss_kl(q_mu, q_sqrt) whitened (models.py:79); float64 [1]."""
+        return ops.gauss_kl_white(self.q_mu, self.q_sqrt, out=out)
+
+    def conditional_kn(self, X, LinvT=None, bufs=None):
+        """Whitened conditional for X [N, D]: fmean, fvar as expert-major [K, N] views.
+
+        LinvT: (L^-1)^T of this layer's Kuu if already factorised (the SMGP
+        factorises both layers in one batched sweep)."""
+        X = self.kernel._x(X)
+        if LinvT is None:
+            _, LinvT, info = self.factorise()
+            self._last_info = info
+            LinvT = LinvT[0]
+        bufs = bufs or {}
+        Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
+                          out=bufs.get("Kuf"))
+        A, stats = ops.trsm_stats(LinvT, Kuf, self.q_mu, A=bufs.get("A"), stats=bufs.get("stats"))
+        return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
+                                      fmean=bufs.get("fmean"), fvar=bufs.get("fvar"))
+
+    def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
+        """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior
+        (models.py:129-144).  Xnew [..., N, D] -> mean, var [..., N, K]."""
+        if full_cov or full_output_cov:
+            raise NotImplementedError("full_cov predictions are not used by the SMGP path")
+        X = self.kernel._x(Xnew)
+        lead = X.shape[:-2]
+        Xf = X.reshape(-1, X.shape[-1])
+        if len(lead) and X.shape[0] > 1 and bool(torch.equal(X, X[:1].expand_as(X))):
+            Xf = X.reshape(-1, *X.shape[-2:])[0]            # tiled copies (SGP.integrate)
+            fm, fv = self.conditional_kn(Xf)
+            shape = (*lead, Xf.shape[0], self.num_latent_gps)
+            return fm.t().expand(shape), fv.t().expand(shape)
+        fm, fv = self.conditional_kn(Xf)
+        shape = (*lead, X.shape[-2], self.num_latent_gps)
+        return fm.t().reshape(shape), fv.t().reshape(shape)
+
+
+class SGP:
+    """Scalable GP: X -> Xt = integrate(X) -> GP -> Y (models.py:23-41)."""
+
+    def __init__(self, likelihood, pred_layer, num_samples=1, num_data=None):
+        self.num_samples = int(num_samples)
+        self.num_data = num_data
+        self.likelihood = BroadcastingLikelihood(likelihood)
+        self.pred_layer = pred_layer
+
+    def integrate(self, X, S=1):
+        """models.py:35-36 (kept for API parity; the hot path never tiles)."""
+        X = torch.as_tensor(X)
+        return X[None].expand(S, *X.shape), None
+
+    def predict_y(self, Xnew, S=1):
+        """models.py:38-41 -> (mean, var) [S, N, K] (S broadcast copies)."""
+        lik = self.likelihood.likelihood
+        X = self.pred_layer.kernel._x(Xnew)
+        fm, fv = self.pred_layer.conditional_kn(X)
+        ym, yv, _ = ops.predict_epilogue(fm, fv, None, lik.variance.reshape(-1), want_y=True)
+        return ym[None].expand(S, *ym.shape), yv[None].expand(S, *yv.shape)
+
+
+class SMGP(SGP):
+    """Mixture of Gaussian processes (models.py:44-103)."""
+
+    def __init__(self, likelihood, pred_layer, assign_layer, K=3, num_samples=1, num_data=None,
+                 seed=0):
+        SGP.__init__(self, likelihood, pred_layer, num_samples, num_data)
+        self.assign_layer = assign_layer
+        self.K = int(K)
+        if pred_layer.num_latent_gps != self.K or assign_layer.num_latent_gps != self.K:
+            raise ValueError("both layers must have num_latent_gps == K")
+        self.device = pred_layer.device
+        self.seed = int(seed)
+        self._draws = 0
+        self._bufs = {}
+        self.last_info = None
+
+    # ------------------------------------------------------------------ internals
+    def _buffers(self, N):
+        key = N
+        b = self._bufs.get(key)
+        if b is not None:
+            return b
+        dev = self.device
+        Mf, Ma, K = self.pred_layer.num_inducing, self.assign_layer.num_inducing, self.K
+        Mx = max(Mf, Ma)
+        T = ops.stats_tiles(Mx)
+        kuf = ops.padded(Mx, N, dev)
+        a = ops.padded(Mx, N, dev)
+        st = ops.padded(T * (K + 1), N, dev)
+        cond = ops.padded(4 * K, N, dev)          # mu_f, var_f, mu_a, var_a
+        b = {
+            "Kuf_f": kuf[:Mf], "Kuf_a": kuf[:Ma], "A_f": a[:Mf], "A_a": a[:Ma],
+            "stats_f": st[:ops.stats_tiles(Mf) * (K + 1)].unflatten(0, (-1, K + 1)),
+            "stats_a": st[:ops.stats_tiles(Ma) * (K + 1)].unflatten(0, (-1, K + 1)),
+            "mu_f": cond[0:K], "var_f": cond[K:2 * K], "mu_a": cond[2 * K:3 * K],
+            "var_a": cond[3 * K:4 * K],
+            "kl": torch.empty(2, dtype=torch.float64, device=dev),
+            "data_sum": torch.empty(1, dtype=torch.float64, device=dev),
+            "elbo": torch.empty((), dtype=torch.float32, device=dev),
+            "elbo64": torch.empty((), dtype=torch.float64, device=dev),
+        }
+        if Mf == Ma and self.pred_layer.Z.shape[1] == self.assign_layer.Z.shape[1]:
+            b["LinvT2"] = ops.padded(Mf, Mf, dev, batch=2)
+        self._bufs[key] = b
+        return b
+
+    def _factorise(self, b):
+        """Kuu of both layers and their batched Cholesky + inverse (one K3 sweep)."""
+        pf, pa = self.pred_layer, self.assign_layer
+        if "LinvT2" in b:
+            if pf.Z.stride(0) != pa.Z.stride(0):
+                pa.Z = pa.Z.contiguous()
+                pf.Z = pf.Z.contiguous()
+            _, LinvT, info = ops.kuu_potrf_trtri(
+                [pf.Z, pa.Z], [pf.kernel.variance, pa.kernel.variance],
+                [pf.kernel.lengthscales, pa.kernel.lengthscales], default_jitter(), LinvT=b["LinvT2"])
+            self.last_info = info
+            return LinvT[0], LinvT[1]
+        outs = []
+        infos = []
+        for layer in (pf, pa):
+            _, LinvT, info = layer.factorise()
+            outs.append(LinvT[0])
+            infos.append(info)
+        self.last_info = torch.cat(infos)
+        return outs[0], outs[1]
+
+    def conditionals(self, X):
+        """(mu_f, var_f, mu_a, var_a), each an expert-major [K, N] device view."""
+        X = self.pred_layer.kernel._x(X)
+        N = X.shape[0]
+        b = self._buffers(N)
+        LinvT_f, LinvT_a = self._factorise(b)
+        self.pred_layer.conditional_kn(X, LinvT_f, bufs={"Kuf": b["Kuf_f"], "A": b["A_f"],
+                                                         "stats": b["stats_f"], "fmean": b["mu_f"],
+                                                         "fvar": b["var_f"]})
+        self.assign_layer.conditional_kn(X, LinvT_a, bufs={"Kuf": b["Kuf_a"], "A": b["A_a"],
+                                                           "stats": b["stats_a"], "fmean": b["mu_a"],
+                                                           "fvar": b["var_a"]})
+        return b["mu_f"], b["var_f"], b["mu_a"], b["var_a"]
+
+    def next_seed(self):
+        """Fresh Philox key per evaluation (TF's stateful RNG advances per call)."""
+        self._draws += 1
+        return _splitmix64(self.seed * 0x100000001B3 + self._draws)
+
+    # ------------------------------------------------------------------ ELBO
+    def _build_likelihood(self, X, Y, noise=None, seed=None, n_offset=0, n_total=None,
+                          process_group=None, return64=False):
+        """ELBO (models.py:69-79) as a 0-d float32 device tensor.
+
+        noise: optional explicit (z, u) [S, N, K] device tensors (parity mode);
+        otherwise in-kernel Philox keyed by (seed, global n, s, k).
+        n_offset / n_total / process_group: data-parallel sharding over N (each
+        rank passes its shard; one all-reduce of the data-term sum)."""
+        X = self.pred_layer.kernel._x(X)
+        N = X.shape[0]
+        Yd = _to_dev(Y, self.device).reshape(-1).contiguous()
+        if Yd.numel() != N:
+            raise ValueError("X and Y must have the same number of rows")
+        b = self._buffers(N)
+        mu_f, var_f, mu_a, var_a = self.conditionals(X)
+        kl = b["kl"]
+        self.pred_layer.prior_kl(out=kl[0:1])
+        self.assign_layer.prior_kl(out=kl[1:2])
+        lik_var = self.likelihood.likelihood.variance.reshape(-1)
+        if seed is None and noise is None:
+            seed = self.next_seed()
+        ops.elbo_terms(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU, noise=noise,
+                       seed=seed or 0, n_offset=n_offset, out=b["data_sum"])
+        if process_group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(b["data_sum"], op=dist.ReduceOp.SUM, group=process_group)
+        n_batch = n_total if n_total is not None else N
+        num_data = self.num_data if self.num_data is not None else n_batch
+        ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"],
+                         out64=b["elbo64"])
+        return b["elbo64"] if return64 else b["elbo"]
+
+    def elbo(self, data, **kw):
+        X, Y = data
+        return self._build_likelihood(X, Y, **kw)
+
+    def _training_loss(self, data):
+        """models.py:81-83."""
+        X, Y = data
+        return -self._build_likelihood(X, Y)
+
+    def training_loss(self, data):
+        return self._training_loss(data)
+
+    # ------------------------------------------------------------------ predictions
+    def predict_assign(self, Xnew, S=1):
+        """models.py:85-89: softmax_K(mean_S mu_a) -> [N, K]."""
+        X = self.assign_layer.kernel._x(Xnew)
+        am, _ = self.assign_layer.conditional_kn(X)
+        _, _, asg = ops.predict_epilogue(None, None, am, None, want_y=False, want_assign=True)
+        return asg
+
+    def predict_samples(self, Xnew, S=1, noise=None, seed=None):
+        """models.py:91-103 -> samples_y, samples_f [S, N, 1]."""
+        X = self.pred_layer.kernel._x(Xnew)
+        mu_f, var_f, mu_a, var_a = self.conditionals(X)
+        if seed is None and noise is None:
+            seed = self.next_seed()
+        sy, sf = ops.predict_samples(mu_f, var_f, mu_a, var_a,
+                                     self.likelihood.likelihood.variance.reshape(-1), S, TAU,
+                                     noise=noise, seed=seed or 0)
+        return sy[..., None], sf[..., None]
+
+
+class SMGPModified(SMGP):
+    """SMGP with a second (assignment) likelihood (models.py:106-123).  Round-1
+    scope: the constructor and API exist; the fused kernel variant of its
+    E_log_p_Y is the next §8(f) item and is not implemented yet."""
+
+    def __init__(self, likelihood, assign_likelihood, pred_layer, assign_layer, K=3, num_samples=1,
+                 num_data=None, seed=0):
+        SMGP.__init__(self, likelihood, pred_layer, assign_layer, K, num_samples, num_data, seed)
+        self.assign_likelihood = BroadcastingLikelihood(assign_likelihood)
+
+    def _build_likelihood(self, *a, **kw):
+        raise NotImplementedError("SMGPModified ELBO kernel is not built yet (SURVEY §8f item 3)")

@@ -1,0 +1,321 @@
+"""Torch-tensor wrappers over the libmgp_hip C-ABI (device memory + streams only).
+
+PyTorch is used here as plumbing: it allocates device buffers and supplies the
+current HIP stream.  Every arithmetic op runs in a hand-written gfx950 kernel
+of libmgp_hip.so; nothing here computes on the CPU or with torch kernels.
+
+Layout conventions (see include/mgp_hip.h): float32, row-major, leading
+dimensions padded to a multiple of 4 elements so rows can be read as float4.
+``padded(rows, cols)`` returns such a view; the expert-major conditional
+outputs are [K][N] views.
+"""
+import torch
+
+from . import _lib
+
+F32 = torch.float32
+
+
+def _round4(x):
+    return (int(x) + 3) // 4 * 4
+
+
+def _stream():
+    return ctypes_stream(torch.cuda.current_stream())
+
+
+def ctypes_stream(s):
+    return s.cuda_stream
+
+
+def padded(rows, cols, device, batch=None, dtype=F32, zero=False):
+    """[batch?][rows][cols] view over storage whose rows are padded to a multiple of 4."""
+    ld = _round4(max(cols, 1))
+    shape = (rows, ld) if batch is None else (batch, rows, ld)
+    fn = torch.zeros if zero else torch.empty
+    buf = fn(shape, dtype=dtype, device=device)
+    return buf[..., :cols]
+
+
+def as_padded(t, device=None, dtype=F32):
+    """Copy a 2-D/3-D tensor (or array) into padded storage (unless it already is)."""
+    t = torch.as_tensor(t)
+    device = device or t.device
+    if (t.device == torch.device(device) and t.dtype == dtype and t.stride(-1) == 1
+            and t.stride(-2) % 4 == 0 and t.data_ptr() % 16 == 0
+            and (t.dim() == 2 or t.stride(0) % 4 == 0)):
+        return t
+    out = padded(t.shape[-2], t.shape[-1], device, batch=t.shape[0] if t.dim() == 3 else None,
+                 dtype=dtype)
+    out.copy_(t.to(device=device, dtype=dtype))
+    return out
+
+
+def _ld(t):
+    if t.stride(-1) != 1:
+        raise ValueError("innermost dimension must be contiguous")
+    return t.stride(-2) if t.dim() >= 2 else t.shape[-1]
+
+
+def _check(t, name, ndim=None):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if t.dtype != F32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# --------------------------------------------------------------------------- K1 / K2
+def rbf_kuf(X, Z, variance, lengthscales, out=None):
+    """Kuf = K(Z, X) [M, N] (models.py:139)."""
+    _check(X, "X", 2), _check(Z, "Z", 2), _check(variance, "variance"), _check(lengthscales, "lengthscales")
+    N, D = X.shape
+    M = Z.shape[0]
+    if Z.shape[1] != D:
+        raise ValueError("X and Z must have the same number of columns")
+    if out is None:
+        out = padded(M, N, X.device)
+    _lib.call("mgp_rbf_kuf", X.data_ptr(), _ld(X), Z.data_ptr(), _ld(Z), N, M, D,
+              variance.data_ptr(), lengthscales.data_ptr(), lengthscales.numel(), out.data_ptr(),
+              _ld(out), _stream())
+    return out
+
+
+def rbf_kuu(Z, variance, lengthscales, jitter, out=None):
+    """Kuu = K(Z, Z) + jitter I [M, M] (models.py:135)."""
+    _check(Z, "Z", 2)
+    M, D = Z.shape
+    if out is None:
+        out = padded(M, M, Z.device)
+    _lib.call("mgp_rbf_kuu", Z.data_ptr(), _ld(Z), M, D, variance.data_ptr(), lengthscales.data_ptr(),
+              lengthscales.numel(), float(jitter), out.data_ptr(), _ld(out), _stream())
+    return out
+
+
+# --------------------------------------------------------------------------- K3
+def potrf_trtri(A, L=None, LinvT=None, info=None, workspace=None):
+    """Batched Cholesky + inverse of A [B, M, M] (lower part read).
+    Returns L [B,M,M], LinvT [B,M,M] and info int32 [B] (device; 0 = success)."""
+    _check(A, "A", 3)
+    Bt, M, _ = A.shape
+    dev = A.device
+    if L is None:
+        L = padded(M, M, dev, batch=Bt)
+    if LinvT is None:
+        LinvT = padded(M, M, dev, batch=Bt)
+    if info is None:
+        info = torch.empty(Bt, dtype=torch.int32, device=dev)
+    nbytes = _lib.load().mgp_chol_workspace_bytes(M, Bt)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    if L.stride(0) != LinvT.stride(0) or _ld(L) != _ld(LinvT):
+        raise ValueError("L and LinvT must share a layout")
+    _lib.call("mgp_potrf_trtri", A.data_ptr(), _ld(A), A.stride(0), M, Bt, L.data_ptr(),
+              LinvT.data_ptr(), _ld(L), L.stride(0), info.data_ptr(), workspace.data_ptr(),
+              workspace.numel(), _stream())
+    return L, LinvT, info
+
+
+def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, info=None,
+                    workspace=None, want_L=False):
+    """Kuu (float64, from Z) + Cholesky + inverse for a batch of layers sharing M, D.
+    Zs / variances / lengthscales: lists of device tensors.  Returns L (or None),
+    LinvT [B, M, M] and info int32 [B]."""
+    import ctypes
+    Bt = len(Zs)
+    M, D = Zs[0].shape
+    ldz = _ld(Zs[0])
+    for Z in Zs:
+        _check(Z, "Z", 2)
+        if tuple(Z.shape) != (M, D) or _ld(Z) != ldz:
+            raise ValueError("all Z must share shape and leading dimension")
+    dev = Zs[0].device
+    if LinvT is None:
+        LinvT = padded(M, M, dev, batch=Bt)
+    if want_L and L is None:
+        L = padded(M, M, dev, batch=Bt)
+    if info is None:
+        info = torch.empty(Bt, dtype=torch.int32, device=dev)
+    nbytes = _lib.load().mgp_chol_workspace_bytes(M, Bt)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    P = ctypes.c_void_p * Bt
+    zp = P(*[z.data_ptr() for z in Zs])
+    vp = P(*[v.data_ptr() for v in variances])
+    lp = P(*[l.data_ptr() for l in lengthscales])
+    nl = (ctypes.c_int32 * Bt)(*[l.numel() for l in lengthscales])
+    _lib.call("mgp_kuu_potrf_trtri", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
+              L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
+              LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(), _stream())
+    return L, LinvT, info
+
+
+def check_info(info):
+    """Raise MGPLinAlgError if any factorisation reported a bad pivot (host sync)."""
+    bad = info.cpu()
+    if bool((bad != 0).any()):
+        raise _lib.MGPLinAlgError("mgp_potrf_trtri", int(bad.max()),
+                                  "Cholesky decomposition was not successful: the input might "
+                                  "not be valid (non-positive pivot at column %s)" % bad.tolist())
+
+
+# --------------------------------------------------------------------------- K4 / K5
+def stats_tiles(M):
+    return _lib.load().mgp_stats_tiles(M)
+
+
+def trsm_stats(LinvT, Kuf, q_mu, A=None, stats=None):
+    """A = L^-1 Kuf and per-row-tile column stats [T, K+1, N]."""
+    _check(LinvT, "LinvT", 2), _check(Kuf, "Kuf", 2), _check(q_mu, "q_mu", 2)
+    M, N = Kuf.shape
+    K = q_mu.shape[1]
+    dev = Kuf.device
+    if A is None:
+        A = padded(M, N, dev)
+    if stats is None:
+        T = stats_tiles(M)
+        stats = padded(T * (K + 1), N, dev).unflatten(0, (T, K + 1))
+    _lib.call("mgp_trsm_stats", LinvT.data_ptr(), _ld(LinvT), Kuf.data_ptr(), _ld(Kuf), M, N,
+              q_mu.data_ptr(), _ld(q_mu), K, A.data_ptr(), _ld(A), stats.data_ptr(), _ld(stats),
+              _stream())
+    return A, stats
+
+
+def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None):
+    """fmean, fvar [K, N] of the whitened K-expert conditional."""
+    _check(A, "A", 2), _check(q_sqrt, "q_sqrt", 3), _check(stats, "stats", 3)
+    M, N = A.shape
+    K = q_sqrt.shape[0]
+    dev = A.device
+    if fmean is None:
+        fmean = padded(K, N, dev)
+    if fvar is None:
+        fvar = padded(K, N, dev)
+    if _ld(fmean) != _ld(fvar):
+        raise ValueError("fmean and fvar must share a leading dimension")
+    _lib.call("mgp_expert_conditional", A.data_ptr(), _ld(A), q_sqrt.data_ptr(), _ld(q_sqrt),
+              q_sqrt.stride(0), stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K,
+              fmean.data_ptr(), fvar.data_ptr(), _ld(fmean), _stream())
+    return fmean, fvar
+
+
+# --------------------------------------------------------------------------- K7
+def gauss_kl_white(q_mu, q_sqrt, out=None, workspace=None):
+    """Whitened KL (models.py:79) as a float64 device tensor of shape [1]."""
+    _check(q_mu, "q_mu", 2), _check(q_sqrt, "q_sqrt", 3)
+    M, K = q_mu.shape
+    dev = q_mu.device
+    if out is None:
+        out = torch.empty(1, dtype=torch.float64, device=dev)
+    nbytes = _lib.load().mgp_kl_workspace_bytes(M, K)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    _lib.call("mgp_gauss_kl_white", q_mu.data_ptr(), _ld(q_mu), q_sqrt.data_ptr(), _ld(q_sqrt),
+              q_sqrt.stride(0), M, K, out.data_ptr(), workspace.data_ptr(), workspace.numel(),
+              _stream())
+    return out
+
+
+# --------------------------------------------------------------------------- K6
+def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0, n_offset=0,
+               out=None, workspace=None):
+    """Sum over local points of logsumexp_s(sum_k W ve) - log S (float64 [1])."""
+    for t, n in ((mu_f, "mu_f"), (var_f, "var_f"), (mu_a, "mu_a"), (var_a, "var_a")):
+        _check(t, n, 2)
+    ldf = _ld(mu_f)
+    if not (_ld(var_f) == _ld(mu_a) == _ld(var_a) == ldf):
+        raise ValueError("conditional outputs must share a leading dimension")
+    K, N = mu_f.shape
+    dev = mu_f.device
+    Y = Y.reshape(-1)
+    _check(Y, "Y"), _check(lik_var, "lik_var")
+    if Y.numel() != N or not Y.is_contiguous():
+        raise ValueError("Y must be contiguous with N elements")
+    if out is None:
+        out = torch.empty(1, dtype=torch.float64, device=dev)
+    nbytes = _lib.load().mgp_elbo_workspace_bytes(N)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    zp = up = None
+    if noise is not None:
+        z, u = noise
+        _check(z, "noise_z", 3), _check(u, "noise_u", 3)
+        if tuple(z.shape) != (S, N, K) or tuple(u.shape) != (S, N, K):
+            raise ValueError("explicit noise must be [S, N, K]")
+        z, u = z.contiguous(), u.contiguous()
+        zp, up = z.data_ptr(), u.data_ptr()
+    _lib.call("mgp_elbo_terms", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(), var_a.data_ptr(),
+              ldf, Y.data_ptr(), lik_var.data_ptr(), N, K, S, float(tau), zp, up,
+              int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(), workspace.data_ptr(),
+              workspace.numel(), _stream())
+    return out
+
+
+def elbo_combine(data_sum, kl_f, kl_a, n_batch, num_data, out=None, out64=None):
+    dev = data_sum.device
+    if out is None:
+        out = torch.empty((), dtype=F32, device=dev)
+    if out64 is None:
+        out64 = torch.empty((), dtype=torch.float64, device=dev)
+    _lib.call("mgp_elbo_combine", data_sum.data_ptr(), kl_f.data_ptr(), kl_a.data_ptr(),
+              float(n_batch), float(num_data), out.data_ptr(), out64.data_ptr(), _stream())
+    return out, out64
+
+
+def predict_epilogue(fmean, fvar, amean, lik_var, want_y=True, want_assign=False):
+    """[N, K] outputs: y mean/var (likelihoods.py:31-32) and softmax assignment."""
+    ref = fmean if fmean is not None else amean
+    K, N = ref.shape
+    dev = ref.device
+    ym = torch.empty(N, K, dtype=F32, device=dev) if want_y else None
+    yv = torch.empty(N, K, dtype=F32, device=dev) if want_y else None
+    asg = torch.empty(N, K, dtype=F32, device=dev) if want_assign else None
+    _lib.call("mgp_predict_epilogue", fmean.data_ptr() if fmean is not None else None,
+              fvar.data_ptr() if fvar is not None else None,
+              amean.data_ptr() if amean is not None else None, _ld(ref),
+              lik_var.data_ptr() if lik_var is not None else None, N, K,
+              ym.data_ptr() if ym is not None else None, yv.data_ptr() if yv is not None else None,
+              asg.data_ptr() if asg is not None else None, _stream())
+    return ym, yv, asg
+
+
+def philox_noise(seed, n_offset, N, K, S, device, want_z=True, want_u=True):
+    z = torch.empty(S, N, K, dtype=F32, device=device) if want_z else None
+    u = torch.empty(S, N, K, dtype=F32, device=device) if want_u else None
+    _lib.call("mgp_philox_noise", int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), N, K, S,
+              z.data_ptr() if z is not None else None, u.data_ptr() if u is not None else None,
+              _stream())
+    return z, u
+
+
+def philox_normal2(seed, n_offset, N, K, S, device):
+    z = torch.empty(S, N, K, dtype=F32, device=device)
+    _lib.call("mgp_philox_normal2", int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), N, K, S,
+              z.data_ptr(), _stream())
+    return z
+
+
+def predict_samples(mu_f, var_f, mu_a, var_a, lik_var, S, tau=1e-2, noise=None, seed=0,
+                    n_offset=0):
+    """samples_y, samples_f [S, N] (models.py:91-103)."""
+    K, N = mu_f.shape
+    dev = mu_f.device
+    sy = torch.empty(S, N, dtype=F32, device=dev)
+    sf = torch.empty(S, N, dtype=F32, device=dev)
+    ptrs = [None, None, None]
+    if noise is not None:
+        noise = [t.contiguous() for t in noise]
+        for t in noise:
+            _check(t, "noise", 3)
+            if tuple(t.shape) != (S, N, K):
+                raise ValueError("explicit noise must be [S, N, K]")
+        ptrs = [t.data_ptr() for t in noise]
+    _lib.call("mgp_predict_samples", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
+              var_a.data_ptr(), _ld(mu_f), lik_var.data_ptr(), N, K, S, float(tau), *ptrs,
+              int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), sy.data_ptr(), sf.data_ptr(), _stream())
+    return sy, sf

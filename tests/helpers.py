@@ -1,0 +1,53 @@
+"""Shared test helpers: build device models from oracle parameter sets."""
+import os
+
+import numpy as np
+import torch
+
+from oracle import cpu_ref as R
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load_golden(name):
+    return dict(np.load(os.path.join(GOLDEN, name)))
+
+
+def params_from_golden(d):
+    layers = {}
+    for name in ("pred", "assign"):
+        layers[name] = {k: d[f"{name}_{k}"] for k in ("Z", "variance", "lengthscales", "q_mu", "q_sqrt")}
+    return R.SMGPParams(layers["pred"], layers["assign"], d["lik_variance"], int(d["num_data"]),
+                        int(d["S"]))
+
+
+def build_model(p, device, seed=0):
+    """SMGP on the device from an oracle SMGPParams (float64 -> float32)."""
+    from modulatedgps_amd.kernels import SquaredExponential
+    from modulatedgps_amd.likelihoods import GaussianModified
+    from modulatedgps_amd.models import SMGP, SVGPModified
+
+    K = p.lik_variance.shape[1]
+    lik = GaussianModified(variance=p.lik_variance, device=device)
+    layers = []
+    for L in (p.pred, p.assign):
+        kern = SquaredExponential(variance=L["variance"], lengthscales=L["lengthscales"], device=device)
+        layer = SVGPModified(kern, lik, L["Z"], num_latent_gps=K, whiten=True, device=device)
+        layer.set_variational(L["q_mu"], L["q_sqrt"])
+        layers.append(layer)
+    return SMGP(lik, layers[0], layers[1], K=K, num_samples=p.S, num_data=p.num_data, seed=seed)
+
+
+def normwise(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def to_np(t):
+    return t.detach().double().cpu().numpy()
+
+
+def dev_noise(z, u, device):
+    return (torch.as_tensor(z, dtype=torch.float32, device=device),
+            torch.as_tensor(u, dtype=torch.float32, device=device))

@@ -1,0 +1,184 @@
+"""Per-kernel parity of libmgp_hip (via the C-ABI, through modulatedgps_amd.ops)
+against the float64 oracle.  Tolerances (fp32 kernels vs fp64 oracle):
+  Kuf/Kuu: elementwise |err| <= 2e-6 * variance
+  L, L^-1, A, conditional mean/var: normwise ||a-b||/||b|| <= 1e-4
+  KL, data term: relative 1e-5 / 1e-4
+"""
+import numpy as np
+import pytest
+import scipy.linalg as sla
+import torch
+
+from oracle import cpu_ref as R
+from oracle import philox
+from tests.helpers import normwise, to_np
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev):
+    return torch.as_tensor(np.asarray(x), dtype=torch.float32, device=dev)
+
+
+@pytest.mark.parametrize("N,M,D,ard", [(1000, 37, 1, False), (4099, 256, 2, False), (2048, 130, 8, True),
+                                       (3, 5, 16, True), (1500, 64, 3, True)])
+def test_rbf_kuf_kuu(device, N, M, D, ard):
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(N + M)
+    X = rng.standard_normal((N, D))
+    Z = rng.standard_normal((M, D))
+    ls = rng.uniform(0.5, 2.0, D) if ard else np.array([0.8])
+    var = 0.7
+    Kuf = to_np(ops.rbf_kuf(_t(X, device), _t(Z, device), _t([var], device), _t(ls, device)))
+    ref = R.rbf_K(Z, X, var, ls)
+    assert np.abs(Kuf - ref).max() <= 2e-6 * var
+    Kuu = to_np(ops.rbf_kuu(_t(Z, device), _t([var], device), _t(ls, device), 1e-6))
+    refu = R.rbf_Kuu(Z, var, ls)
+    assert np.abs(Kuu - refu).max() <= 2e-6 * var
+    assert np.array_equal(Kuu, Kuu.T)
+
+
+@pytest.mark.parametrize("M,batch", [(1, 1), (25, 2), (64, 1), (100, 2), (256, 2), (1024, 2)])
+def test_potrf_trtri(device, M, batch):
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(M)
+    As = []
+    for b in range(batch):
+        Z = rng.standard_normal((M, 4))
+        As.append(R.rbf_Kuu(Z, 1.0, 1.5) + 1e-3 * np.eye(M))
+    A = ops.padded(M, M, device, batch=batch)
+    A.copy_(torch.as_tensor(np.stack(As), dtype=torch.float32))
+    L, LinvT, info = ops.potrf_trtri(A)
+    assert (info.cpu() == 0).all()
+    for b in range(batch):
+        # fp32 forward-error bound scale: cond(L) * eps32 (cond(L) = sqrt(cond(A)))
+        tol = max(1e-5, 10 * np.sqrt(np.linalg.cond(As[b])) * 1.2e-7)
+        Lr = np.linalg.cholesky(As[b])
+        Lg = to_np(L[b])
+        assert np.array_equal(np.triu(Lg, 1), np.zeros_like(Lg))
+        assert normwise(Lg, Lr) < tol
+        Li = sla.solve_triangular(Lr, np.eye(M), lower=True)
+        Lt = to_np(LinvT[b])
+        assert np.array_equal(np.tril(Lt, -1), np.zeros_like(Lt))
+        assert normwise(Lt.T, Li) < tol
+
+
+def test_potrf_reports_non_spd(device):
+    from modulatedgps_amd import ops
+    M = 130
+    A = np.eye(M)
+    A[70, 70] = -1.0
+    At = ops.padded(M, M, device, batch=1)
+    At.copy_(torch.as_tensor(A[None], dtype=torch.float32))
+    _, _, info = ops.potrf_trtri(At)
+    assert int(info.cpu()[0]) == 71
+    with pytest.raises(Exception):
+        ops.check_info(info)
+
+
+@pytest.mark.parametrize("N,M,K,D,ls", [(1000, 25, 3, 1, 0.5), (8192, 256, 4, 2, 0.15),
+                                         (5000, 300, 5, 3, 0.7), (16384, 1024, 8, 8, 1.0),
+                                         (777, 64, 1, 2, 1.0)])
+def test_conditional(device, N, M, K, D, ls):
+    """K3 (fused float64 Kuu) + K1 + K4 + K5: whitened conditional vs GPflow
+    base_conditional semantics.  Tolerance 1e-4 normwise where cond(Kuu) < 1e6;
+    above that the float32 rounding of L^-1 alone costs ~cond(L) eps32 and the
+    bound is 5e-4 (the float32-input floor measured on the CPU)."""
+    from modulatedgps_amd import ops
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
+    L = p.pred
+    mu_ref, var_ref = R.svgp_predict_f_dedup(X, L["Z"], L["variance"], L["lengthscales"], L["q_mu"], L["q_sqrt"])
+    tol = 1e-4 if np.linalg.cond(R.rbf_Kuu(L["Z"], L["variance"], ls)) < 1e6 else 5e-4
+    _, LinvT, info = ops.kuu_potrf_trtri([_t(L["Z"], device)], [_t([L["variance"]], device)],
+                                         [_t([ls], device)], 1e-6)
+    assert int(info.cpu()[0]) == 0
+    Kuf = ops.rbf_kuf(_t(X, device), _t(L["Z"], device), _t([L["variance"]], device), _t([ls], device))
+    A, stats = ops.trsm_stats(LinvT[0], Kuf, _t(L["q_mu"], device))
+    qs = ops.as_padded(_t(L["q_sqrt"], device))
+    fm, fv = ops.expert_conditional(A, qs, stats, _t([L["variance"]], device))
+    assert normwise(to_np(fm).T, mu_ref) < tol
+    assert normwise(to_np(fv).T, var_ref) < tol
+
+
+def test_kuu_factorisation_matches_float64(device):
+    """Fused float64 Kuu + Cholesky + inverse: L and L^-1 to float32 rounding."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(0)
+    Zs = [rng.standard_normal((300, 3)), rng.standard_normal((300, 3))]
+    var, ls = [0.5, 0.1], [np.array([0.7]), np.array([0.5, 1.0, 1.5])]
+    L, LinvT, info = ops.kuu_potrf_trtri([_t(z, device) for z in Zs], [_t([v], device) for v in var],
+                                         [_t(l, device) for l in ls], 1e-6, want_L=True)
+    assert (info.cpu() == 0).all()
+    for b in range(2):
+        Lr = np.linalg.cholesky(R.rbf_Kuu(Zs[b].astype(np.float32), var[b], ls[b]))
+        Li = sla.solve_triangular(Lr, np.eye(300), lower=True)
+        assert normwise(to_np(L[b]), Lr) < 1e-6
+        assert normwise(to_np(LinvT[b]).T, Li) < 1e-6
+
+
+def test_conditional_ignores_upper_triangle(device):
+    """band_part(q_sqrt, -1, 0): garbage above the diagonal must not matter."""
+    from modulatedgps_amd import ops
+    N, M, K = 600, 40, 2
+    X, Y, p = R.synthetic_problem(N, M, K, 2, 0.6, state="perturbed", S=2)
+    L = p.pred
+    Kuu = ops.rbf_kuu(_t(L["Z"], device), _t([0.5], device), _t([0.6], device), 1e-6)
+    _, LinvT, _ = ops.potrf_trtri(Kuu.unsqueeze(0))
+    Kuf = ops.rbf_kuf(_t(X, device), _t(L["Z"], device), _t([0.5], device), _t([0.6], device))
+    A, st = ops.trsm_stats(LinvT[0], Kuf, _t(L["q_mu"], device))
+    q1 = ops.as_padded(_t(np.tril(L["q_sqrt"]), device))
+    junk = np.tril(L["q_sqrt"]) + np.triu(np.random.default_rng(0).standard_normal((K, M, M)), 1)
+    q2 = ops.as_padded(_t(junk, device))
+    a = ops.expert_conditional(A, q1, st, _t([0.5], device))[1]
+    b = ops.expert_conditional(A, q2, st, _t([0.5], device))[1]
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,K", [(25, 3), (256, 4), (1024, 8), (1, 1)])
+def test_gauss_kl(device, M, K):
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(M)
+    q_mu = 0.5 * rng.standard_normal((M, K))
+    q_sqrt = 0.5 * np.eye(M) + np.tril(0.1 * rng.standard_normal((K, M, M)))
+    kl = float(ops.gauss_kl_white(_t(q_mu, device), ops.as_padded(_t(q_sqrt, device))).cpu())
+    ref = R.gauss_kl_white(q_mu.astype(np.float32), q_sqrt.astype(np.float32))
+    assert kl == pytest.approx(ref, rel=1e-5)
+
+
+def test_philox_stream_bitexact(device):
+    """The device noise stream equals oracle/philox.py (uniforms bit-exact, normals ~1 ulp)."""
+    from modulatedgps_amd import ops
+    seed, S, N, K = 0x1234ABCD9876, 3, 1000, 7
+    z, u = ops.philox_noise(seed, 500, N, K, S, device)
+    uref = philox.noise_uniform(seed, S, np.arange(500, 500 + N), K)
+    zref = philox.noise_normal(seed, S, np.arange(500, 500 + N), K)
+    assert np.array_equal(to_np(u), uref.astype(np.float32).astype(np.float64))
+    assert np.abs(to_np(z) - zref).max() < 2e-5
+    z2 = ops.philox_normal2(seed, 500, N, K, S, device)
+    assert np.abs(to_np(z2) - philox.noise_normal(seed, S, np.arange(500, 500 + N), K, stream=2)).max() < 2e-5
+
+
+@pytest.mark.parametrize("N,K,S", [(1000, 3, 25), (4097, 8, 5), (300, 1, 4), (513, 16, 2)])
+def test_elbo_terms_explicit_and_philox(device, N, K, S):
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(N)
+    mu_f, mu_a = rng.standard_normal((2, N, K))
+    var_f, var_a = rng.uniform(0.05, 1.0, (2, N, K))
+    Y = rng.standard_normal((N, 1))
+    lv = rng.uniform(0.2, 1.0, (1, K))
+    z, u = R.explicit_noise(S, N, K, seed=3)
+
+    def ref(z, u):
+        W = R.assignment_weights(mu_a[None], var_a[None], z, u)
+        return np.sum(R.e_log_p_y(mu_f[None], var_f[None], Y, lv, W, S))
+
+    dev = lambda a: ops.as_padded(_t(a.T, device))
+    args = (dev(mu_f), dev(var_f), dev(mu_a), dev(var_a), _t(Y[:, 0], device), _t(lv[0], device), S)
+    out = float(ops.elbo_terms(*args, noise=(_t(z, device), _t(u, device))).cpu())
+    r = ref(z, u)
+    assert out == pytest.approx(r, rel=1e-4, abs=1e-3)
+    seed = 99
+    out2 = float(ops.elbo_terms(*args, seed=seed).cpu())
+    n = np.arange(N)
+    r2 = ref(philox.noise_normal(seed, S, n, K), philox.noise_uniform(seed, S, n, K))
+    assert out2 == pytest.approx(r2, rel=1e-4, abs=1e-3)

@@ -1,0 +1,42 @@
+"""CPU tests of the C-ABI boundary: libmgp_hip.so loads without a GPU and exports
+every function declared in include/mgp_hip.h (no compute calls are made)."""
+import ctypes
+
+import pytest
+
+from modulatedgps_amd import _lib
+
+
+def test_library_loads_and_reports_gfx950():
+    lib = _lib.load()
+    assert lib.mgp_version().decode().endswith("gfx950")
+
+
+def test_exports_every_header_symbol():
+    syms = _lib.header_symbols()
+    assert len(syms) >= 18
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in syms if not hasattr(raw, s)]
+    assert not missing, missing
+
+
+def test_binding_table_matches_header():
+    assert sorted(_lib.SIGNATURES) == _lib.header_symbols()
+
+
+def test_status_strings_and_argument_checks():
+    lib = _lib.load()
+    assert lib.mgp_status_string(0) == b"ok"
+    assert b"workspace" in lib.mgp_status_string(1)
+    # invalid arguments are rejected before any HIP call (safe without a GPU)
+    assert lib.mgp_rbf_kuf(None, 1, None, 1, 10, 10, 1, None, None, 1, None, 12, None) == -1
+    assert lib.mgp_trsm_stats(None, 0, None, 0, 4, 4, None, 0, 1, None, 0, None, 0, None) == -1
+    assert lib.mgp_chol_workspace_bytes(1024, 2) == 2 * (2 * 1024 * 1024 + 16 * 64 * 64) * 8
+    assert lib.mgp_stats_tiles(1024) == 8
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    with pytest.raises(_lib.MGPLibraryError):
+        _lib.load()
