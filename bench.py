@@ -1,0 +1,255 @@
+#!/usr/bin/env python
+"""Benchmark of the SMGP ELBO hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one full SMGP ELBO evaluation (SMGP._build_likelihood,
+MixtureGPs/models.py:69-79: both SVGP layers, S = 25 Monte-Carlo samples,
+both KLs) over one batch of synthetic input already resident in HBM, with
+fresh in-kernel Philox noise per step.  Workload (N = 1): BASELINE config 3,
+N = 65536, M = 1024, K = 8, D = 8, fp32, per GPU.  Multi-GPU: data-parallel
+over N with weak scaling (every rank holds its own 65536-point shard of the
+global batch; Kuu/Cholesky/KL replicated; ONE RCCL all-reduce of the data-term
+scalar per step).  `value` = ELBO steps/s in units of config-3 evaluations,
+i.e. world_size * steps / max-over-ranks wall time.
+
+Rank 0 prints ONE JSON line (see README/DESIGN for the fields).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (N per GPU, M, K, D, lengthscale, S)
+    "c2": (8192, 256, 4, 2, 0.15, 25),
+    "c3": (65536, 1024, 8, 8, 1.0, 25),
+    "c5": (262144, 2048, 16, 16, 2.0, 25),
+}
+PEAK_F32_MFMA = 157.3e12      # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_F64 = 78.6e12            # FP64 vector/matrix (half the f32 rate)
+PEAK_HBM = 8.0e12             # HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, nargs=2, default=(2048, 4096),
+                    help="two N sizes of the CPU oracle sample (linear fit in N)")
+    return ap.parse_args()
+
+
+def synthetic(cfg, rank, device):
+    """SURVEY §8(d) synthetic inputs: X ~ N(0, I_D) (per-rank shard), multimodal Y,
+    Z = a random subset of rank-0 X, perturbed variational state (seeded)."""
+    N, M, K, D, ls, S = cfg
+    rng = np.random.default_rng(1000 + rank)
+    X = rng.standard_normal((N, D)).astype(np.float32)
+    w = np.random.default_rng(1).standard_normal((K, D)) / np.sqrt(D)
+    c = np.arange(N) % K
+    Y = (np.sin(np.sum(w[c] * X, 1) + c) + 0.1 * rng.standard_normal(N)).astype(np.float32)
+    X0 = np.random.default_rng(1000).standard_normal((N, D)).astype(np.float32)
+    Zf = X0[np.random.default_rng(2).choice(N, M, replace=False)]
+    Za = X0[np.random.default_rng(3).choice(N, M, replace=False)]
+    r4 = np.random.default_rng(4)
+    layers = []
+    for Z, var in ((Zf, 0.5), (Za, 0.1)):
+        q_mu = (0.5 * r4.standard_normal((M, K))).astype(np.float32)
+        q_sqrt = np.empty((K, M, M), np.float32)
+        for k in range(K):
+            q_sqrt[k] = 0.5 * np.eye(M, dtype=np.float32) + np.tril(
+                0.1 * r4.standard_normal((M, M)).astype(np.float32))
+        layers.append((Z, var, q_mu, q_sqrt))
+    return X, Y, layers
+
+
+def build_model(cfg, layers, device, num_data):
+    from MixtureGPs.likelihoods import GaussianModified
+    from MixtureGPs.models import SMGP, SVGPModified
+    from modulatedgps_amd.kernels import SquaredExponential
+    N, M, K, D, ls, S = cfg
+    lik = GaussianModified(variance=0.5, D=K, device=device)
+    svgp = []
+    for Z, var, q_mu, q_sqrt in layers:
+        kern = SquaredExponential(variance=var, lengthscales=ls, device=device)
+        layer = SVGPModified(kernel=kern, likelihood=lik, inducing_variable=Z, num_latent_gps=K,
+                             whiten=True, device=device)
+        layer.set_variational(torch.from_numpy(q_mu), torch.from_numpy(q_sqrt))
+        svgp.append(layer)
+    return SMGP(likelihood=lik, pred_layer=svgp[0], assign_layer=svgp[1], K=K, num_samples=S,
+                num_data=num_data, seed=1234)
+
+
+def stage_stats(timing):
+    """{stage: (avg ms per launch, launches)} from recorded HIP event pairs."""
+    out = {}
+    for name, pairs in timing.items():
+        ts = [a.elapsed_time(b) for a, b in pairs]
+        out[name] = (float(np.mean(ts)), len(ts))
+    return out
+
+
+def cpu_baseline(cfg, sizes):
+    """Float64 oracle (oracle/cpu_ref.py, S-deduplicated restatement of the reference
+    semantics) timed on this host's cores on a bounded sample: config shapes with N
+    reduced to `sizes`, t(N) = a + b N fitted and extrapolated to the full N."""
+    from oracle import cpu_ref as R
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count()
+    Nfull, M, K, D, ls, S = cfg
+    ts = []
+    for n in sizes:
+        X, Y, p = R.synthetic_problem(n, M, K, D, ls, state="perturbed", S=S)
+        z, u = R.explicit_noise(S, n, K)
+        R.smgp_elbo(X[:256], Y[:256], p, z[:, :256], u[:, :256])   # warm BLAS
+        t0 = time.perf_counter()
+        R.smgp_elbo(X, Y, p, z, u)
+        ts.append(time.perf_counter() - t0)
+    b = (ts[1] - ts[0]) / (sizes[1] - sizes[0])
+    a = max(ts[0] - b * sizes[0], 0.0)
+    t_full = a + b * Nfull
+    return {"value": 1.0 / t_full, "unit": "ELBO steps/s", "cores": int(cores), "kind": "port",
+            "sample": (f"float64 oracle (oracle/cpu_ref.py; reference semantics, S-deduplicated, "
+                       f"TF2 unavailable) at M={M},K={K},D={D},S={S} with N={sizes[0]} "
+                       f"({ts[0]:.2f}s) and N={sizes[1]} ({ts[1]:.2f}s), t = a + b N "
+                       f"extrapolated to N={Nfull}: {t_full:.2f}s per ELBO"),
+            "seconds_per_step": t_full}
+
+
+def load_traffic(kernel):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    e = d.get(kernel)
+    if not e:
+        return None, None
+    return e.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+    device = torch.device("cuda", local if world > 1 else 0)
+    cfg = CONFIGS[args.config]
+    N, M, K, D, ls, S = cfg
+    X_np, Y_np, layers = synthetic(cfg, rank, device)
+    n_total = N * world
+    model = build_model(cfg, layers, device, num_data=n_total)
+    X = torch.from_numpy(X_np).to(device)
+    Y = torch.from_numpy(Y_np).to(device)
+    kw = dict(n_offset=rank * N, n_total=n_total, process_group=group)
+
+    for _ in range(args.warmup):
+        model._build_likelihood(X, Y, **kw)
+    torch.cuda.synchronize()
+    timing = {}
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        elbo = model._build_likelihood(X, Y, timing=timing, **kw)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    elbo_val = float(elbo.item())
+    info = model.last_info.cpu().tolist()
+    st = stage_stats(timing)
+
+    # algorithmic work per launch
+    kuf_bytes = 4.0 * (N * D + M * D + M * N)
+    trsm_flops = float(M) * M * N
+    expert_flops = float(K) * M * M * N
+    chol_flops = 2 * (2.0 * M ** 3 / 3.0)        # potrf + trtri, both layers (one batched sweep)
+    kernels = {}
+    if "rbf_kuf" in st:
+        ms = st["rbf_kuf"][0]
+        kernels["rbf_kuf"] = {"bound": "hbm", "avg_us": ms * 1e3, "bytes": kuf_bytes,
+                              "achieved": kuf_bytes / (ms * 1e-3) / 1e9, "unit": "GB/s",
+                              "peak": PEAK_HBM / 1e9, "frac": kuf_bytes / (ms * 1e-3) / PEAK_HBM}
+    for name, fl in (("trsm_stats", trsm_flops), ("expert_cond", expert_flops)):
+        if name in st:
+            ms = st[name][0]
+            kernels[name] = {"bound": "mfma", "avg_us": ms * 1e3, "flops": fl,
+                             "achieved": fl / (ms * 1e-3) / 1e12, "unit": "TFLOP/s",
+                             "peak": PEAK_F32_MFMA / 1e12, "frac": fl / (ms * 1e-3) / PEAK_F32_MFMA}
+    if "kuu_chol" in st:
+        ms = st["kuu_chol"][0]
+        kernels["kuu_chol"] = {"bound": "latency", "avg_us": ms * 1e3, "flops": chol_flops,
+                               "achieved": chol_flops / (ms * 1e-3) / 1e12, "unit": "TFLOP/s",
+                               "peak": PEAK_F64 / 1e12, "frac": chol_flops / (ms * 1e-3) / PEAK_F64}
+    for name in ("elbo_terms", "gauss_kl", "allreduce"):
+        if name in st:
+            kernels[name] = {"avg_us": st[name][0] * 1e3}
+
+    ek = kernels.get("expert_cond", {})
+    traffic, traffic_src = load_traffic("expert_cond_kernel")
+    roofline = {"kernel": "expert_cond_kernel (K5, L_k^T A + sum of squares)", "bound": "mfma",
+                "achieved": ek.get("achieved"), "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
+                "frac": ek.get("frac"), "traffic": traffic, "traffic_source": traffic_src,
+                "algorithmic_per_launch": f"K*M^2*N = {expert_flops:.4g} flop"}
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * args.steps / elapsed
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, tuple(args.cpu_sample))
+    step_flops = 2 * (2.0 * M ** 3 / 3.0 + (K + 1.0) * M * M * N + N * M * (3 * D + 4.0))
+    if rank == 0:
+        out = {
+            "metric": "ELBO steps/sec (N=65536, M=1024, K=8); Kuf HBM GB/s vs roofline",
+            "value": value, "unit": "ELBO steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: SMGP ELBO forward, N={N}/GPU, M={M}, K={K}, "
+                                   f"D={D}, S={S}, lengthscale={ls}",
+                       "global_batch": n_total, "N_per_gpu": N, "M": M, "K": K, "D": D, "S": S,
+                       "parallelism": f"dp{world} (N-sharded, scalar RCCL all-reduce)"},
+            "roofline": roofline,
+            "kernels": kernels,
+            "kuf_hbm": kernels.get("rbf_kuf"),
+            "step_tflops": step_flops / (ms_per_step * 1e-3) / 1e12,
+            "step_frac_f32_mfma": step_flops / (ms_per_step * 1e-3) / PEAK_F32_MFMA,
+            "cpu_baseline": cpu,
+            "elbo": elbo_val, "cholesky_info": info,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

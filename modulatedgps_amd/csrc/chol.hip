@@ -61,15 +61,20 @@ __device__ __forceinline__ double* ws_D(const CholArgs& a, int b, int j) {
 __device__ __forceinline__ double input_elem(const CholArgs& a, int b, int64_t gr, int64_t gc) {
   if (gr >= a.M || gc >= a.M) return gr == gc ? 1.0 : 0.0;
   if (a.A) return (double)a.A[(int64_t)b * a.strideA + gr * a.lda + gc];
-  const float* Z = a.Z[b];
-  const float* ls = a.ls[b];
+  // select this batch entry without dynamic indexing of the by-value argument
+  // arrays (that would copy the whole struct to scratch)
+  const float *Z = a.Z[0], *ls = a.ls[0], *var = a.var[0];
+  int nls = a.n_ls[0];
+#pragma unroll
+  for (int i = 1; i < kMaxBatch; ++i)
+    if (b == i) { Z = a.Z[i]; ls = a.ls[i]; var = a.var[i]; nls = a.n_ls[i]; }
   double s = 0.0;
   for (int d = 0; d < a.D; ++d) {
-    const double l = (double)ls[a.n_ls[b] == 1 ? 0 : d];
+    const double l = (double)ls[nls == 1 ? 0 : d];
     const double diff = ((double)Z[gr * a.ldz + d] - (double)Z[gc * a.ldz + d]) / l;
     s = fma(diff, diff, s);
   }
-  double v = (double)a.var[b][0] * exp(-0.5 * s);
+  double v = (double)var[0] * exp(-0.5 * s);
   if (gr == gc) v += a.jitter;
   return v;
 }
@@ -164,47 +169,68 @@ __device__ __forceinline__ void quad_to_global(double* __restrict__ g, int64_t l
   quad_foreach([&](int ti, int tj, int r, int row, int col) { g[(int64_t)row * ld + col] = q.c[ti][tj][r]; });
 }
 
+// Diagonal-tile factorisation: wave 0, lane r owns row r; the tile is walked in
+// four 16-column panels (left-looking): each panel is first updated with the
+// finished panels (L[r][k] L[s][k], k < 16J), then factored column by column
+// with in-register shuffles.  Only 16 doubles per lane are live (no scratch).
+template <int J>
+__device__ __forceinline__ void chol_panel(double* __restrict__ sF, int r, int& bad) {
+  constexpr int C0 = 16 * J;
+  double a[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) a[t] = sF[r * LDT + C0 + t];
+#pragma unroll 4
+  for (int k = 0; k < C0; ++k) {
+    const double lrk = sF[r * LDT + k];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) a[t] = fma(-lrk, sF[(C0 + t) * LDT + k], a[t]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double piv = __shfl(a[c], C0 + c, 64);
+    if (!(piv > 0.0) && bad == 0) bad = C0 + c + 1;
+    const double d = sqrt(piv);
+    const double lc = (r > C0 + c) ? a[c] / d : (r == C0 + c ? d : 0.0);
+    a[c] = lc;
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      if (s2 > c) a[s2] = fma(-lc, __shfl(lc, C0 + s2, 64), a[s2]);
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) sF[r * LDT + C0 + t] = (C0 + t <= r) ? a[t] : 0.0;
+}
+
+// Inverse row I: lane c owns column c of X = L^-1 in x[0..63]; row I of L is
+// read from LDS (wave-uniform address -> broadcast).
+template <int I>
+__device__ __forceinline__ void inv_row(double (&x)[CB], const double* __restrict__ sL, int c) {
+  double s = (I == c) ? 1.0 : 0.0;
+#pragma unroll
+  for (int t = 0; t < I; ++t) s = fma(-sL[I * LDT + t], x[t], s);
+  x[I] = s / sL[I * LDT + I];
+  if constexpr (I + 1 < CB) inv_row<I + 1>(x, sL, c);
+}
+
 // Factor the symmetric 64x64 tile in sF (lower part used) in place: sF <- L
-// (zeros above), sX <- L^-1.  Wave 0 only (lane r owns row r for the factor,
-// column r for the inverse).  Records the first non-positive pivot.
-__device__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX, double* __restrict__ col,
+// (zeros above), sX <- L^-1.  Wave 0 only.  Records the first non-positive pivot.
+__device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX, double* __restrict__ col,
                                  int32_t* info, int64_t gcol0) {
   if (threadIdx.x >= 64) return;
   const int r = threadIdx.x;
-  double a[CB];
-#pragma unroll
-  for (int t = 0; t < CB; ++t) a[t] = sF[r * LDT + t];
   int bad = 0;
-#pragma unroll
-  for (int c = 0; c < CB; ++c) {
-    const double piv = __shfl(a[c], c, 64);
-    if (!(piv > 0.0) && bad == 0) bad = c + 1;
-    const double d = sqrt(piv);
-    const double lc = (r > c) ? a[c] / d : (r == c ? d : 0.0);
-    a[c] = lc;
-    col[r] = lc;
-#pragma unroll
-    for (int s = c + 1; s < CB; ++s) a[s] = fma(-lc, col[s], a[s]);
-  }
+  chol_panel<0>(sF, r, bad);
+  chol_panel<1>(sF, r, bad);
+  chol_panel<2>(sF, r, bad);
+  chol_panel<3>(sF, r, bad);
   if (bad && r == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
-#pragma unroll
-  for (int t = 0; t < CB; ++t) sF[r * LDT + t] = (t <= r) ? a[t] : 0.0;
-  // inverse: lane c owns column c of X = L^-1 (forward substitution over rows)
-  const int c = r;
   double x[CB];
+  inv_row<0>(x, sF, r);
 #pragma unroll
-  for (int i = 0; i < CB; ++i) {
-    double s = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-    for (int t = 0; t < i; ++t) s = fma(-sF[i * LDT + t], x[t], s);
-    x[i] = s / sF[i * LDT + i];
-  }
-#pragma unroll
-  for (int i = 0; i < CB; ++i) sX[i * LDT + c] = x[i];
+  for (int i = 0; i < CB; ++i) sX[i * LDT + r] = x[i];
 }
 
 // Write the factored diagonal tile j: L block (f32, guarded to M; optional) and D_j (f64).
-__device__ void write_diag(const CholArgs& a, int b, int j, const double* sF, const double* sX) {
+__device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, const double* sF, const double* sX) {
   const int64_t g0 = (int64_t)j * CB;
   const int nr = (int)min<int64_t>(CB, a.M - g0);
   if (a.L) tile_store_f32(a.L + (int64_t)b * a.strideL + g0 * a.ldl + g0, a.ldl, sF, false, nr, nr);

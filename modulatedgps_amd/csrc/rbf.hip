@@ -22,7 +22,7 @@ namespace mgp {
 constexpr int kRbfThreads = 256;
 constexpr int kRbfCols = 4;                       // columns per thread
 constexpr int kRbfTileN = kRbfThreads * kRbfCols; // 1024 columns per workgroup
-constexpr int kRbfTileM = 16;                     // rows per workgroup
+constexpr int kRbfTileM = 64;                     // rows per workgroup (X re-read M/64 times)
 
 template <int DMAX>
 __global__ __launch_bounds__(kRbfThreads) void rbf_kernel(

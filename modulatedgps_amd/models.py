@@ -44,6 +44,27 @@ def _splitmix64(x):
     return x ^ (x >> 31)
 
 
+class _Stage:
+    """Optional HIP-event bracket around a stage, recorded on torch's current
+    stream (the stream every libmgp_hip call of the model is launched on)."""
+
+    def __init__(self, timing, name):
+        self.timing, self.name = timing, name
+
+    def __enter__(self):
+        if self.timing is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.timing is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.timing.setdefault(self.name, []).append((self.e0, e1))
+        return False
+
+
 def _to_dev(x, device, dtype=torch.float32):
     t = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x)
     return t.to(device=device, dtype=dtype)
@@ -121,7 +142,7 @@ class SVGPModified:
         """GPflow SVGP.prior_kl -> gauss_kl(q_mu, q_sqrt) whitened (models.py:79); float64 [1]."""
         return ops.gauss_kl_white(self.q_mu, self.q_sqrt, out=out)
 
-    def conditional_kn(self, X, LinvT=None, bufs=None):
+    def conditional_kn(self, X, LinvT=None, bufs=None, timing=None):
         """Whitened conditional for X [N, D]: fmean, fvar as expert-major [K, N] views.
 
         LinvT: (L^-1)^T of this layer's Kuu if already factorised (the SMGP
@@ -132,11 +153,15 @@ class SVGPModified:
             self._last_info = info
             LinvT = LinvT[0]
         bufs = bufs or {}
-        Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
-                          out=bufs.get("Kuf"))
-        A, stats = ops.trsm_stats(LinvT, Kuf, self.q_mu, A=bufs.get("A"), stats=bufs.get("stats"))
-        return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
-                                      fmean=bufs.get("fmean"), fvar=bufs.get("fvar"))
+        with _Stage(timing, "rbf_kuf"):
+            Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
+                              out=bufs.get("Kuf"))
+        with _Stage(timing, "trsm_stats"):
+            A, stats = ops.trsm_stats(LinvT, Kuf, self.q_mu, A=bufs.get("A"),
+                                      stats=bufs.get("stats"))
+        with _Stage(timing, "expert_cond"):
+            return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
+                                          fmean=bufs.get("fmean"), fvar=bufs.get("fvar"))
 
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
         """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior
@@ -246,18 +271,19 @@ class SMGP(SGP):
         self.last_info = torch.cat(infos)
         return outs[0], outs[1]
 
-    def conditionals(self, X):
+    def conditionals(self, X, timing=None):
         """(mu_f, var_f, mu_a, var_a), each an expert-major [K, N] device view."""
         X = self.pred_layer.kernel._x(X)
         N = X.shape[0]
         b = self._buffers(N)
-        LinvT_f, LinvT_a = self._factorise(b)
+        with _Stage(timing, "kuu_chol"):
+            LinvT_f, LinvT_a = self._factorise(b)
         self.pred_layer.conditional_kn(X, LinvT_f, bufs={"Kuf": b["Kuf_f"], "A": b["A_f"],
                                                          "stats": b["stats_f"], "fmean": b["mu_f"],
-                                                         "fvar": b["var_f"]})
+                                                         "fvar": b["var_f"]}, timing=timing)
         self.assign_layer.conditional_kn(X, LinvT_a, bufs={"Kuf": b["Kuf_a"], "A": b["A_a"],
                                                            "stats": b["stats_a"], "fmean": b["mu_a"],
-                                                           "fvar": b["var_a"]})
+                                                           "fvar": b["var_a"]}, timing=timing)
         return b["mu_f"], b["var_f"], b["mu_a"], b["var_a"]
 
     def next_seed(self):
@@ -267,7 +293,7 @@ class SMGP(SGP):
 
     # ------------------------------------------------------------------ ELBO
     def _build_likelihood(self, X, Y, noise=None, seed=None, n_offset=0, n_total=None,
-                          process_group=None, return64=False):
+                          process_group=None, return64=False, timing=None):
         """ELBO (models.py:69-79) as a 0-d float32 device tensor.
 
         noise: optional explicit (z, u) [S, N, K] device tensors (parity mode);
@@ -280,18 +306,21 @@ class SMGP(SGP):
         if Yd.numel() != N:
             raise ValueError("X and Y must have the same number of rows")
         b = self._buffers(N)
-        mu_f, var_f, mu_a, var_a = self.conditionals(X)
+        mu_f, var_f, mu_a, var_a = self.conditionals(X, timing=timing)
         kl = b["kl"]
-        self.pred_layer.prior_kl(out=kl[0:1])
-        self.assign_layer.prior_kl(out=kl[1:2])
+        with _Stage(timing, "gauss_kl"):
+            self.pred_layer.prior_kl(out=kl[0:1])
+            self.assign_layer.prior_kl(out=kl[1:2])
         lik_var = self.likelihood.likelihood.variance.reshape(-1)
         if seed is None and noise is None:
             seed = self.next_seed()
-        ops.elbo_terms(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU, noise=noise,
-                       seed=seed or 0, n_offset=n_offset, out=b["data_sum"])
+        with _Stage(timing, "elbo_terms"):
+            ops.elbo_terms(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU,
+                           noise=noise, seed=seed or 0, n_offset=n_offset, out=b["data_sum"])
         if process_group is not None:
             import torch.distributed as dist
-            dist.all_reduce(b["data_sum"], op=dist.ReduceOp.SUM, group=process_group)
+            with _Stage(timing, "allreduce"):
+                dist.all_reduce(b["data_sum"], op=dist.ReduceOp.SUM, group=process_group)
         n_batch = n_total if n_total is not None else N
         num_data = self.num_data if self.num_data is not None else n_batch
         ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"],
