@@ -1,0 +1,71 @@
+"""Per-kernel micro-benchmark at BASELINE config shapes (HIP events, interleaved
+repeats in one process).  Usage: python tools/bench_kernels.py [--config c3] [--reps 5]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from modulatedgps_amd import ops  # noqa: E402
+
+CFG = {"c2": (8192, 256, 4, 2, 0.15), "c3": (65536, 1024, 8, 8, 1.0), "c5": (262144, 2048, 16, 16, 2.0)}
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts)), float(np.min(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    N, M, K, D, ls = CFG[a.config]
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(N, D, device=dev, generator=g)
+    Z = X[:M].clone()
+    var = torch.tensor([0.5], device=dev)
+    lsc = torch.tensor([ls], device=dev)
+    q_mu = 0.5 * torch.randn(M, K, device=dev, generator=g)
+    q_sqrt = ops.padded(M, M, dev, batch=K)
+    q_sqrt.copy_(0.5 * torch.eye(M, device=dev) + torch.tril(0.1 * torch.randn(K, M, M, device=dev, generator=g)))
+    out = {}
+    _, LinvT, info = ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6)
+    Kuf = ops.rbf_kuf(X, Z, var, lsc)
+    A, stats = ops.trsm_stats(LinvT[0], Kuf, q_mu)
+    fm, fv = ops.expert_conditional(A, q_sqrt, stats, var)
+    torch.cuda.synchronize()
+    runs = {
+        "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
+        "rbf_kuf": lambda: ops.rbf_kuf(X, Z, var, lsc, out=Kuf),
+        "trsm_stats": lambda: ops.trsm_stats(LinvT[0], Kuf, q_mu, A=A, stats=stats),
+        "expert_cond": lambda: ops.expert_conditional(A, q_sqrt, stats, var, fmean=fm, fvar=fv),
+    }
+    for _ in range(2):
+        for f in runs.values():
+            f()
+    torch.cuda.synchronize()
+    for name, f in runs.items():
+        med, mn = timeit(f, a.reps)
+        out[name] = {"median_ms": med, "min_ms": mn}
+    out["expert_cond"]["tflops"] = K * M * M * N / (out["expert_cond"]["median_ms"] * 1e-3) / 1e12
+    out["trsm_stats"]["tflops"] = M * M * N / (out["trsm_stats"]["median_ms"] * 1e-3) / 1e12
+    out["rbf_kuf"]["GBps"] = 4 * (N * D + M * D + M * N) / (out["rbf_kuf"]["median_ms"] * 1e-3) / 1e9
+    print(json.dumps({"config": a.config, "env": {k: v for k, v in os.environ.items() if k.startswith("MGP_")}, **out}))
+
+
+if __name__ == "__main__":
+    main()
