@@ -145,15 +145,9 @@ def load_traffic(kernel):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    group = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        group = dist.group.WORLD
+    from modulatedgps_amd.distributed import init_from_env
+    rank, world, local = init_from_env("nccl")
+    group = torch.distributed.group.WORLD if world > 1 else None
     device = torch.device("cuda", local if world > 1 else 0)
     cfg = CONFIGS[args.config]
     N, M, K, D, ls, S = cfg
