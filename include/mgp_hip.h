@@ -116,11 +116,14 @@ int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ld
  * Replaces the LTA = matmul(L, A_tiled, transpose_a=True) / reduce_sum(square)
  * tail of GPflow base_conditional (models.py:141-143; Knn = var from
  * models.py:133).  q_sqrt: [K][M][ldqs] at element stride strideq.
- * fmean, fvar: [K][ldf] (expert-major; ldf >= N). */
+ * fmean, fvar: [K][ldf] (expert-major; ldf >= N).  Workspace (per-row-tile
+ * partial sums): mgp_expert_workspace_bytes(M, N, K). */
+size_t mgp_expert_workspace_bytes(int64_t M, int64_t N, int32_t K);
 int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
                            int64_t strideq, const float* stats, int64_t lds,
                            const float* variance, int64_t M, int64_t N, int32_t K, float* fmean,
-                           float* fvar, int64_t ldf, mgp_stream_t stream);
+                           float* fvar, int64_t ldf, void* workspace, size_t workspace_bytes,
+                           mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K7
  * Whitened Gaussian KL (GPflow gauss_kl(q_mu, q_sqrt, K=None), reached through

@@ -54,8 +54,10 @@ SIGNATURES = {
     "mgp_stats_tiles": (ctypes.c_int, [c_i64]),
     "mgp_trsm_stats": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                       c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "mgp_expert_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
     "mgp_expert_conditional": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr,
-                                              c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr]),
+                                              c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
+                                              c_ptr]),
     "mgp_kl_workspace_bytes": (c_size, [c_i64, c_i32]),
     "mgp_gauss_kl_white": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr,
                                           c_ptr, c_size, c_ptr]),

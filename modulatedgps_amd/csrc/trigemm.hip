@@ -40,8 +40,8 @@ constexpr int kTgBK = 16;
 // (BM/WR) x (BN/WC) as RT x CT 32x32 accumulators.
 template <int BM, int BN>
 struct TgCfg {
-  static constexpr int WR = 2;
-  static constexpr int WC = BN >= 256 ? 4 : 2;
+  static constexpr int WR = BM >= 128 ? 2 : 1;
+  static constexpr int WC = 4;
   static constexpr int THREADS = WR * WC * 64;
 };
 
@@ -223,7 +223,7 @@ __global__ __launch_bounds__((TgCfg<BM, BN>::THREADS), (TgCfg<BM, BN>::THREADS /
     }
   // ---- stats: stage q_mu rows of this tile (zero beyond M / K)
   float* sQ = lds;                       // [BM][KMAX]
-  float* sRed = lds + BM * KMAX;         // [2][KMAX + 1][BN]
+  float* sRed = lds + BM * KMAX;         // [WR][KMAX + 1][BN]
   for (int idx = threadIdx.x; idx < BM * KMAX; idx += G::NT) {
     const int r = idx / KMAX, kk = idx % KMAX;
     sQ[idx] = (i0 + r < M && kk < K) ? q_mu[(i0 + r) * ldq + kk] : 0.f;
@@ -273,64 +273,98 @@ __global__ __launch_bounds__((TgCfg<BM, BN>::THREADS), (TgCfg<BM, BN>::THREADS /
   for (int idx = threadIdx.x; idx < (K + 1) * BN; idx += G::NT) {
     const int row = idx / BN, lc = idx % BN;
     const int64_t n = n0 + lc;
-    if (n < N) st[row * lds_ + n] = sRed[row * BN + lc] + sRed[((KMAX + 1) + row) * BN + lc];
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < G::WR; ++q) v += sRed[(q * (KMAX + 1) + row) * BN + lc];
+    if (n < N) st[row * lds_ + n] = v;
   }
 }
 
 // ------------------------------------------------------------------ K5
-// grid.x = K * nTiles_n, block b -> (expert k = b / nTn, n-tile = b % nTn):
-// the K experts of one n-tile share an XCD group (b % 8) when nTn % 8 == 0.
+// One workgroup per item (expert k, column tile tn, row tile t): the partial
+// sum over the tile's 128 rows of (L_k^T A)^2 is written to part[k][t][n]
+// (deterministic; cond_finalize adds the T partials).  Items are dispatched
+// heaviest row tile first (LPT: the t-th tile walks M - 128 t rows of K), and
+// within a row tile the 8 experts of one column tile sit at block ids that
+// are equal mod 8, i.e. on one XCD (round-robin dispatch), so they share the
+// A slab in that XCD's L2.
 template <int BM, int BN, bool GUARD>
 __global__ __launch_bounds__((TgCfg<BM, BN>::THREADS), (TgCfg<BM, BN>::THREADS / 256)) void expert_cond_kernel(
     const float* __restrict__ Amat, int64_t lda, const float* __restrict__ q_sqrt, int64_t ldqs,
-    int64_t strideq, const float* __restrict__ stats, int64_t lds_, int nTs,
-    const float* __restrict__ variance, int64_t M, int64_t N, int K, float* __restrict__ fmean,
-    float* __restrict__ fvar, int64_t ldf) {
+    int64_t strideq, int64_t M, int64_t N, int K, float* __restrict__ part, int64_t ldp) {
   using G = TriGemm<BM, BN, true, GUARD>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nTn = (int)((N + BN - 1) / BN), nTm = (int)((M + BM - 1) / BM);
-  const int k = (int)(blockIdx.x / nTn);
-  const int tn = (int)(blockIdx.x % nTn);
-  const int64_t n0 = (int64_t)tn * BN;
+  // block -> (t, tn, k): b = 8 * j + x (x = XCD group); within a group j runs
+  // over (t heavy-first, column tiles tn = x mod 8, experts k).
+  const int b = blockIdx.x;
+  int t, tn, k;
+  if (nTn % 8 == 0) {
+    const int x = b & 7, j = b >> 3;
+    const int per_t = (nTn / 8) * K;
+    t = j / per_t;
+    const int rem = j % per_t;
+    tn = (rem / K) * 8 + x;
+    k = rem % K;
+  } else {
+    const int per_t = nTn * K;
+    t = b / per_t;
+    tn = (b % per_t) / K;
+    k = b % K;
+  }
+  const int tm = t;                         // heavy first: tile 0 walks all M rows
+  const int64_t n0 = (int64_t)tn * BN, i0 = (int64_t)tm * BM;
   const float* Lk = q_sqrt + (int64_t)k * strideq;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w / G::WC, wc = w % G::WC, l32 = lane & 31;
+  floatx16 acc[G::RT][G::CT];
+  G::run(acc, lds, Lk, ldqs, Amat, lda, M, N, i0, n0, i0, M);
   float colsq[G::CT];
 #pragma unroll
-  for (int c = 0; c < G::CT; ++c) colsq[c] = 0.f;
-  for (int tm = 0; tm < nTm; ++tm) {
-    const int64_t i0 = (int64_t)tm * BM;
-    floatx16 acc[G::RT][G::CT];
-    G::run(acc, lds, Lk, ldqs, Amat, lda, M, N, i0, n0, i0, M);
+  for (int c = 0; c < G::CT; ++c) {
+    colsq[c] = 0.f;
 #pragma unroll
     for (int r = 0; r < G::RT; ++r)
 #pragma unroll
-      for (int c = 0; c < G::CT; ++c)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) colsq[c] = fmaf(acc[r][c][e], acc[r][c][e], colsq[c]);
+      for (int e = 0; e < 16; ++e) colsq[c] = fmaf(acc[r][c][e], acc[r][c][e], colsq[c]);
+    colsq[c] += __shfl_xor(colsq[c], 32, 64);
   }
-#pragma unroll
-  for (int c = 0; c < G::CT; ++c) colsq[c] += __shfl_xor(colsq[c], 32, 64);
-  float* sRed = lds;  // [2][BN]
+  float* sRed = lds;  // [WR][BN]
   if (lane < 32) {
 #pragma unroll
     for (int c = 0; c < G::CT; ++c) sRed[wr * BN + wc * G::WN + 32 * c + l32] = colsq[c];
   }
   __syncthreads();
-  const float var = variance[0];
+  float* dst = part + ((int64_t)k * nTm + tm) * ldp;
   for (int lc = threadIdx.x; lc < BN; lc += G::NT) {
     const int64_t n = n0 + lc;
-    if (n >= N) continue;
-    float a2 = 0.f, fm = 0.f;
-    for (int t = 0; t < nTs; ++t) {
-      const float* st = stats + (int64_t)t * (K + 1) * lds_;
-      a2 += st[n];
-      fm += st[(int64_t)(1 + k) * lds_ + n];
-    }
-    fmean[(int64_t)k * ldf + n] = fm;
-    fvar[(int64_t)k * ldf + n] = (var - a2) + (sRed[lc] + sRed[BN + lc]);
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < G::WR; ++q) v += sRed[q * BN + lc];
+    if (n < N) dst[n] = v;
   }
+}
+
+// fmean[k][n] = sum_t stats[t][1+k][n];
+// fvar[k][n]  = var - sum_t stats[t][0][n] + sum_t part[k][t][n].
+__global__ __launch_bounds__(256) void cond_finalize_kernel(const float* __restrict__ stats, int64_t lds_,
+                                                            const float* __restrict__ part, int64_t ldp,
+                                                            int nT, const float* __restrict__ variance,
+                                                            int64_t N, int K, float* __restrict__ fmean,
+                                                            float* __restrict__ fvar, int64_t ldf) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (n >= N) return;
+  float a2 = 0.f, fm = 0.f, q = 0.f;
+  for (int t = 0; t < nT; ++t) {
+    const float* st = stats + (int64_t)t * (K + 1) * lds_;
+    a2 += st[n];
+    fm += st[(int64_t)(1 + k) * lds_ + n];
+    q += part[((int64_t)k * nT + t) * ldp + n];
+  }
+  fmean[(int64_t)k * ldf + n] = fm;
+  fvar[(int64_t)k * ldf + n] = (variance[0] - a2) + q;
 }
 
 }  // namespace mgp
@@ -344,9 +378,12 @@ static bool force_guard() {  // experiment switch: MGP_FORCE_GUARD=1 selects the
   return v == 1;
 }
 
-// Tile choice shared by K4 and K5: row tile BM = 128 always (the stats tiling
-// depends on it: T = ceil(M / 128)); column tile 256 for large N, else 128.
-constexpr int kTgBM = 128;
+// Tile choice shared by K4 and K5: row tile BM = kTgBM always (the stats tiling
+// depends on it: T = ceil(M / BM)); column tile 256 for large N, else 128.
+#ifndef MGP_TG_BM
+#define MGP_TG_BM 64
+#endif
+constexpr int kTgBM = MGP_TG_BM;
 static inline int tg_bn(int64_t N) { return N >= 256 * 64 ? 256 : 128; }
 
 extern "C" int mgp_stats_tiles(int64_t M) { return (int)((M + kTgBM - 1) / kTgBM); }
@@ -407,27 +444,41 @@ extern "C" int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf,
   return dispatch_trsm<128>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, s);
 }
 
+static int64_t expert_ldp(int64_t N) { return (N + 3) / 4 * 4; }
+
+extern "C" size_t mgp_expert_workspace_bytes(int64_t M, int64_t N, int32_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 16;
+  return (size_t)K * (size_t)((M + kTgBM - 1) / kTgBM) * (size_t)expert_ldp(N) * sizeof(float);
+}
+
 template <int BN>
-static void launch_expert(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
-                          int64_t strideq, const float* stats, int64_t lds, const float* variance,
-                          int64_t M, int64_t N, int K, float* fmean, float* fvar, int64_t ldf,
-                          hipStream_t s) {
+static int launch_expert(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
+                         int64_t strideq, const float* stats, int64_t lds, const float* variance,
+                         int64_t M, int64_t N, int K, float* fmean, float* fvar, int64_t ldf,
+                         float* part, hipStream_t s) {
   constexpr int BM = kTgBM;
-  const int nTn = (int)((N + BN - 1) / BN), nTs = (int)((M + BM - 1) / BM);
+  const int nTn = (int)((N + BN - 1) / BN), nTm = (int)((M + BM - 1) / BM);
+  const int64_t ldp = expert_ldp(N);
   const size_t shm = (size_t)TriGemm<BM, BN, true, false>::LDS_FLOATS * sizeof(float);
-  const dim3 grid(K * nTn), block(TgCfg<BM, BN>::THREADS);
+  const dim3 grid(K * nTn * nTm), block(TgCfg<BM, BN>::THREADS);
   if (M % BM == 0 && N % BN == 0 && !force_guard())
     hipLaunchKernelGGL((expert_cond_kernel<BM, BN, false>), grid, block, shm, s, A, lda, q_sqrt, ldqs,
-                       strideq, stats, lds, nTs, variance, M, N, K, fmean, fvar, ldf);
+                       strideq, M, N, K, part, ldp);
   else
     hipLaunchKernelGGL((expert_cond_kernel<BM, BN, true>), grid, block, shm, s, A, lda, q_sqrt, ldqs,
-                       strideq, stats, lds, nTs, variance, M, N, K, fmean, fvar, ldf);
+                       strideq, M, N, K, part, ldp);
+  int st = launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(cond_finalize_kernel, dim3((unsigned)((N + 255) / 256), K), dim3(256), 0, s, stats,
+                     lds, part, ldp, nTm, variance, N, K, fmean, fvar, ldf);
+  return launch_status();
 }
 
 extern "C" int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
                                       int64_t strideq, const float* stats, int64_t lds,
                                       const float* variance, int64_t M, int64_t N, int32_t K,
-                                      float* fmean, float* fvar, int64_t ldf, mgp_stream_t stream) {
+                                      float* fmean, float* fvar, int64_t ldf, void* workspace,
+                                      size_t workspace_bytes, mgp_stream_t stream) {
   if (!A) return -1;
   if (lda < N) return -2;
   if (!q_sqrt) return -3;
@@ -445,11 +496,13 @@ extern "C" int mgp_expert_conditional(const float* A, int64_t lda, const float* 
   if (lda % 4 || ldqs % 4 || lds % 4) return MGP_ERR_ALIGN;
   if (!aligned16(A) || !aligned16(q_sqrt) || (strideq % 4)) return MGP_ERR_ALIGN;
   if (M * lda * 4 >= (int64_t)1 << 31 || M * ldqs * 4 >= (int64_t)1 << 31) return MGP_ERR_UNSUPPORTED;
-  if (N == 0) return MGP_OK;
+  if (N == 0 || M == 0) return MGP_OK;
+  if (!workspace || workspace_bytes < mgp_expert_workspace_bytes(M, N, K)) return MGP_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
   if (tg_bn(N) == 256)
-    launch_expert<256>(A, lda, q_sqrt, ldqs, strideq, stats, lds, variance, M, N, K, fmean, fvar, ldf, s);
-  else
-    launch_expert<128>(A, lda, q_sqrt, ldqs, strideq, stats, lds, variance, M, N, K, fmean, fvar, ldf, s);
-  return launch_status();
+    return launch_expert<256>(A, lda, q_sqrt, ldqs, strideq, stats, lds, variance, M, N, K, fmean, fvar,
+                              ldf, part, s);
+  return launch_expert<128>(A, lda, q_sqrt, ldqs, strideq, stats, lds, variance, M, N, K, fmean, fvar,
+                            ldf, part, s);
 }

@@ -161,7 +161,8 @@ class SVGPModified:
                                       stats=bufs.get("stats"))
         with _Stage(timing, "expert_cond"):
             return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
-                                          fmean=bufs.get("fmean"), fvar=bufs.get("fvar"))
+                                          fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
+                                          workspace=bufs.get("ws_expert"))
 
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
         """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior
@@ -244,6 +245,8 @@ class SMGP(SGP):
             "data_sum": torch.empty(1, dtype=torch.float64, device=dev),
             "elbo": torch.empty((), dtype=torch.float32, device=dev),
             "elbo64": torch.empty((), dtype=torch.float64, device=dev),
+            "ws_expert": torch.empty(ops.expert_workspace_bytes(Mx, N, K), dtype=torch.uint8,
+                                     device=dev),
         }
         if Mf == Ma and self.pred_layer.Z.shape[1] == self.assign_layer.Z.shape[1]:
             b["LinvT2"] = ops.padded(Mf, Mf, dev, batch=2)
@@ -280,10 +283,12 @@ class SMGP(SGP):
             LinvT_f, LinvT_a = self._factorise(b)
         self.pred_layer.conditional_kn(X, LinvT_f, bufs={"Kuf": b["Kuf_f"], "A": b["A_f"],
                                                          "stats": b["stats_f"], "fmean": b["mu_f"],
-                                                         "fvar": b["var_f"]}, timing=timing)
+                                                         "fvar": b["var_f"],
+                                                         "ws_expert": b["ws_expert"]}, timing=timing)
         self.assign_layer.conditional_kn(X, LinvT_a, bufs={"Kuf": b["Kuf_a"], "A": b["A_a"],
                                                            "stats": b["stats_a"], "fmean": b["mu_a"],
-                                                           "fvar": b["var_a"]}, timing=timing)
+                                                           "fvar": b["var_a"],
+                                                           "ws_expert": b["ws_expert"]}, timing=timing)
         return b["mu_f"], b["var_f"], b["mu_a"], b["var_a"]
 
     def next_seed(self):

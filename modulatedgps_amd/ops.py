@@ -186,7 +186,11 @@ def trsm_stats(LinvT, Kuf, q_mu, A=None, stats=None):
     return A, stats
 
 
-def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None):
+def expert_workspace_bytes(M, N, K):
+    return max(int(_lib.load().mgp_expert_workspace_bytes(M, N, K)), 16)
+
+
+def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None, workspace=None):
     """fmean, fvar [K, N] of the whitened K-expert conditional."""
     _check(A, "A", 2), _check(q_sqrt, "q_sqrt", 3), _check(stats, "stats", 3)
     M, N = A.shape
@@ -198,9 +202,13 @@ def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None):
         fvar = padded(K, N, dev)
     if _ld(fmean) != _ld(fvar):
         raise ValueError("fmean and fvar must share a leading dimension")
+    nbytes = _lib.load().mgp_expert_workspace_bytes(M, N, K)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
     _lib.call("mgp_expert_conditional", A.data_ptr(), _ld(A), q_sqrt.data_ptr(), _ld(q_sqrt),
               q_sqrt.stride(0), stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K,
-              fmean.data_ptr(), fvar.data_ptr(), _ld(fmean), _stream())
+              fmean.data_ptr(), fvar.data_ptr(), _ld(fmean), workspace.data_ptr(),
+              workspace.numel(), _stream())
     return fmean, fvar
 
 
