@@ -125,6 +125,31 @@ int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int
                            float* fvar, int64_t ldf, void* workspace, size_t workspace_bytes,
                            mgp_stream_t stream);
 
+/* ---------------------------------------------------------------- K5, split-bf16
+ * The same K-expert conditional on the bf16 matrix cores at f32 accuracy:
+ * every f32 operand is split exactly into three bf16 planes and each product
+ * is formed from the six plane products of weight >= 2^-16 (f32-accumulated;
+ * see csrc/split3.hip).  Operands are passed as "fragment images":
+ *   mgp_split_lower_x6: L_k = band_part(q_sqrt[k], -1, 0) -> Lfr
+ *       (mgp_x6_lower_bytes(M, K) bytes; replaces the band_part at
+ *       models.py:141-143 and is rebuilt whenever q_sqrt changes);
+ *   mgp_split_cols_x6:  A [M][lda] -> Afr (mgp_x6_cols_bytes(M, N) bytes);
+ *       mgp_trsm_stats_x6 writes Afr directly instead.
+ * mgp_expert_conditional_x6 then produces fmean/fvar exactly as
+ * mgp_expert_conditional.  Images must be < 4 GiB.  Workspace:
+ * mgp_expert_x6_workspace_bytes(M, N, K). */
+size_t mgp_x6_lower_bytes(int64_t M, int32_t K);
+size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
+int mgp_split_lower_x6(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
+                       void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
+int mgp_split_cols_x6(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr, size_t afr_bytes,
+                      mgp_stream_t stream);
+size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K);
+int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                              const float* stats, int64_t lds, const float* variance, int64_t M,
+                              int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                              void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+
 /* ---------------------------------------------------------------- K7
  * Whitened Gaussian KL (GPflow gauss_kl(q_mu, q_sqrt, K=None), reached through
  * SVGP.prior_kl at models.py:79):

@@ -39,6 +39,13 @@ constexpr int LDT = CB + 2;   // LDS leading dimension (doubles): conflict-free 
 constexpr int kCholThreads = 256;
 constexpr int kMaxBatch = 8;
 
+#ifdef MGP_DBG_STAMPS
+__device__ unsigned long long g_stamps[64 * 16];
+#define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(j, k) do {} while (0)
+#endif
+
 struct CholArgs {
   // input: either a float32 matrix A (per batch at A + b*strideA) ...
   const float* A; int64_t lda, strideA;
@@ -169,62 +176,72 @@ __device__ __forceinline__ void quad_to_global(double* __restrict__ g, int64_t l
   quad_foreach([&](int ti, int tj, int r, int row, int col) { g[(int64_t)row * ld + col] = q.c[ti][tj][r]; });
 }
 
-// Diagonal-tile factorisation: wave 0, lane r owns row r; the tile is walked in
-// four 16-column panels (left-looking): each panel is first updated with the
-// finished panels (L[r][k] L[s][k], k < 16J), then factored column by column
-// with in-register shuffles.  Only 16 doubles per lane are live (no scratch).
-template <int J>
-__device__ __forceinline__ void chol_panel(double* __restrict__ sF, int r, int& bad) {
-  constexpr int C0 = 16 * J;
-  double a[16];
-#pragma unroll
-  for (int t = 0; t < 16; ++t) a[t] = sF[r * LDT + C0 + t];
-#pragma unroll 4
-  for (int k = 0; k < C0; ++k) {
-    const double lrk = sF[r * LDT + k];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) a[t] = fma(-lrk, sF[(C0 + t) * LDT + k], a[t]);
-  }
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const double piv = __shfl(a[c], C0 + c, 64);
-    if (!(piv > 0.0) && bad == 0) bad = C0 + c + 1;
-    const double d = sqrt(piv);
-    const double lc = (r > C0 + c) ? a[c] / d : (r == C0 + c ? d : 0.0);
-    a[c] = lc;
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2)
-      if (s2 > c) a[s2] = fma(-lc, __shfl(lc, C0 + s2, 64), a[s2]);
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) sF[r * LDT + C0 + t] = (C0 + t <= r) ? a[t] : 0.0;
+// Uniform double from lane `lane` (compile-time) of a VGPR pair.
+__device__ __forceinline__ double read_lane_f64(double v, int lane) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), lane);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// Inverse row I: lane c owns column c of X = L^-1 in x[0..63]; row I of L is
-// read from LDS (wave-uniform address -> broadcast).
-template <int I>
-__device__ __forceinline__ void inv_row(double (&x)[CB], const double* __restrict__ sL, int c) {
-  double s = (I == c) ? 1.0 : 0.0;
-#pragma unroll
-  for (int t = 0; t < I; ++t) s = fma(-sL[I * LDT + t], x[t], s);
-  x[I] = s / sL[I * LDT + I];
-  if constexpr (I + 1 < CB) inv_row<I + 1>(x, sL, c);
+// 1/p to full f64 precision: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rcp_f64(double p) {
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  return fma(r, fma(-p, r, 1.0), r);
 }
 
 // Factor the symmetric 64x64 tile in sF (lower part used) in place: sF <- L
-// (zeros above), sX <- L^-1.  Wave 0 only.  Records the first non-positive pivot.
-__device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX, double* __restrict__ col,
-                                 int32_t* info, int64_t gcol0) {
+// (zeros above), sX <- L^-1 (zeros above).  Wave 0 only; the other waves return.
+//
+// Factorisation: square-root-free right-looking sweep.  Lane r keeps row r in
+// registers; at column c the pivot p_c is read from lane c, column c is
+// broadcast through LDS, and every lane updates a[s] -= (a[c]/p_c) a_s[c]
+// (s > c).  Afterwards L[r][c] = a[c] / sqrt(p_c) (c <= r).  The critical path
+// per column is one readlane, one reciprocal and one LDS round trip; no sqrt or
+// division sits on it.
+// Inverse: X = L^-1 by a right-looking forward substitution, lane c keeping
+// column c of X; column I of L is read as a broadcast from L^T staged in sX.
+// Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
+__device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX,
+                                                 double* __restrict__ col, int32_t* info, int64_t gcol0) {
   if (threadIdx.x >= 64) return;
   const int r = threadIdx.x;
+  double* bc = sX;  // column broadcast buffer (row 0 of sX, free until L^T is staged)
   int bad = 0;
-  chol_panel<0>(sF, r, bad);
-  chol_panel<1>(sF, r, bad);
-  chol_panel<2>(sF, r, bad);
-  chol_panel<3>(sF, r, bad);
+  {
+    double a[CB];
+#pragma unroll
+    for (int t = 0; t < CB; ++t) a[t] = sF[r * LDT + t];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const double piv = read_lane_f64(a[c], c);
+      if (!(piv > 0.0) && bad == 0) bad = c + 1;
+      const double t = a[c] * rcp_f64(piv);
+      bc[r] = a[c];
+      col[c] = 1.0 / sqrt(piv);
+#pragma unroll
+      for (int s = c + 1; s < CB; ++s) a[s] = fma(-t, bc[s], a[s]);
+    }
+    // L = a[c] / sqrt(p_c) below and on the diagonal; stage L (row-major) and L^T.
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const double l = (c <= r) ? a[c] * col[c] : 0.0;
+      sF[r * LDT + c] = l;
+      sX[c * LDT + r] = l;
+    }
+  }
   if (bad && r == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
+  STAMP((int)(gcol0 / CB) - 1, 5);
   double x[CB];
-  inv_row<0>(x, sF, r);
+#pragma unroll
+  for (int t = 0; t < CB; ++t) x[t] = (t == r) ? 1.0 : 0.0;
+#pragma unroll
+  for (int I = 0; I < CB; ++I) {
+    x[I] *= col[I];  // 1 / L[I][I]
+#pragma unroll
+    for (int J = I + 1; J < CB; ++J) x[J] = fma(-sX[I * LDT + J], x[I], x[J]);
+  }
 #pragma unroll
   for (int i = 0; i < CB; ++i) sX[i * LDT + r] = x[i];
 }
@@ -316,10 +333,13 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     while ((ai + 1) * (ai + 2) / 2 <= idx) ++ai;
     const int bl_ = idx - ai * (ai + 1) / 2;
     const int i = j + 1 + ai, l = j + 1 + bl_;
+    const bool la = (ai == 0 && bl_ == 0);
+    if (la) STAMP(j, 0);
     tile_load(s1, Wt(i, j), Mp);
     tile_load(sD, ws_D(a, b, j), CB);
     if (l != i) tile_load(s2, Wt(l, j), Mp);
     __syncthreads();
+    if (la) STAMP(j, 1);
     Quad pi = quad_zero(), pl = quad_zero();
     tile_mma<false, true>(pi, s1, sD, 1.0);                 // P_i = W_ij D_j^T
     if (l != i) tile_mma<false, true>(pl, s2, sD, 1.0);     // P_l
@@ -327,6 +347,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     quad_to_lds(s1, pi);
     if (l != i) quad_to_lds(s2, pl);
     __syncthreads();
+    if (la) STAMP(j, 2);
     if (l == i && a.L) {
       const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
       tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
@@ -337,11 +358,16 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     tile_mma<false, true>(u, s1, (l == i) ? s1 : s2, -1.0);  // W_il -= P_i P_l^T
     if (ai == 0 && bl_ == 0) {  // look-ahead: factor the next diagonal tile
       __syncthreads();
+      STAMP(j, 3);
       quad_to_lds(s1, u);
       __syncthreads();
+      STAMP(j, 4);
       factor_diag_tile(s1, s2, col, a.info + b, (int64_t)(j + 1) * CB);
+      STAMP(j, 6);
       __syncthreads();
       write_diag(a, b, j + 1, s1, s2);
+      __syncthreads();
+      STAMP(j, 7);
     } else {
       quad_to_global(Wt(i, l), Mp, u);
     }
@@ -379,6 +405,12 @@ static int64_t chol_ws_doubles_per_batch(int64_t M) {
   const int64_t Mp = chol_mp(M);
   return 2 * Mp * Mp + (Mp / CB) * CB * CB;
 }
+
+#ifdef MGP_DBG_STAMPS
+extern "C" int mgp_dbg_chol_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
+}
+#endif
 
 extern "C" size_t mgp_chol_workspace_bytes(int64_t M, int32_t batch) {
   if (M <= 0 || batch <= 0) return 0;

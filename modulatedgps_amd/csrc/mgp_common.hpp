@@ -19,6 +19,12 @@ inline int hip_status(hipError_t e) { return e == hipSuccess ? MGP_OK : MGP_ERR_
 inline int launch_status() { return hip_status(hipGetLastError()); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// fmean[k][n] = sum over nTs stats tiles; fvar[k][n] = var - sum_t ||A||^2 part
+// + sum over nTp expert partials (trigemm.hip; shared by the f32 and split-bf16 K5).
+int mgp_launch_cond_finalize(const float* stats, int64_t lds, int nTs, const float* part, int64_t ldp, int nTp,
+                             const float* variance, int64_t N, int K, float* fmean, float* fvar, int64_t ldf,
+                             hipStream_t s);
+
 // ------------------------------------------------------------------ MFMA
 // D(32x32) += A(32x2) * B(2x32), exact f32 (fmaf chain).  Lane l supplies
 // A[i = l & 31][k = l >> 5] and B[k = l >> 5][j = l & 31].  Result register r of

@@ -1,0 +1,352 @@
+// K5 on the bf16 matrix cores at f32 accuracy ("split-bf16 x6").
+//
+// Reference: the same contraction as trigemm.hip's K5 -- for every expert k,
+// fvar[k][n] += sum_m' (L_k^T A)[m'][n]^2 with L_k = band_part(q_sqrt[k], -1, 0)
+// (GPflow base_conditional, reached from MixtureGPs/models.py:141-143).
+//
+// Every f32 operand x is split exactly into three bf16 planes,
+//     x = hi + mid + lo (+ |x| 2^-25 at most),   hi = bf16(x), mid = bf16(x - hi),
+//     lo = bf16(x - hi - mid)
+// (each difference is exact in f32).  A product is formed from the six plane
+// products whose weight is >= 2^-16 of the leading one,
+//     a b ~ a_hi b_hi + a_hi b_mid + a_mid b_hi + a_hi b_lo + a_mid b_mid + a_lo b_hi,
+// so the per-product error is a few f32 ulps and the sum is accumulated in the
+// f32 MFMA accumulator -- the accuracy class of an f32 GEMM.  Six
+// v_mfma_f32_32x32x16_bf16 (32 cycles each for 32x32x16) replace eight
+// v_mfma_f32_32x32x2_f32 (64 cycles each for 32x32x2): 192 vs 512 cycles per
+// 32x32x16 block, 2.7x the f32 matrix rate on the same silicon.
+//
+// Data layout ("fragment images", built once per step, 6 B per element):
+//   Lfr[k][mb][mk][p][lane][8]  A-operand of (L_k)^T: lane (r = lane&31,
+//       h = lane>>5), element j holds L_k[m][m'] with m' = 32 mb + r and
+//       m = 16 mk + kperm(h, j), kperm(h, j) = (j&3) + 8 (j>>2) + 4 h; zero above
+//       the diagonal (m < m') and outside M.
+//   Afr[nb][mk][p][lane][8]     B-operand of A: element j holds
+//       A[16 mk + kperm(h, j)][32 nb + r]; zero outside M x N.
+// kperm is the row order in which a 32x32 MFMA accumulator holds its rows
+// (register 8s + j of lane half h is row 16 s + kperm(h, j)), so K4's epilogue
+// can emit A's image straight from its accumulators; both operands use the
+// same k order, which leaves the contraction unchanged.
+// Each fragment is 1 KiB contiguous per plane: a wave reads it with one
+// coalesced 16-B-per-lane load (global for A, LDS for L), no transposes.
+//
+// K5x6 kernel: one 256-thread workgroup per item (expert k, row tile t of 128
+// rows m', column tile of 256 n).  Wave w owns all 128 rows x 64 columns
+// (4 x 2 accumulators of 32x32).  Per k-step (16 rows of m): the workgroup
+// stages the 12 KiB of L fragments of its 4 row sub-tiles in LDS (double
+// buffered, one barrier per k-step); each wave loads its 6 A fragments (6 KiB)
+// straight from global into registers one k-step ahead; 48 MFMAs per wave.
+// The triangle is exploited at row-tile granularity (k-steps start at 128 t);
+// the zero blocks inside the diagonal tile come from Lfr's zero fill.
+#include "mgp_common.hpp"
+
+namespace mgp {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int kX6BM = 128;   // rows m' per item
+constexpr int kX6BN = 256;   // columns n per item
+constexpr int kFragBytes = 1024;
+
+__device__ __forceinline__ int kperm(int h, int j) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
+
+// x -> (hi, mid, lo) bf16 planes, exact differences in f32.
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)x;
+  const float r1 = x - (float)hi;
+  mid = (__bf16)r1;
+  const float r2 = r1 - (float)mid;
+  lo = (__bf16)r2;
+}
+
+__device__ __forceinline__ void store_split(bf16x8* __restrict__ dst, const float (&v)[8]) {
+  bf16x8 h, m, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 a, b, c;
+    split3(v[j], a, b, c);
+    h[j] = a; m[j] = b; l[j] = c;
+  }
+  dst[0] = h;
+  dst[64] = m;
+  dst[128] = l;
+}
+
+// One wave per fragment block (k, mb, mk): grid.x = K * nmb * nmk / 4 (4 waves per block).
+__global__ __launch_bounds__(256) void split_lower_kernel(const float* __restrict__ q_sqrt, int64_t ldqs,
+                                                          int64_t strideq, int64_t M, int nmb, int nmk,
+                                                          int64_t nfrag, bf16x8* __restrict__ Lfr) {
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= nfrag) return;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int mk = (int)(f % nmk);
+  const int64_t kb = f / nmk;
+  const int mb = (int)(kb % nmb);
+  const int k = (int)(kb / nmb);
+  const int64_t mc = 32 * (int64_t)mb + r;
+  const float* L = q_sqrt + (int64_t)k * strideq;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t m = 16 * (int64_t)mk + kperm(h, j);
+    v[j] = (m < M && mc < M && m >= mc) ? L[m * ldqs + mc] : 0.f;
+  }
+  store_split(Lfr + f * 3 * 64 + lane, v);
+}
+
+// One wave per fragment block (nb, mk): grid.x = nnb * nmk / 4.
+__global__ __launch_bounds__(256) void split_cols_kernel(const float* __restrict__ A, int64_t lda, int64_t M,
+                                                         int64_t N, int nmk, int64_t nfrag,
+                                                         bf16x8* __restrict__ Afr) {
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= nfrag) return;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int mk = (int)(f % nmk);
+  const int64_t n = 32 * (f / nmk) + r;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t m = 16 * (int64_t)mk + kperm(h, j);
+    v[j] = (m < M && n < N) ? A[m * lda + n] : 0.f;
+  }
+  store_split(Afr + f * 3 * 64 + lane, v);
+}
+
+__device__ __forceinline__ floatx16 mfma_bf16(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// acc += (a_hi + a_mid + a_lo)(b_hi + b_mid + b_lo) without the three
+// products of weight < 2^-16; smallest terms first.
+__device__ __forceinline__ floatx16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 acc) {
+  acc = mfma_bf16(a[2], b[0], acc);
+  acc = mfma_bf16(a[1], b[1], acc);
+  acc = mfma_bf16(a[0], b[2], acc);
+  acc = mfma_bf16(a[1], b[0], acc);
+  acc = mfma_bf16(a[0], b[1], acc);
+  return mfma_bf16(a[0], b[0], acc);
+}
+
+// Item b -> (row tile t heavy-first, column tile tn, expert k); the K experts of
+// a column tile are 8 block ids apart (one XCD) when nTn % 8 == 0.
+__device__ __forceinline__ void x6_item(int b, int nTn, int K, int& t, int& tn, int& k) {
+  if (nTn % 8 == 0) {
+    const int x = b & 7, j = b >> 3;
+    const int per_t = (nTn / 8) * K;
+    t = j / per_t;
+    const int rem = j % per_t;
+    tn = (rem / K) * 8 + x;
+    k = rem % K;
+  } else {
+    const int per_t = nTn * K;
+    t = b / per_t;
+    tn = (b % per_t) / K;
+    k = b % K;
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
+                                                                const bf16x8* __restrict__ Lfr,
+                                                                uint32_t afr_bytes, uint32_t lfr_bytes,
+                                                                int nmk, int nmb, int nTn, int K,
+                                                                int64_t N, float* __restrict__ part,
+                                                                int64_t ldp) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];  // 2 x 12 KiB: [row sub-tile][plane][lane]
+  int t, tn, k;
+  x6_item(blockIdx.x, nTn, K, t, tn, k);
+  const int nTp = nmb / 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mk0 = 8 * t, nks = nmk - mk0;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Afr, (short)0, (int)afr_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc((void*)Lfr, (short)0, (int)lfr_bytes, 0x00020000);
+  // A fragments of this wave: column blocks nb = 8 tn + 2 w + c, k-step mk, plane p
+  //   byte offset ((nb * nmk + mk) * 3 + p) * 1 KiB + 16 lane
+  const uint32_t vA = 16u * lane;
+  const uint32_t sA0 = (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes;
+  const uint32_t sA1 = sA0 + (uint32_t)nmk * 3u * kFragBytes;
+  // L stage: 768 16-B units per k-step, 3 per thread: unit e = tid + 256 s ->
+  //   row sub-tile i = e / 192, rest = e % 192 (= p * 64 + lane)
+  //   byte offset (((k * nmb + 4 t + i) * nmk + mk) * 192 + rest) * 16
+  uint32_t vL[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int e = tid + 256 * s;
+    vL[s] = (uint32_t)(((e / 192) * nmk * 192 + (e % 192)) * 16);
+  }
+  const uint32_t sLbase = (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 192u * 16u;
+
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][c][e] = 0.f;
+
+  auto load_a = [&](bf16x8 (&b)[2][3], int mk) {
+    const uint32_t o = (uint32_t)mk * 3u * kFragBytes;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      b[0][p] = ld_frag(rA, vA, sA0 + o + p * kFragBytes);
+      b[1][p] = ld_frag(rA, vA, sA1 + o + p * kFragBytes);
+    }
+  };
+  auto load_l = [&](u32x4v (&st)[3], int mk) {
+    const uint32_t o = sLbase + (uint32_t)mk * 192u * 16u;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rL, vL[s], o, 0);
+  };
+  auto store_l = [&](int buf, const u32x4v (&st)[3]) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
+  };
+  auto compute = [&](int buf, const bf16x8 (&b)[2][3]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p] = sL[buf][(i * 3 + p) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) acc[i][c] = mfma_x6(a, b[c], acc[i][c]);
+    }
+  };
+
+  bf16x8 b0[2][3], b1[2][3];
+  u32x4v st[3];
+  load_l(st, mk0);
+  load_a(b0, mk0);
+  store_l(0, st);
+  __syncthreads();
+  // two k-steps per iteration (nks is even): buffers and fragment sets alternate
+#pragma nounroll
+  for (int q = 0; q < nks; q += 2) {
+    const int m1 = mk0 + q + 1;
+    load_l(st, m1);
+    load_a(b1, m1);
+    compute(0, b0);
+    store_l(1, st);
+    __syncthreads();
+    const int m2 = mk0 + q + 2 < nmk ? mk0 + q + 2 : nmk - 1;  // last pair: harmless reload
+    load_l(st, m2);
+    load_a(b0, m2);
+    compute(1, b1);
+    store_l(0, st);
+    __syncthreads();
+  }
+
+  // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
+  const int64_t nbase = (int64_t)tn * kX6BN + 64 * w + (lane & 31);
+  float* dst = part + ((int64_t)k * nTp + t) * ldp;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s = fmaf(acc[i][c][e], acc[i][c][e], s);
+    s += __shfl_xor(s, 32, 64);
+    const int64_t n = nbase + 32 * c;
+    if (lane < 32 && n < N) dst[n] = s;
+  }
+}
+
+}  // namespace mgp
+
+using namespace mgp;
+
+static int64_t x6_mp(int64_t M) { return (M + kX6BM - 1) / kX6BM * kX6BM; }
+static int64_t x6_np(int64_t N) { return (N + kX6BN - 1) / kX6BN * kX6BN; }
+
+extern "C" size_t mgp_x6_lower_bytes(int64_t M, int32_t K) {
+  if (M <= 0 || K <= 0) return 0;
+  const int64_t Mp = x6_mp(M);
+  return (size_t)K * (size_t)(Mp / 32) * (size_t)(Mp / 16) * 3 * kFragBytes;
+}
+
+extern "C" size_t mgp_x6_cols_bytes(int64_t M, int64_t N) {
+  if (M <= 0 || N <= 0) return 0;
+  return (size_t)(x6_np(N) / 32) * (size_t)(x6_mp(M) / 16) * 3 * kFragBytes;
+}
+
+extern "C" int mgp_split_lower_x6(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
+                                  void* Lfr, size_t lfr_bytes, mgp_stream_t stream) {
+  if (!q_sqrt) return -1;
+  if (ldqs < M) return -2;
+  if (K > 1 && strideq < ldqs * M) return -3;
+  if (M < 0) return -4;
+  if (K < 0) return -5;
+  if (!Lfr) return -6;
+  if (M == 0 || K == 0) return MGP_OK;
+  if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(Lfr)) return MGP_ERR_ALIGN;
+  const int64_t Mp = x6_mp(M);
+  const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
+  const int64_t nfrag = (int64_t)K * nmb * nmk;
+  hipLaunchKernelGGL(split_lower_kernel, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     q_sqrt, ldqs, strideq, M, nmb, nmk, nfrag, (bf16x8*)Lfr);
+  return launch_status();
+}
+
+extern "C" int mgp_split_cols_x6(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr,
+                                 size_t afr_bytes, mgp_stream_t stream) {
+  if (!A) return -1;
+  if (lda < N) return -2;
+  if (M < 0) return -3;
+  if (N < 0) return -4;
+  if (!Afr) return -5;
+  if (M == 0 || N == 0) return MGP_OK;
+  if (afr_bytes < mgp_x6_cols_bytes(M, N)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(Afr)) return MGP_ERR_ALIGN;
+  const int nmk = (int)(x6_mp(M) / 16);
+  const int64_t nfrag = (x6_np(N) / 32) * nmk;
+  hipLaunchKernelGGL(split_cols_kernel, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     A, lda, M, N, nmk, nfrag, (bf16x8*)Afr);
+  return launch_status();
+}
+
+extern "C" size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 16;
+  return (size_t)K * (size_t)(x6_mp(M) / kX6BM) * (size_t)((N + 3) / 4 * 4) * sizeof(float);
+}
+
+extern "C" int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                         const float* stats, int64_t lds, const float* variance, int64_t M,
+                                         int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                                         void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  if (!Afr) return -1;
+  if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
+  if (!Lfr) return -3;
+  if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return -4;
+  if (!stats) return -5;
+  if (lds < N) return -6;
+  if (!variance) return -7;
+  if (M < 0) return -8;
+  if (N < 0) return -9;
+  if (K < 1) return -10;
+  if (!fmean) return -11;
+  if (!fvar) return -12;
+  if (ldf < N) return -13;
+  if (!aligned16(Afr) || !aligned16(Lfr)) return MGP_ERR_ALIGN;
+  if (afr_bytes >= ((size_t)1 << 32) || lfr_bytes >= ((size_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  if (M == 0 || N == 0) return MGP_OK;
+  if (!workspace || workspace_bytes < mgp_expert_x6_workspace_bytes(M, N, K)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t Mp = x6_mp(M);
+  const int nmk = (int)(Mp / 16), nmb = (int)(Mp / 32), nTp = (int)(Mp / kX6BM);
+  const int nTn = (int)(x6_np(N) / kX6BN);
+  const int64_t ldp = (N + 3) / 4 * 4;
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(expert_cond_x6_kernel, dim3((unsigned)(K * nTp * nTn)), dim3(256), 0, s,
+                     (const bf16x8*)Afr, (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N),
+                     (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N, part, ldp);
+  int st = launch_status();
+  if (st) return st;
+  return mgp_launch_cond_finalize(stats, lds, mgp_stats_tiles(M), part, ldp, nTp, variance, N, K, fmean, fvar,
+                                  ldf, s);
+}

@@ -349,7 +349,7 @@ __global__ __launch_bounds__((TgCfg<BM, BN>::THREADS), (TgCfg<BM, BN>::THREADS /
 // fmean[k][n] = sum_t stats[t][1+k][n];
 // fvar[k][n]  = var - sum_t stats[t][0][n] + sum_t part[k][t][n].
 __global__ __launch_bounds__(256) void cond_finalize_kernel(const float* __restrict__ stats, int64_t lds_,
-                                                            const float* __restrict__ part, int64_t ldp,
+                                                            int nTs, const float* __restrict__ part, int64_t ldp,
                                                             int nT, const float* __restrict__ variance,
                                                             int64_t N, int K, float* __restrict__ fmean,
                                                             float* __restrict__ fvar, int64_t ldf) {
@@ -357,12 +357,12 @@ __global__ __launch_bounds__(256) void cond_finalize_kernel(const float* __restr
   const int k = blockIdx.y;
   if (n >= N) return;
   float a2 = 0.f, fm = 0.f, q = 0.f;
-  for (int t = 0; t < nT; ++t) {
+  for (int t = 0; t < nTs; ++t) {
     const float* st = stats + (int64_t)t * (K + 1) * lds_;
     a2 += st[n];
     fm += st[(int64_t)(1 + k) * lds_ + n];
-    q += part[((int64_t)k * nT + t) * ldp + n];
   }
+  for (int t = 0; t < nT; ++t) q += part[((int64_t)k * nT + t) * ldp + n];
   fmean[(int64_t)k * ldf + n] = fm;
   fvar[(int64_t)k * ldf + n] = (variance[0] - a2) + q;
 }
@@ -444,6 +444,14 @@ extern "C" int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf,
   return dispatch_trsm<128>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, s);
 }
 
+int mgp::mgp_launch_cond_finalize(const float* stats, int64_t lds, int nTs, const float* part, int64_t ldp,
+                                  int nTp, const float* variance, int64_t N, int K, float* fmean, float* fvar,
+                                  int64_t ldf, hipStream_t s) {
+  hipLaunchKernelGGL(cond_finalize_kernel, dim3((unsigned)((N + 255) / 256), K), dim3(256), 0, s, stats, lds,
+                     nTs, part, ldp, nTp, variance, N, K, fmean, fvar, ldf);
+  return launch_status();
+}
+
 static int64_t expert_ldp(int64_t N) { return (N + 3) / 4 * 4; }
 
 extern "C" size_t mgp_expert_workspace_bytes(int64_t M, int64_t N, int32_t K) {
@@ -469,9 +477,7 @@ static int launch_expert(const float* A, int64_t lda, const float* q_sqrt, int64
                        strideq, M, N, K, part, ldp);
   int st = launch_status();
   if (st) return st;
-  hipLaunchKernelGGL(cond_finalize_kernel, dim3((unsigned)((N + 255) / 256), K), dim3(256), 0, s, stats,
-                     lds, part, ldp, nTm, variance, N, K, fmean, fvar, ldf);
-  return launch_status();
+  return mgp_launch_cond_finalize(stats, lds, nTm, part, ldp, nTm, variance, N, K, fmean, fvar, ldf, s);
 }
 
 extern "C" int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,

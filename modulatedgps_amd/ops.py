@@ -212,6 +212,49 @@ def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None, worksp
     return fmean, fvar
 
 
+# ------------------------------------------------------------ K5, split-bf16 (x6)
+def split_lower_x6(q_sqrt, out=None):
+    """Fragment image (uint8 device tensor) of L_k = tril(q_sqrt[k]) for the split-bf16 K5."""
+    _check(q_sqrt, "q_sqrt", 3)
+    K, M = q_sqrt.shape[0], q_sqrt.shape[1]
+    nbytes = _lib.load().mgp_x6_lower_bytes(M, K)
+    if out is None or out.numel() < nbytes:
+        out = _ws(nbytes, q_sqrt.device)
+    _lib.call("mgp_split_lower_x6", q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), M, K, out.data_ptr(),
+              out.numel(), _stream())
+    return out
+
+
+def split_cols_x6(A, out=None):
+    """Fragment image (uint8 device tensor) of A [M, N] for the split-bf16 K5."""
+    _check(A, "A", 2)
+    M, N = A.shape
+    nbytes = _lib.load().mgp_x6_cols_bytes(M, N)
+    if out is None or out.numel() < nbytes:
+        out = _ws(nbytes, A.device)
+    _lib.call("mgp_split_cols_x6", A.data_ptr(), _ld(A), M, N, out.data_ptr(), out.numel(), _stream())
+    return out
+
+
+def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=None, workspace=None):
+    """fmean, fvar [K, N] of the whitened K-expert conditional from split-bf16 images."""
+    _check(stats, "stats", 3)
+    dev = stats.device
+    if fmean is None:
+        fmean = padded(K, N, dev)
+    if fvar is None:
+        fvar = padded(K, N, dev)
+    if _ld(fmean) != _ld(fvar):
+        raise ValueError("fmean and fvar must share a leading dimension")
+    nbytes = _lib.load().mgp_expert_x6_workspace_bytes(M, N, K)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    _lib.call("mgp_expert_conditional_x6", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
+              stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(), fvar.data_ptr(),
+              _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
+    return fmean, fvar
+
+
 # --------------------------------------------------------------------------- K7
 def gauss_kl_white(q_mu, q_sqrt, out=None, workspace=None):
     """Whitened KL (models.py:79) as a float64 device tensor of shape [1]."""

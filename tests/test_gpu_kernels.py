@@ -182,3 +182,47 @@ def test_elbo_terms_explicit_and_philox(device, N, K, S):
     n = np.arange(N)
     r2 = ref(philox.noise_normal(seed, S, n, K), philox.noise_uniform(seed, S, n, K))
     assert out2 == pytest.approx(r2, rel=1e-4, abs=1e-3)
+
+
+@pytest.mark.parametrize("N,M,K,D,ls", [(1000, 25, 3, 1, 0.5), (8192, 256, 4, 2, 0.15),
+                                         (5000, 300, 5, 3, 0.7), (16384, 1024, 8, 8, 1.0),
+                                         (777, 64, 1, 2, 1.0)])
+def test_conditional_split_bf16(device, N, M, K, D, ls):
+    """K5 on split-bf16 fragment images (x6): same bound as the f32 path against
+    the float64 oracle, and within 2e-6 normwise of the exact-f32 MFMA K5."""
+    from modulatedgps_amd import ops
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
+    L = p.pred
+    mu_ref, var_ref = R.svgp_predict_f_dedup(X, L["Z"], L["variance"], L["lengthscales"], L["q_mu"], L["q_sqrt"])
+    tol = 1e-4 if np.linalg.cond(R.rbf_Kuu(L["Z"], L["variance"], ls)) < 1e6 else 5e-4
+    _, LinvT, info = ops.kuu_potrf_trtri([_t(L["Z"], device)], [_t([L["variance"]], device)],
+                                         [_t([ls], device)], 1e-6)
+    Kuf = ops.rbf_kuf(_t(X, device), _t(L["Z"], device), _t([L["variance"]], device), _t([ls], device))
+    A, stats = ops.trsm_stats(LinvT[0], Kuf, _t(L["q_mu"], device))
+    qs = ops.as_padded(_t(L["q_sqrt"], device))
+    var = _t([L["variance"]], device)
+    fm32, fv32 = ops.expert_conditional(A, qs, stats, var)
+    Afr = ops.split_cols_x6(A)
+    Lfr = ops.split_lower_x6(qs)
+    fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K)
+    assert torch.equal(fm[:, :N], fm32[:, :N])
+    assert normwise(to_np(fv).T, to_np(fv32).T) < 2e-6
+    assert normwise(to_np(fm).T, mu_ref) < tol
+    assert normwise(to_np(fv).T, var_ref) < tol
+
+
+def test_split_bf16_layout_exact(device):
+    """Operands exactly representable in bf16 (small integers): the split is
+    exact (mid = lo = 0), so the x6 sum of squares must match float64 to f32
+    rounding of the final sums -- catches any k-order / lane-map mismatch."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(3)
+    M, N, K = 256, 512, 2
+    A = rng.integers(-3, 4, size=(M, N)).astype(np.float32)
+    Ls = np.tril(rng.integers(-2, 3, size=(K, M, M))).astype(np.float32)
+    At, qs = _t(A, device), ops.as_padded(_t(Ls, device))
+    stats = torch.zeros(ops.stats_tiles(M), K + 1, N, device=device)
+    fm, fv = ops.expert_conditional_x6(ops.split_cols_x6(At), ops.split_lower_x6(qs), stats,
+                                       _t([0.0], device), M, N, K)
+    ref = np.stack([np.sum((Ls[k].T.astype(np.float64) @ A) ** 2, axis=0) for k in range(K)])
+    assert np.array_equal(to_np(fv)[:, :N].astype(np.float64), ref)

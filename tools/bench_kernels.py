@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="", help="comma-separated subset of the kernels to time")
     a = ap.parse_args()
     N, M, K, D, ls = CFG[a.config]
     dev = torch.device("cuda", 0)
@@ -47,13 +48,21 @@ def main():
     Kuf = ops.rbf_kuf(X, Z, var, lsc)
     A, stats = ops.trsm_stats(LinvT[0], Kuf, q_mu)
     fm, fv = ops.expert_conditional(A, q_sqrt, stats, var)
+    Afr = ops.split_cols_x6(A)
+    Lfr = ops.split_lower_x6(q_sqrt)
+    fm6, fv6 = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K)
     torch.cuda.synchronize()
     runs = {
         "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
         "rbf_kuf": lambda: ops.rbf_kuf(X, Z, var, lsc, out=Kuf),
         "trsm_stats": lambda: ops.trsm_stats(LinvT[0], Kuf, q_mu, A=A, stats=stats),
         "expert_cond": lambda: ops.expert_conditional(A, q_sqrt, stats, var, fmean=fm, fvar=fv),
+        "split_cols_x6": lambda: ops.split_cols_x6(A, out=Afr),
+        "split_lower_x6": lambda: ops.split_lower_x6(q_sqrt, out=Lfr),
+        "expert_cond_x6": lambda: ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmean=fm6, fvar=fv6),
     }
+    if a.only:
+        runs = {k: v for k, v in runs.items() if k in a.only.split(",")}
     for _ in range(2):
         for f in runs.values():
             f()
@@ -61,9 +70,14 @@ def main():
     for name, f in runs.items():
         med, mn = timeit(f, a.reps)
         out[name] = {"median_ms": med, "min_ms": mn}
-    out["expert_cond"]["tflops"] = K * M * M * N / (out["expert_cond"]["median_ms"] * 1e-3) / 1e12
-    out["trsm_stats"]["tflops"] = M * M * N / (out["trsm_stats"]["median_ms"] * 1e-3) / 1e12
-    out["rbf_kuf"]["GBps"] = 4 * (N * D + M * D + M * N) / (out["rbf_kuf"]["median_ms"] * 1e-3) / 1e9
+    if "expert_cond" in out:
+        out["expert_cond"]["tflops"] = K * M * M * N / (out["expert_cond"]["median_ms"] * 1e-3) / 1e12
+    if "expert_cond_x6" in out:
+        out["expert_cond_x6"]["tflops"] = K * M * M * N / (out["expert_cond_x6"]["median_ms"] * 1e-3) / 1e12
+    if "trsm_stats" in out:
+        out["trsm_stats"]["tflops"] = M * M * N / (out["trsm_stats"]["median_ms"] * 1e-3) / 1e12
+    if "rbf_kuf" in out:
+        out["rbf_kuf"]["GBps"] = 4 * (N * D + M * D + M * N) / (out["rbf_kuf"]["median_ms"] * 1e-3) / 1e9
     print(json.dumps({"config": a.config, "env": {k: v for k, v in os.environ.items() if k.startswith("MGP_")}, **out}))
 
 
