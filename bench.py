@@ -36,6 +36,8 @@ CONFIGS = {
     "c5": (262144, 2048, 16, 16, 2.0, 25),
 }
 PEAK_F32_MFMA = 157.3e12      # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_BF16_MFMA = 2.5e15       # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
+PEAK_X6 = PEAK_BF16_MFMA / 6  # split-bf16 K4/K5: 6 bf16 products per f32 product
 PEAK_F64 = 78.6e12            # FP64 vector/matrix (half the f32 rate)
 PEAK_HBM = 8.0e12             # HBM3E spec
 
@@ -145,6 +147,8 @@ def load_traffic(kernel):
 
 def main():
     args = parse()
+    from modulatedgps_amd.config import conditional_mode
+    x6 = conditional_mode() == "x6"
     from modulatedgps_amd.distributed import init_from_env
     rank, world, local = init_from_env("nccl")
     group = torch.distributed.group.WORLD if world > 1 else None
@@ -194,27 +198,32 @@ def main():
         kernels["rbf_kuf"] = {"bound": "hbm", "avg_us": ms * 1e3, "bytes": kuf_bytes,
                               "achieved": kuf_bytes / (ms * 1e-3) / 1e9, "unit": "GB/s",
                               "peak": PEAK_HBM / 1e9, "frac": kuf_bytes / (ms * 1e-3) / PEAK_HBM}
-    for name, fl in (("trsm_stats", trsm_flops), ("expert_cond", expert_flops)):
+    for name, fl, peak in (("trsm_stats", trsm_flops, PEAK_F32_MFMA),
+                           ("expert_cond", expert_flops, PEAK_X6 if x6 else PEAK_F32_MFMA)):
         if name in st:
             ms = st[name][0]
             kernels[name] = {"bound": "mfma", "avg_us": ms * 1e3, "flops": fl,
                              "achieved": fl / (ms * 1e-3) / 1e12, "unit": "TFLOP/s",
-                             "peak": PEAK_F32_MFMA / 1e12, "frac": fl / (ms * 1e-3) / PEAK_F32_MFMA}
+                             "peak": peak / 1e12, "frac": fl / (ms * 1e-3) / peak}
     if "kuu_chol" in st:
         ms = st["kuu_chol"][0]
         kernels["kuu_chol"] = {"bound": "latency", "avg_us": ms * 1e3, "flops": chol_flops,
                                "achieved": chol_flops / (ms * 1e-3) / 1e12, "unit": "TFLOP/s",
                                "peak": PEAK_F64 / 1e12, "frac": chol_flops / (ms * 1e-3) / PEAK_F64}
-    for name in ("elbo_terms", "gauss_kl", "allreduce"):
+    for name in ("elbo_terms", "gauss_kl", "allreduce", "split_lower"):
         if name in st:
             kernels[name] = {"avg_us": st[name][0] * 1e3}
 
     ek = kernels.get("expert_cond", {})
-    traffic, traffic_src = load_traffic("expert_cond_kernel")
-    roofline = {"kernel": "expert_cond_kernel (K5, L_k^T A + sum of squares)", "bound": "mfma",
-                "achieved": ek.get("achieved"), "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
-                "frac": ek.get("frac"), "traffic": traffic, "traffic_source": traffic_src,
-                "algorithmic_per_launch": f"K*M^2*N = {expert_flops:.4g} flop"}
+    kname = "expert_cond_x6_kernel" if x6 else "expert_cond_kernel"
+    traffic, traffic_src = load_traffic(kname)
+    roofline = {"kernel": f"{kname} (K5, L_k^T A + sum of squares, + cond_finalize)", "bound": "mfma",
+                "achieved": ek.get("achieved"), "peak": (PEAK_X6 if x6 else PEAK_F32_MFMA) / 1e12,
+                "unit": "TFLOP/s", "frac": ek.get("frac"), "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_per_launch": f"K*M^2*N = {expert_flops:.4g} f32 flop",
+                "peak_note": ("split-bf16: each f32 product is 6 bf16 MFMA products, peak = "
+                              "2.5 PF bf16 dense / 6" if x6 else "f32 MFMA dense peak")}
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
@@ -228,6 +237,9 @@ def main():
             "value": value, "unit": "ELBO steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "dtype_note": ("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
+                           "3-plane split (6 products, f32-accurate); K3 in f64" if x6 else
+                           "f32 MFMA (exact f32); K3 in f64"),
             "config": {"workload": f"{args.config}: SMGP ELBO forward, N={N}/GPU, M={M}, K={K}, "
                                    f"D={D}, S={S}, lengthscale={ls}",
                        "global_batch": n_total, "N_per_gpu": N, "M": M, "K": K, "D": D, "S": S,

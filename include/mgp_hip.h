@@ -107,6 +107,12 @@ int mgp_stats_tiles(int64_t M);
 int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M,
                    int64_t N, const float* q_mu, int64_t ldq, int32_t K, float* A, int64_t lda,
                    float* stats, int64_t lds, mgp_stream_t stream);
+/* The same, additionally (or only: A may be NULL) writing the split-bf16
+ * fragment image of A consumed by mgp_expert_conditional_x6 (Afr, at least
+ * mgp_x6_cols_bytes(M, N) bytes; every fragment of the padded image is written). */
+int mgp_trsm_stats_x6(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M,
+                      int64_t N, const float* q_mu, int64_t ldq, int32_t K, float* A, int64_t lda,
+                      void* Afr, size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K5
  * K-expert whitened conditional, finalised:
@@ -134,7 +140,7 @@ int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int
  *       (mgp_x6_lower_bytes(M, K) bytes; replaces the band_part at
  *       models.py:141-143 and is rebuilt whenever q_sqrt changes);
  *   mgp_split_cols_x6:  A [M][lda] -> Afr (mgp_x6_cols_bytes(M, N) bytes);
- *       mgp_trsm_stats_x6 writes Afr directly instead.
+ *       mgp_trsm_stats_x6 (K4) writes Afr directly instead.
  * mgp_expert_conditional_x6 then produces fmean/fvar exactly as
  * mgp_expert_conditional.  Images must be < 4 GiB.  Workspace:
  * mgp_expert_x6_workspace_bytes(M, N, K). */

@@ -3,9 +3,13 @@
 
 The compute dtype of this build is float32 (the MI355X path); the reference's
 float64 semantics are the parity target (tolerances in tests/)."""
+import os
+
 import torch
 
-_CFG = {"jitter": 1e-6, "device": None}
+# conditional: "x6" = K5 on split-bf16 fragment images (f32-accurate, bf16 MFMA),
+#              "f32" = K5 on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32).
+_CFG = {"jitter": 1e-6, "device": None, "conditional": os.environ.get("MGP_CONDITIONAL", "x6")}
 
 
 def default_jitter():
@@ -30,3 +34,13 @@ def default_device():
 
 def set_default_device(dev):
     _CFG["device"] = torch.device(dev)
+
+
+def conditional_mode():
+    return _CFG["conditional"]
+
+
+def set_conditional_mode(mode):
+    if mode not in ("x6", "f32"):
+        raise ValueError("conditional mode must be 'x6' or 'f32'")
+    _CFG["conditional"] = mode

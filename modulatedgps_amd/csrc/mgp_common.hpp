@@ -34,6 +34,39 @@ __device__ __forceinline__ floatx16 mfma32x32x2(float a, float b, floatx16 c) {
 }
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// ------------------------------------------------------------------ split-bf16 (x6) images
+// See split3.hip.  A fragment is 64 lanes x 8 bf16 per plane (1 KiB); lane
+// (r = lane & 31, h = lane >> 5), element j <-> k-row kperm(h, j) of a 16-row
+// k-step, the order in which a 32x32 accumulator holds its rows.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int kperm(int h, int j) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
+
+// x -> (hi, mid, lo) bf16 planes; both differences are exact in f32.
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)x;
+  const float r1 = x - (float)hi;
+  mid = (__bf16)r1;
+  const float r2 = r1 - (float)mid;
+  lo = (__bf16)r2;
+}
+
+// Split 8 values and store the three planes of one lane (dst = plane 0 of the
+// lane; planes are 64 bf16x8 apart).
+__device__ __forceinline__ void store_split(bf16x8* __restrict__ dst, const float (&v)[8]) {
+  bf16x8 h, m, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 a, b, c;
+    split3(v[j], a, b, c);
+    h[j] = a; m[j] = b; l[j] = c;
+  }
+  dst[0] = h;
+  dst[64] = m;
+  dst[128] = l;
+}
+
 // ------------------------------------------------------------------ reductions
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

@@ -42,36 +42,9 @@
 
 namespace mgp {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-
 constexpr int kX6BM = 128;   // rows m' per item
 constexpr int kX6BN = 256;   // columns n per item
 constexpr int kFragBytes = 1024;
-
-__device__ __forceinline__ int kperm(int h, int j) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
-
-// x -> (hi, mid, lo) bf16 planes, exact differences in f32.
-__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
-  hi = (__bf16)x;
-  const float r1 = x - (float)hi;
-  mid = (__bf16)r1;
-  const float r2 = r1 - (float)mid;
-  lo = (__bf16)r2;
-}
-
-__device__ __forceinline__ void store_split(bf16x8* __restrict__ dst, const float (&v)[8]) {
-  bf16x8 h, m, l;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    __bf16 a, b, c;
-    split3(v[j], a, b, c);
-    h[j] = a; m[j] = b; l[j] = c;
-  }
-  dst[0] = h;
-  dst[64] = m;
-  dst[128] = l;
-}
 
 // One wave per fragment block (k, mb, mk): grid.x = K * nmb * nmk / 4 (4 waves per block).
 __global__ __launch_bounds__(256) void split_lower_kernel(const float* __restrict__ q_sqrt, int64_t ldqs,

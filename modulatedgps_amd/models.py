@@ -9,8 +9,12 @@ arguments and method names).  The SMGP ELBO hot path
     K3 mgp_potrf_trtri      L, L^-1 (both layers    models.py:141 (cholesky)
                             batched in one sweep)
     K1 mgp_rbf_kuf          Kuf [M, N]              models.py:139
-    K4 mgp_trsm_stats       A = L^-1 Kuf + stats    models.py:141-143 (triangular_solve, A^T q_mu)
-    K5 mgp_expert_conditional  fmean, fvar [K, N]   models.py:141-143 (LTA, fvar)
+    K4 mgp_trsm_stats_x6    A = L^-1 Kuf + stats    models.py:141-143 (triangular_solve, A^T q_mu)
+                            (A as a split-bf16 image)
+    K5 mgp_split_lower_x6 + mgp_expert_conditional_x6
+                            fmean, fvar [K, N]      models.py:141-143 (LTA, fvar)
+    (config.set_conditional_mode("f32"): K4 mgp_trsm_stats + K5 mgp_expert_conditional
+     on the exact-f32 MFMA instead)
     K7 mgp_gauss_kl_white   KL                      models.py:79 (prior_kl)
   K6 mgp_elbo_terms         sum_n lse_s(...)        models.py:55-67,73-76
   mgp_elbo_combine          ELBO scalar             models.py:76,79
@@ -31,7 +35,7 @@ import torch
 
 from . import ops
 from .broadcasting_lik import BroadcastingLikelihood
-from .config import default_device, default_jitter
+from .config import conditional_mode, default_device, default_jitter
 from .kernels import SquaredExponential
 
 TAU = 1e-2  # RelaxedOneHotCategorical temperature, models.py:60
@@ -156,13 +160,24 @@ class SVGPModified:
         with _Stage(timing, "rbf_kuf"):
             Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
                               out=bufs.get("Kuf"))
+        if conditional_mode() == "f32":
+            with _Stage(timing, "trsm_stats"):
+                A, stats = ops.trsm_stats(LinvT, Kuf, self.q_mu, A=bufs.get("A"),
+                                          stats=bufs.get("stats"))
+            with _Stage(timing, "expert_cond"):
+                return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
+                                              fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
+                                              workspace=bufs.get("ws_expert"))
+        M, N, K = self.num_inducing, X.shape[0], self.num_latent_gps
         with _Stage(timing, "trsm_stats"):
-            A, stats = ops.trsm_stats(LinvT, Kuf, self.q_mu, A=bufs.get("A"),
-                                      stats=bufs.get("stats"))
+            Afr, stats = ops.trsm_stats_x6(LinvT, Kuf, self.q_mu, Afr=bufs.get("Afr"),
+                                           stats=bufs.get("stats"))
+        with _Stage(timing, "split_lower"):
+            Lfr = ops.split_lower_x6(self.q_sqrt, out=bufs.get("Lfr"))
         with _Stage(timing, "expert_cond"):
-            return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
-                                          fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
-                                          workspace=bufs.get("ws_expert"))
+            return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, K,
+                                             fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
+                                             workspace=bufs.get("ws_expert"))
 
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
         """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior
@@ -223,7 +238,7 @@ class SMGP(SGP):
 
     # ------------------------------------------------------------------ internals
     def _buffers(self, N):
-        key = N
+        key = (N, conditional_mode())
         b = self._bufs.get(key)
         if b is not None:
             return b
@@ -232,11 +247,13 @@ class SMGP(SGP):
         Mx = max(Mf, Ma)
         T = ops.stats_tiles(Mx)
         kuf = ops.padded(Mx, N, dev)
-        a = ops.padded(Mx, N, dev)
+        x6 = conditional_mode() == "x6"
+        a = None if x6 else ops.padded(Mx, N, dev)
         st = ops.padded(T * (K + 1), N, dev)
         cond = ops.padded(4 * K, N, dev)          # mu_f, var_f, mu_a, var_a
         b = {
-            "Kuf_f": kuf[:Mf], "Kuf_a": kuf[:Ma], "A_f": a[:Mf], "A_a": a[:Ma],
+            "Kuf_f": kuf[:Mf], "Kuf_a": kuf[:Ma],
+            "A_f": None if x6 else a[:Mf], "A_a": None if x6 else a[:Ma],
             "stats_f": st[:ops.stats_tiles(Mf) * (K + 1)].unflatten(0, (-1, K + 1)),
             "stats_a": st[:ops.stats_tiles(Ma) * (K + 1)].unflatten(0, (-1, K + 1)),
             "mu_f": cond[0:K], "var_f": cond[K:2 * K], "mu_a": cond[2 * K:3 * K],
@@ -245,9 +262,14 @@ class SMGP(SGP):
             "data_sum": torch.empty(1, dtype=torch.float64, device=dev),
             "elbo": torch.empty((), dtype=torch.float32, device=dev),
             "elbo64": torch.empty((), dtype=torch.float64, device=dev),
-            "ws_expert": torch.empty(ops.expert_workspace_bytes(Mx, N, K), dtype=torch.uint8,
+            "ws_expert": torch.empty(max(ops.expert_workspace_bytes(Mx, N, K),
+                                         ops.expert_x6_workspace_bytes(Mx, N, K)), dtype=torch.uint8,
                                      device=dev),
         }
+        if x6:  # split-bf16 images, shared by the two layers (processed in turn)
+            b["Afr"] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
+            b["Lfr"] = torch.empty(ops.x6_lower_bytes(Mx, K), dtype=torch.uint8, device=dev)
+        b["x6"] = x6
         if Mf == Ma and self.pred_layer.Z.shape[1] == self.assign_layer.Z.shape[1]:
             b["LinvT2"] = ops.padded(Mf, Mf, dev, batch=2)
         self._bufs[key] = b
@@ -281,14 +303,13 @@ class SMGP(SGP):
         b = self._buffers(N)
         with _Stage(timing, "kuu_chol"):
             LinvT_f, LinvT_a = self._factorise(b)
+        shared = {"ws_expert": b["ws_expert"], "Afr": b.get("Afr"), "Lfr": b.get("Lfr")}
         self.pred_layer.conditional_kn(X, LinvT_f, bufs={"Kuf": b["Kuf_f"], "A": b["A_f"],
                                                          "stats": b["stats_f"], "fmean": b["mu_f"],
-                                                         "fvar": b["var_f"],
-                                                         "ws_expert": b["ws_expert"]}, timing=timing)
+                                                         "fvar": b["var_f"], **shared}, timing=timing)
         self.assign_layer.conditional_kn(X, LinvT_a, bufs={"Kuf": b["Kuf_a"], "A": b["A_a"],
                                                            "stats": b["stats_a"], "fmean": b["mu_a"],
-                                                           "fvar": b["var_a"],
-                                                           "ws_expert": b["ws_expert"]}, timing=timing)
+                                                           "fvar": b["var_a"], **shared}, timing=timing)
         return b["mu_f"], b["var_f"], b["mu_a"], b["var_a"]
 
     def next_seed(self):

@@ -186,8 +186,40 @@ def trsm_stats(LinvT, Kuf, q_mu, A=None, stats=None):
     return A, stats
 
 
+def trsm_stats_x6(LinvT, Kuf, q_mu, Afr=None, stats=None, A=None):
+    """K4 writing the split-bf16 image Afr of A = L^-1 Kuf (and the stats; the f32
+    A only when `A` is given).  Returns (Afr, stats)."""
+    _check(LinvT, "LinvT", 2), _check(Kuf, "Kuf", 2), _check(q_mu, "q_mu", 2)
+    M, N = Kuf.shape
+    K = q_mu.shape[1]
+    dev = Kuf.device
+    nbytes = _lib.load().mgp_x6_cols_bytes(M, N)
+    if Afr is None or Afr.numel() < nbytes:
+        Afr = _ws(nbytes, dev)
+    if stats is None:
+        T = stats_tiles(M)
+        stats = padded(T * (K + 1), N, dev).unflatten(0, (T, K + 1))
+    _lib.call("mgp_trsm_stats_x6", LinvT.data_ptr(), _ld(LinvT), Kuf.data_ptr(), _ld(Kuf), M, N,
+              q_mu.data_ptr(), _ld(q_mu), K, A.data_ptr() if A is not None else None,
+              _ld(A) if A is not None else N, Afr.data_ptr(), Afr.numel(), stats.data_ptr(), _ld(stats),
+              _stream())
+    return Afr, stats
+
+
 def expert_workspace_bytes(M, N, K):
     return max(int(_lib.load().mgp_expert_workspace_bytes(M, N, K)), 16)
+
+
+def expert_x6_workspace_bytes(M, N, K):
+    return max(int(_lib.load().mgp_expert_x6_workspace_bytes(M, N, K)), 16)
+
+
+def x6_cols_bytes(M, N):
+    return int(_lib.load().mgp_x6_cols_bytes(M, N))
+
+
+def x6_lower_bytes(M, K):
+    return int(_lib.load().mgp_x6_lower_bytes(M, K))
 
 
 def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None, workspace=None):

@@ -226,3 +226,25 @@ def test_split_bf16_layout_exact(device):
                                        _t([0.0], device), M, N, K)
     ref = np.stack([np.sum((Ls[k].T.astype(np.float64) @ A) ** 2, axis=0) for k in range(K)])
     assert np.array_equal(to_np(fv)[:, :N].astype(np.float64), ref)
+
+
+@pytest.mark.parametrize("N,M", [(8192, 256), (1000, 25), (777, 300), (4096, 1024)])
+def test_trsm_writes_split_image(device, N, M):
+    """K4's fused split-bf16 epilogue produces the same image (bit for bit) as
+    splitting its f32 A afterwards, including the zero padding."""
+    from modulatedgps_amd import ops
+    X, Y, p = R.synthetic_problem(N, M, 3, 2, 0.7, state="perturbed", S=2)
+    L = p.pred
+    _, LinvT, _ = ops.kuu_potrf_trtri([_t(L["Z"], device)], [_t([L["variance"]], device)],
+                                      [_t([0.7], device)], 1e-6)
+    Kuf = ops.rbf_kuf(_t(X, device), _t(L["Z"], device), _t([L["variance"]], device), _t([0.7], device))
+    A, st = ops.trsm_stats(LinvT[0], Kuf, _t(L["q_mu"], device))
+    ref = ops.split_cols_x6(A)
+    A2 = ops.padded(M, N, device)
+    img = torch.full_like(ref, 0x7F)  # garbage: every byte must be written
+    img, st2 = ops.trsm_stats_x6(LinvT[0], Kuf, _t(L["q_mu"], device), Afr=img, A=A2)
+    assert torch.equal(img, ref)
+    assert torch.equal(st2, st)
+    assert torch.equal(A2, A)
+    img3, _ = ops.trsm_stats_x6(LinvT[0], Kuf, _t(L["q_mu"], device))
+    assert torch.equal(img3, ref)
