@@ -188,7 +188,11 @@ def main():
     st = stage_stats(timing)
 
     # algorithmic work per launch
-    kuf_bytes = 4.0 * (N * D + M * D + M * N)
+    if x6:   # K1 writes the split-bf16 image of Kuf (6 B per element of the padded [Mp, Np])
+        Mp, Np = -(-M // 128) * 128, -(-N // 256) * 256
+        kuf_bytes = 4.0 * (N * D + M * D) + 6.0 * Mp * Np
+    else:
+        kuf_bytes = 4.0 * (N * D + M * D + M * N)
     trsm_flops = float(M) * M * N
     expert_flops = float(K) * M * M * N
     chol_flops = 2 * (2.0 * M ** 3 / 3.0)        # potrf + trtri, both layers (one batched sweep)
@@ -198,7 +202,7 @@ def main():
         kernels["rbf_kuf"] = {"bound": "hbm", "avg_us": ms * 1e3, "bytes": kuf_bytes,
                               "achieved": kuf_bytes / (ms * 1e-3) / 1e9, "unit": "GB/s",
                               "peak": PEAK_HBM / 1e9, "frac": kuf_bytes / (ms * 1e-3) / PEAK_HBM}
-    for name, fl, peak in (("trsm_stats", trsm_flops, PEAK_F32_MFMA),
+    for name, fl, peak in (("trsm_stats", trsm_flops, PEAK_X6 if x6 else PEAK_F32_MFMA),
                            ("expert_cond", expert_flops, PEAK_X6 if x6 else PEAK_F32_MFMA)):
         if name in st:
             ms = st[name][0]
@@ -210,7 +214,7 @@ def main():
         kernels["kuu_chol"] = {"bound": "latency", "avg_us": ms * 1e3, "flops": chol_flops,
                                "achieved": chol_flops / (ms * 1e-3) / 1e12, "unit": "TFLOP/s",
                                "peak": PEAK_F64 / 1e12, "frac": chol_flops / (ms * 1e-3) / PEAK_F64}
-    for name in ("elbo_terms", "gauss_kl", "allreduce", "split_lower"):
+    for name in ("elbo_terms", "gauss_kl", "allreduce", "split_tri"):
         if name in st:
             kernels[name] = {"avg_us": st[name][0] * 1e3}
 

@@ -107,12 +107,6 @@ int mgp_stats_tiles(int64_t M);
 int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M,
                    int64_t N, const float* q_mu, int64_t ldq, int32_t K, float* A, int64_t lda,
                    float* stats, int64_t lds, mgp_stream_t stream);
-/* The same, additionally (or only: A may be NULL) writing the split-bf16
- * fragment image of A consumed by mgp_expert_conditional_x6 (Afr, at least
- * mgp_x6_cols_bytes(M, N) bytes; every fragment of the padded image is written). */
-int mgp_trsm_stats_x6(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M,
-                      int64_t N, const float* q_mu, int64_t ldq, int32_t K, float* A, int64_t lda,
-                      void* Afr, size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K5
  * K-expert whitened conditional, finalised:
@@ -140,16 +134,30 @@ int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int
  *       (mgp_x6_lower_bytes(M, K) bytes; replaces the band_part at
  *       models.py:141-143 and is rebuilt whenever q_sqrt changes);
  *   mgp_split_cols_x6:  A [M][lda] -> Afr (mgp_x6_cols_bytes(M, N) bytes);
- *       mgp_trsm_stats_x6 (K4) writes Afr directly instead.
+ *       on the ELBO path K4 (mgp_trsm_stats_x6) writes Afr directly.
  * mgp_expert_conditional_x6 then produces fmean/fvar exactly as
  * mgp_expert_conditional.  Images must be < 4 GiB.  Workspace:
  * mgp_expert_x6_workspace_bytes(M, N, K). */
-size_t mgp_x6_lower_bytes(int64_t M, int32_t K);
+size_t mgp_x6_lower_bytes(int64_t M, int32_t K);    /* also the LinvT image: K = 1 */
 size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
 int mgp_split_lower_x6(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
                        void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
 int mgp_split_cols_x6(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr, size_t afr_bytes,
                       mgp_stream_t stream);
+/* Image of LinvT (upper triangle kept) as K4's T operand. */
+int mgp_split_upper_x6(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, size_t tfr_bytes,
+                       mgp_stream_t stream);
+/* K1 writing the image of Kuf directly (same arguments as mgp_rbf_kuf; the
+ * f32 Kuf is not materialised). */
+int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                   int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                   void* Kfr, size_t kfr_bytes, mgp_stream_t stream);
+/* K4 on images: A = LinvT^T Kuf from Tfr (mgp_split_upper_x6) and Kfr
+ * (mgp_rbf_kuf_x6 / mgp_split_cols_x6), writing A's image Afr (for
+ * mgp_expert_conditional_x6) and the stats exactly as mgp_trsm_stats. */
+int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
+                      int64_t N, const float* q_mu, int64_t ldq, int32_t K, void* Afr, size_t afr_bytes,
+                      float* stats, int64_t lds, mgp_stream_t stream);
 size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K);
 int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
                               const float* stats, int64_t lds, const float* variance, int64_t M,

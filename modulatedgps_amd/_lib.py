@@ -58,8 +58,11 @@ SIGNATURES = {
     "mgp_expert_conditional": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr,
                                               c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
                                               c_ptr]),
-    "mgp_trsm_stats_x6": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i32,
-                                         c_ptr, c_i64, c_ptr, c_size, c_ptr, c_i64, c_ptr]),
+    "mgp_trsm_stats_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
+                                         c_ptr, c_size, c_ptr, c_i64, c_ptr]),
+    "mgp_split_upper_x6": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_rbf_kuf_x6": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i32,
+                                      c_ptr, c_size, c_ptr]),
     "mgp_x6_lower_bytes": (c_size, [c_i64, c_i32]),
     "mgp_x6_cols_bytes": (c_size, [c_i64, c_i64]),
     "mgp_split_lower_x6": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_size, c_ptr]),

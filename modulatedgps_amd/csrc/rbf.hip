@@ -79,6 +79,55 @@ __global__ __launch_bounds__(kRbfThreads) void rbf_kernel(
   }
 }
 
+// K1 writing Kuf's split-bf16 image (split3.hip layout) instead of f32 Kuf:
+// workgroup = 4 waves = 4 column blocks of 32 (128 columns) x a chunk of 16
+// k-steps (256 rows); lane (r, h) owns column n = 32 nb + r and, per k-step,
+// rows 16 mk + kperm(h, j).  Each wave writes 16 x 3 KiB contiguous.
+// Rows >= M and columns >= N of the padded image are written as zeros.
+template <int DMAX>
+__global__ __launch_bounds__(kRbfThreads) void rbf_kuf_x6_kernel(
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ Z, int64_t ldz, int64_t N,
+    int64_t M, int D, const float* __restrict__ variance, const float* __restrict__ ls, int n_ls, int nmk,
+    bf16x8* __restrict__ Kfr) {
+  __shared__ float zs[256][DMAX];
+  __shared__ float cs[DMAX];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
+  const int64_t nb = (int64_t)blockIdx.x * 4 + w;
+  const int64_t n = 32 * nb + r;
+  const int mk0 = blockIdx.y * 16;
+  const int64_t m0 = 16 * (int64_t)mk0;
+  const float kHalfLog2e = 0.8493218002880191f;  // sqrt(0.5 * log2(e))
+  if (t < DMAX) cs[t] = (t < D) ? kHalfLog2e / ls[n_ls == 1 ? 0 : t] : 0.f;
+  __syncthreads();
+  for (int i = t; i < 256 * DMAX; i += kRbfThreads) {
+    const int rr = i / DMAX, d = i % DMAX;
+    const int64_t m = m0 + rr;
+    zs[rr][d] = (m < M && d < D) ? Z[m * ldz + d] * cs[d] : 0.f;
+  }
+  float xs[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) xs[d] = (n < N && d < D) ? X[n * ldx + d] * cs[d] : 0.f;
+  const float var = variance[0];
+  __syncthreads();
+  const int nk = (nmk - mk0) < 16 ? (nmk - mk0) : 16;
+  bf16x8* dst = Kfr + ((nb * nmk + mk0) * 3) * 64 + lane;
+  for (int q = 0; q < nk; ++q) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 16 * q + kperm(h, j);
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        const float diff = zs[row][d] - xs[d];
+        acc = fmaf(diff, diff, acc);
+      }
+      v[j] = (m0 + row < M && n < N) ? var * exp2f(-acc) : 0.f;
+    }
+    store_split(dst + q * 3 * 64, v);
+  }
+}
+
 static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
                       int D, const float* variance, const float* ls, int n_ls, float jitter, float* out,
                       int64_t ldo, hipStream_t stream) {
@@ -142,4 +191,44 @@ extern "C" int mgp_rbf_kuu(const float* Z, int64_t ldz, int64_t M, int32_t D, co
   if (ldk % 4 || !aligned16(Kuu)) return MGP_ERR_ALIGN;
   return rbf_launch(Z, ldz, Z, ldz, M, M, D, variance, lengthscales, n_ls, jitter, Kuu, ldk,
                     (hipStream_t)stream);
+}
+
+extern "C" size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
+
+extern "C" int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                              int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                              void* Kfr, size_t kfr_bytes, mgp_stream_t stream) {
+  if (!X) return -1;
+  if (ldx < D) return -2;
+  if (!Z) return -3;
+  if (ldz < D) return -4;
+  if (N < 0) return -5;
+  if (M < 0) return -6;
+  if (D < 1) return -7;
+  if (D > 32) return MGP_ERR_UNSUPPORTED;
+  if (!variance) return -8;
+  if (!lengthscales) return -9;
+  if (n_ls != 1 && n_ls != D) return -10;
+  if (!Kfr) return -11;
+  if (N == 0 || M == 0) return MGP_OK;
+  if (kfr_bytes < mgp_x6_cols_bytes(M, N)) return -12;
+  if (!aligned16(Kfr)) return MGP_ERR_ALIGN;
+  const int64_t Mp = (M + 127) / 128 * 128, Np = (N + 255) / 256 * 256;
+  const int nmk = (int)(Mp / 16);
+  const dim3 grid((unsigned)(Np / 128), (unsigned)((nmk + 15) / 16)), block(kRbfThreads);
+  hipStream_t s = (hipStream_t)stream;
+#define MGP_RBF_X6_CASE(DM)                                                                          \
+  if (D <= DM) {                                                                                     \
+    hipLaunchKernelGGL(rbf_kuf_x6_kernel<DM>, grid, block, 0, s, X, ldx, Z, ldz, N, M, D, variance,  \
+                       lengthscales, n_ls, nmk, (bf16x8*)Kfr);                                       \
+    return launch_status();                                                                          \
+  }
+  MGP_RBF_X6_CASE(1)
+  MGP_RBF_X6_CASE(2)
+  MGP_RBF_X6_CASE(4)
+  MGP_RBF_X6_CASE(8)
+  MGP_RBF_X6_CASE(16)
+  MGP_RBF_X6_CASE(32)
+#undef MGP_RBF_X6_CASE
+  return MGP_ERR_UNSUPPORTED;
 }

@@ -46,26 +46,31 @@ constexpr int kX6BM = 128;   // rows m' per item
 constexpr int kX6BN = 256;   // columns n per item
 constexpr int kFragBytes = 1024;
 
-// One wave per fragment block (k, mb, mk): grid.x = K * nmb * nmk / 4 (4 waves per block).
-__global__ __launch_bounds__(256) void split_lower_kernel(const float* __restrict__ q_sqrt, int64_t ldqs,
-                                                          int64_t strideq, int64_t M, int nmb, int nmk,
-                                                          int64_t nfrag, bf16x8* __restrict__ Lfr) {
+// A-operand image of a batch of triangular matrices: element (k-row m, row m')
+// = S_b[m][m'] kept where m >= m' (LOWER: L_k = tril(q_sqrt[k]), K5) or m <= m'
+// (upper: LinvT, K4's T[k][i] = L^-T[k][i]).  One wave per fragment block
+// (b, mb, mk): grid.x = batch * nmb * nmk / 4.
+template <bool LOWER>
+__global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict__ src, int64_t ld,
+                                                        int64_t stride, int64_t M, int nmb, int nmk,
+                                                        int64_t nfrag, bf16x8* __restrict__ img) {
   const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= nfrag) return;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int mk = (int)(f % nmk);
   const int64_t kb = f / nmk;
   const int mb = (int)(kb % nmb);
-  const int k = (int)(kb / nmb);
+  const int b = (int)(kb / nmb);
   const int64_t mc = 32 * (int64_t)mb + r;
-  const float* L = q_sqrt + (int64_t)k * strideq;
+  const float* S = src + (int64_t)b * stride;
   float v[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int64_t m = 16 * (int64_t)mk + kperm(h, j);
-    v[j] = (m < M && mc < M && m >= mc) ? L[m * ldqs + mc] : 0.f;
+    const bool keep = LOWER ? (m >= mc) : (m <= mc);
+    v[j] = (m < M && mc < M && keep) ? S[m * ld + mc] : 0.f;
   }
-  store_split(Lfr + f * 3 * 64 + lane, v);
+  store_split(img + f * 3 * 64 + lane, v);
 }
 
 // One wave per fragment block (nb, mk): grid.x = nnb * nmk / 4.
@@ -123,38 +128,29 @@ __device__ __forceinline__ void x6_item(int b, int nTn, int K, int& t, int& tn, 
   }
 }
 
-__global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
-                                                                const bf16x8* __restrict__ Lfr,
-                                                                uint32_t afr_bytes, uint32_t lfr_bytes,
-                                                                int nmk, int nmb, int nTn, int K,
-                                                                int64_t N, float* __restrict__ part,
-                                                                int64_t ldp) {
-  __shared__ bf16x8 sL[2][4 * 3 * 64];  // 2 x 12 KiB: [row sub-tile][plane][lane]
-  int t, tn, k;
-  x6_item(blockIdx.x, nTn, K, t, tn, k);
-  const int nTp = nmb / 4;
+// Main loop shared by K4 and K5: acc[i][c] (row sub-tile i = 0..3 of the
+// 128-row tile, column sub-tile c = 0..1 of this wave's 64 columns) +=
+// sum over k-steps mk in [mk_begin, mk_end) (even count) of T-image blocks
+// (4 t + i, mk) x B-image blocks (nb0 + c, mk).  T fragments are staged in LDS
+// (shared by the 4 waves), B fragments go global -> registers one k-step ahead.
+//   tbase: byte offset of T block (mb = 4 t, mk = 0) of this matrix
+//   sB0:   byte offset of B block (nb0, mk = 0)
+__device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[4 * 3 * 64],
+                                            __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
+                                            __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
+                                            int mk_end, int nmk) {
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mk0 = 8 * t, nks = nmk - mk0;
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Afr, (short)0, (int)afr_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc((void*)Lfr, (short)0, (int)lfr_bytes, 0x00020000);
-  // A fragments of this wave: column blocks nb = 8 tn + 2 w + c, k-step mk, plane p
-  //   byte offset ((nb * nmk + mk) * 3 + p) * 1 KiB + 16 lane
-  const uint32_t vA = 16u * lane;
-  const uint32_t sA0 = (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes;
-  const uint32_t sA1 = sA0 + (uint32_t)nmk * 3u * kFragBytes;
-  // L stage: 768 16-B units per k-step, 3 per thread: unit e = tid + 256 s ->
+  const uint32_t vB = 16u * lane;
+  const uint32_t sB1 = sB0 + (uint32_t)nmk * 3u * kFragBytes;
+  // T stage: 768 16-B units per k-step, 3 per thread: unit e = tid + 256 s ->
   //   row sub-tile i = e / 192, rest = e % 192 (= p * 64 + lane)
-  //   byte offset (((k * nmb + 4 t + i) * nmk + mk) * 192 + rest) * 16
-  uint32_t vL[3];
+  //   byte offset tbase + ((i * nmk + mk) * 192 + rest) * 16
+  uint32_t vT[3];
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
     const int e = tid + 256 * s;
-    vL[s] = (uint32_t)(((e / 192) * nmk * 192 + (e % 192)) * 16);
+    vT[s] = (uint32_t)(((e / 192) * nmk * 192 + (e % 192)) * 16);
   }
-  const uint32_t sLbase = (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 192u * 16u;
-
-  floatx16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -162,20 +158,20 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][c][e] = 0.f;
 
-  auto load_a = [&](bf16x8 (&b)[2][3], int mk) {
+  auto load_b = [&](bf16x8 (&b)[2][3], int mk) {
     const uint32_t o = (uint32_t)mk * 3u * kFragBytes;
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-      b[0][p] = ld_frag(rA, vA, sA0 + o + p * kFragBytes);
-      b[1][p] = ld_frag(rA, vA, sA1 + o + p * kFragBytes);
+      b[0][p] = ld_frag(rB, vB, sB0 + o + p * kFragBytes);
+      b[1][p] = ld_frag(rB, vB, sB1 + o + p * kFragBytes);
     }
   };
-  auto load_l = [&](u32x4v (&st)[3], int mk) {
-    const uint32_t o = sLbase + (uint32_t)mk * 192u * 16u;
+  auto load_t = [&](u32x4v (&st)[3], int mk) {
+    const uint32_t o = tbase + (uint32_t)mk * 192u * 16u;
 #pragma unroll
-    for (int s = 0; s < 3; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rL, vL[s], o, 0);
+    for (int s = 0; s < 3; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s], o, 0);
   };
-  auto store_l = [&](int buf, const u32x4v (&st)[3]) {
+  auto store_t = [&](int buf, const u32x4v (&st)[3]) {
 #pragma unroll
     for (int s = 0; s < 3; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
   };
@@ -192,26 +188,47 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
 
   bf16x8 b0[2][3], b1[2][3];
   u32x4v st[3];
-  load_l(st, mk0);
-  load_a(b0, mk0);
-  store_l(0, st);
+  load_t(st, mk_begin);
+  load_b(b0, mk_begin);
+  store_t(0, st);
   __syncthreads();
-  // two k-steps per iteration (nks is even): buffers and fragment sets alternate
+  // two k-steps per iteration: LDS buffers and fragment sets alternate
 #pragma nounroll
-  for (int q = 0; q < nks; q += 2) {
-    const int m1 = mk0 + q + 1;
-    load_l(st, m1);
-    load_a(b1, m1);
+  for (int mk = mk_begin; mk < mk_end; mk += 2) {
+    load_t(st, mk + 1);
+    load_b(b1, mk + 1);
     compute(0, b0);
-    store_l(1, st);
+    store_t(1, st);
     __syncthreads();
-    const int m2 = mk0 + q + 2 < nmk ? mk0 + q + 2 : nmk - 1;  // last pair: harmless reload
-    load_l(st, m2);
-    load_a(b0, m2);
+    const int m2 = mk + 2 < nmk ? mk + 2 : nmk - 1;  // after the last pair: harmless reload
+    load_t(st, m2);
+    load_b(b0, m2);
     compute(1, b1);
-    store_l(0, st);
+    store_t(0, st);
     __syncthreads();
   }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+
+// ------------------------------------------------------------------ K5 (x6)
+__global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
+                                                                const bf16x8* __restrict__ Lfr,
+                                                                uint32_t afr_bytes, uint32_t lfr_bytes,
+                                                                int nmk, int nmb, int nTn, int K,
+                                                                int64_t N, float* __restrict__ part,
+                                                                int64_t ldp) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];  // 2 x 12 KiB: [row sub-tile][plane][lane]
+  int t, tn, k;
+  x6_item(blockIdx.x, nTn, K, t, tn, k);
+  const int nTp = nmb / 4;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  floatx16 acc[4][2];
+  x6_mainloop(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+              img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
   const int64_t nbase = (int64_t)tn * kX6BN + 64 * w + (lane & 31);
@@ -226,6 +243,98 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
     s += __shfl_xor(s, 32, 64);
     const int64_t n = nbase + 32 * c;
     if (lane < 32 && n < N) dst[n] = s;
+  }
+}
+
+// ------------------------------------------------------------------ K4 (x6)
+// A = LinvT^T Kuf from the images Tfr (LinvT, upper) and Kfr (Kuf): item =
+// (row tile t of 128 rows, heavy = large t first; column tile tn of 256), the
+// 16 k-steps... 8 t + 8 k-steps of the lower triangle.  Epilogue: the A image
+// (registers 8 s .. 8 s + 7 of each 32x32 tile are one B fragment of K5) and
+// the stats of the two 64-row stats tiles 2 t, 2 t + 1 (same layout as the
+// f32 K4: stats[st][0][n] = sum A^2, stats[st][1 + kk][n] = sum A q_mu[., kk]).
+template <int KMAX>
+__global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
+    const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
+    int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
+    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];
+  const int nT = nmk / 8;
+  int t, tn;
+  {
+    const int b = blockIdx.x;
+    if (nTn % 8 == 0) {  // the row tiles of one column tile share an XCD (its Kuf slab in L2)
+      const int x = b & 7, j = b >> 3, per = nTn / 8;
+      t = nT - 1 - j / per;
+      tn = (j % per) * 8 + x;
+    } else {
+      t = nT - 1 - b / nTn;
+      tn = b % nTn;
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nmb = nmk / 2;
+  floatx16 acc[4][2];
+  x6_mainloop(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
+              img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8,
+              nmk);
+  (void)nmb;
+
+  // ---- A image
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int64_t nb = 8 * (int64_t)tn + 2 * w + c;
+      const int64_t mk = 8 * (int64_t)t + 2 * i;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s + j];
+        store_split(Afr + ((nb * nmk + mk + s) * 3) * 64 + lane, v);
+      }
+    }
+  // ---- stats (rows beyond M are zero in A; tiles starting at or beyond M are not stored)
+  const int64_t i0 = 128 * (int64_t)t;
+  float* sQ = reinterpret_cast<float*>(&sL[0][0]);  // [128][KMAX]; the main loop ended on a barrier
+  for (int idx = threadIdx.x; idx < 128 * KMAX; idx += 256) {
+    const int r = idx / KMAX, kk = idx % KMAX;
+    sQ[idx] = (i0 + r < M && kk < K) ? q_mu[(i0 + r) * ldq + kk] : 0.f;
+  }
+  __syncthreads();
+  // one (column sub-tile, stats tile) at a time keeps 1 + KMAX accumulators live
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int64_t n = (int64_t)tn * kX6BN + 64 * w + 32 * c + (lane & 31);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      float a2 = 0.f, qm[KMAX];
+#pragma unroll
+      for (int kk = 0; kk < KMAX; ++kk) qm[kk] = 0.f;
+#pragma unroll
+      for (int i = 2 * hh; i < 2 * hh + 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int lr = 32 * i + acc_row(e, lane);
+          const float v = acc[i][c][e];
+          a2 = fmaf(v, v, a2);
+#pragma unroll
+          for (int kk = 0; kk < KMAX; ++kk) qm[kk] = fmaf(v, sQ[lr * KMAX + kk], qm[kk]);
+        }
+      a2 += __shfl_xor(a2, 32, 64);
+#pragma unroll
+      for (int kk = 0; kk < KMAX; ++kk) qm[kk] += __shfl_xor(qm[kk], 32, 64);
+      const int64_t st = 2 * (int64_t)t + hh;
+      if (lane < 32 && n < N && 64 * st < M) {
+        float* dst = stats + st * (K + 1) * lds_ + n;
+        dst[0] = a2;
+#pragma unroll
+        for (int kk = 0; kk < KMAX; ++kk)
+          if (kk < K) dst[(int64_t)(1 + kk) * lds_] = qm[kk];
+      }
+    }
   }
 }
 
@@ -261,8 +370,25 @@ extern "C" int mgp_split_lower_x6(const float* q_sqrt, int64_t ldqs, int64_t str
   const int64_t Mp = x6_mp(M);
   const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
   const int64_t nfrag = (int64_t)K * nmb * nmk;
-  hipLaunchKernelGGL(split_lower_kernel, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                     q_sqrt, ldqs, strideq, M, nmb, nmk, nfrag, (bf16x8*)Lfr);
+  hipLaunchKernelGGL(split_tri_kernel<true>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, q_sqrt, ldqs, strideq, M, nmb, nmk, nfrag, (bf16x8*)Lfr);
+  return launch_status();
+}
+
+extern "C" int mgp_split_upper_x6(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, size_t tfr_bytes,
+                                  mgp_stream_t stream) {
+  if (!LinvT) return -1;
+  if (ldl < M) return -2;
+  if (M < 0) return -3;
+  if (!Tfr) return -4;
+  if (M == 0) return MGP_OK;
+  if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(Tfr)) return MGP_ERR_ALIGN;
+  const int64_t Mp = x6_mp(M);
+  const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
+  const int64_t nfrag = (int64_t)nmb * nmk;
+  hipLaunchKernelGGL(split_tri_kernel<false>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, LinvT, ldl, (int64_t)0, M, nmb, nmk, nfrag, (bf16x8*)Tfr);
   return launch_status();
 }
 
@@ -322,4 +448,45 @@ extern "C" int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, cons
   if (st) return st;
   return mgp_launch_cond_finalize(stats, lds, mgp_stats_tiles(M), part, ldp, nTp, variance, N, K, fmean, fvar,
                                   ldf, s);
+}
+
+template <int KMAX>
+static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb, int64_t M, int64_t N,
+                          const float* q_mu, int64_t ldq, int K, void* Afr, float* stats, int64_t lds,
+                          hipStream_t s) {
+  const int64_t Mp = x6_mp(M);
+  const int nmk = (int)(Mp / 16), nT = (int)(Mp / kX6BM), nTn = (int)(x6_np(N) / kX6BN);
+  hipLaunchKernelGGL(trsm_stats_x6_kernel<KMAX>, dim3((unsigned)(nT * nTn)), dim3(256), 0, s,
+                     (const bf16x8*)Tfr, (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu,
+                     ldq, K, (bf16x8*)Afr, stats, lds);
+  return launch_status();
+}
+
+extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes,
+                                 int64_t M, int64_t N, const float* q_mu, int64_t ldq, int32_t K,
+                                 void* Afr, size_t afr_bytes, float* stats, int64_t lds,
+                                 mgp_stream_t stream) {
+  if (!Tfr) return -1;
+  if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return -2;
+  if (!Kfr) return -3;
+  if (kfr_bytes < mgp_x6_cols_bytes(M, N)) return -4;
+  if (M < 0) return -5;
+  if (N < 0) return -6;
+  if (!q_mu) return -7;
+  if (ldq < K) return -8;
+  if (K < 1) return -9;
+  if (K > 16) return MGP_ERR_UNSUPPORTED;
+  if (!Afr) return -10;
+  if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -11;
+  if (!stats) return -12;
+  if (lds < N) return -13;
+  if (!aligned16(Tfr) || !aligned16(Kfr) || !aligned16(Afr)) return MGP_ERR_ALIGN;
+  if (mgp_x6_cols_bytes(M, N) >= ((size_t)1 << 32) || mgp_x6_lower_bytes(M, 1) >= ((size_t)1 << 32))
+    return MGP_ERR_UNSUPPORTED;
+  if (M == 0 || N == 0) return MGP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t tb = mgp_x6_lower_bytes(M, 1), kb = mgp_x6_cols_bytes(M, N);
+  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, s);
+  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, s);
+  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, s);
 }

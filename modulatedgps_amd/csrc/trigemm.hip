@@ -195,12 +195,10 @@ template <int BM, int BN, int KMAX, bool GUARD>
 __global__ __launch_bounds__((TgCfg<BM, BN>::THREADS), (TgCfg<BM, BN>::THREADS / 256)) void trsm_stats_kernel(
     const float* __restrict__ LinvT, int64_t ldl, const float* __restrict__ Kuf, int64_t ldk,
     int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
-    float* __restrict__ A, int64_t lda, float* __restrict__ stats, int64_t lds_,
-    bf16x8* __restrict__ Afr, int nmk, int nTm, int nTn) {
+    float* __restrict__ A, int64_t lda, float* __restrict__ stats, int64_t lds_) {
   using G = TriGemm<BM, BN, false, GUARD>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  // grid = nTm x nTn tiles (nTm, nTn may extend past M, N to cover the padded
-  // split-bf16 image; such tiles compute zeros and skip the stats)
+  const int nTm = (int)((M + BM - 1) / BM), nTn = (int)((N + BN - 1) / BN);
   const int tm = nTm - 1 - (int)(blockIdx.x / nTn);
   const int tn = (int)(blockIdx.x % nTn);
   const int64_t i0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
@@ -220,28 +218,9 @@ __global__ __launch_bounds__((TgCfg<BM, BN>::THREADS), (TgCfg<BM, BN>::THREADS /
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int64_t row = i0 + G::tile_row(wr, r) + acc_row(e, lane);
-        if (A && (!GUARD || (row < M && col < N))) A[row * lda + col] = acc[r][c][e];
+        if (!GUARD || (row < M && col < N)) A[row * lda + col] = acc[r][c][e];
       }
     }
-  // ---- split-bf16 image of A: registers 8s..8s+7 of a 32x32 tile are the
-  // fragment of k-step (row0 / 16 + s) for column block col0 / 32 (split3.hip)
-  if (Afr) {
-#pragma unroll
-    for (int r = 0; r < G::RT; ++r)
-#pragma unroll
-      for (int c = 0; c < G::CT; ++c) {
-        const int64_t nb = (n0 + wc * G::WN + 32 * c) / 32;
-        const int64_t mk = (i0 + G::tile_row(wr, r)) / 16;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = acc[r][c][8 * s + j];
-          store_split(Afr + ((nb * nmk + mk + s) * 3) * 64 + lane, v);
-        }
-      }
-  }
-  if (i0 >= M) return;  // padding tile of the image
   // ---- stats: stage q_mu rows of this tile (zero beyond M / K)
   float* sQ = lds;                       // [BM][KMAX]
   float* sRed = lds + BM * KMAX;         // [WR][KMAX + 1][BN]
@@ -412,52 +391,30 @@ extern "C" int mgp_stats_tiles(int64_t M) { return (int)((M + kTgBM - 1) / kTgBM
 template <int BN, int KMAX>
 static int launch_trsm(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M,
                        int64_t N, const float* q_mu, int64_t ldq, int K, float* A, int64_t lda,
-                       float* stats, int64_t lds, void* Afr, hipStream_t s) {
+                       float* stats, int64_t lds, hipStream_t s) {
   constexpr int BM = kTgBM;
-  int nTm = (int)((M + BM - 1) / BM), nTn = (int)((N + BN - 1) / BN);
-  int nmk = 0;
-  bool pad = false;
-  if (Afr) {  // cover the whole padded image (rows to a multiple of 128, columns of 256)
-    const int64_t Mp = (M + 127) / 128 * 128, Np = (N + 255) / 256 * 256;
-    nmk = (int)(Mp / 16);
-    pad = (Mp / BM != nTm) || (Np / BN != nTn);
-    nTm = (int)(Mp / BM);
-    nTn = (int)(Np / BN);
-  }
+  const int nTm = (int)((M + BM - 1) / BM), nTn = (int)((N + BN - 1) / BN);
   const size_t shm = (size_t)TriGemm<BM, BN, false, false>::LDS_FLOATS * sizeof(float);
   const size_t shm2 = (size_t)(BM * KMAX + 2 * (KMAX + 1) * BN) * sizeof(float);
   const size_t sh = shm > shm2 ? shm : shm2;
   const dim3 grid(nTm * nTn), block(TgCfg<BM, BN>::THREADS);
-  if ((M % BM == 0) && (N % BN == 0) && !pad && !force_guard())
+  if ((M % BM == 0) && (N % BN == 0) && !force_guard())
     hipLaunchKernelGGL((trsm_stats_kernel<BM, BN, KMAX, false>), grid, block, sh, s, LinvT, ldl, Kuf, ldk,
-                       M, N, q_mu, ldq, K, A, lda, stats, lds, (bf16x8*)Afr, nmk, nTm, nTn);
+                       M, N, q_mu, ldq, K, A, lda, stats, lds);
   else
     hipLaunchKernelGGL((trsm_stats_kernel<BM, BN, KMAX, true>), grid, block, sh, s, LinvT, ldl, Kuf, ldk,
-                       M, N, q_mu, ldq, K, A, lda, stats, lds, (bf16x8*)Afr, nmk, nTm, nTn);
+                       M, N, q_mu, ldq, K, A, lda, stats, lds);
   return launch_status();
 }
 
 template <int BN>
 static int dispatch_trsm(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M,
                          int64_t N, const float* q_mu, int64_t ldq, int K, float* A, int64_t lda,
-                         float* stats, int64_t lds, void* Afr, hipStream_t s) {
-  if (K <= 4) return launch_trsm<BN, 4>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, Afr, s);
-  if (K <= 8) return launch_trsm<BN, 8>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, Afr, s);
-  if (K <= 16) return launch_trsm<BN, 16>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, Afr, s);
+                         float* stats, int64_t lds, hipStream_t s) {
+  if (K <= 4) return launch_trsm<BN, 4>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, s);
+  if (K <= 8) return launch_trsm<BN, 8>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, s);
+  if (K <= 16) return launch_trsm<BN, 16>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, s);
   return MGP_ERR_UNSUPPORTED;
-}
-
-static int trsm_checked(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk, int64_t M, int64_t N,
-                        const float* q_mu, int64_t ldq, int32_t K, float* A, int64_t lda, void* Afr,
-                        float* stats, int64_t lds, mgp_stream_t stream) {
-  if (ldl % 4 || ldk % 4 || (A && lda % 4) || lds % 4) return MGP_ERR_ALIGN;
-  if (!aligned16(LinvT) || !aligned16(Kuf) || (A && !aligned16(A)) || !aligned16(stats) || (Afr && !aligned16(Afr)))
-    return MGP_ERR_ALIGN;
-  if (M * ldk * 4 >= (int64_t)1 << 31 || M * ldl * 4 >= (int64_t)1 << 31) return MGP_ERR_UNSUPPORTED;
-  if (M == 0 || N == 0) return MGP_OK;
-  hipStream_t s = (hipStream_t)stream;
-  if (tg_bn(N) == 256) return dispatch_trsm<256>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, Afr, s);
-  return dispatch_trsm<128>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, Afr, s);
 }
 
 extern "C" int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk,
@@ -478,29 +435,13 @@ extern "C" int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf,
   if (lda < N) return -11;
   if (!stats) return -12;
   if (lds < N) return -13;
-  return trsm_checked(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, nullptr, stats, lds, stream);
-}
-
-extern "C" int mgp_trsm_stats_x6(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ldk,
-                                 int64_t M, int64_t N, const float* q_mu, int64_t ldq, int32_t K,
-                                 float* A, int64_t lda, void* Afr, size_t afr_bytes, float* stats,
-                                 int64_t lds, mgp_stream_t stream) {
-  if (!LinvT) return -1;
-  if (ldl < M) return -2;
-  if (!Kuf) return -3;
-  if (ldk < N) return -4;
-  if (M < 0) return -5;
-  if (N < 0) return -6;
-  if (!q_mu) return -7;
-  if (ldq < K) return -8;
-  if (K < 1) return -9;
-  if (K > 16) return MGP_ERR_UNSUPPORTED;
-  if (A && lda < N) return -11;
-  if (!Afr) return -12;
-  if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -13;
-  if (!stats) return -14;
-  if (lds < N) return -15;
-  return trsm_checked(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, Afr, stats, lds, stream);
+  if (ldl % 4 || ldk % 4 || lda % 4 || lds % 4) return MGP_ERR_ALIGN;
+  if (!aligned16(LinvT) || !aligned16(Kuf) || !aligned16(A) || !aligned16(stats)) return MGP_ERR_ALIGN;
+  if (M * ldk * 4 >= (int64_t)1 << 31 || M * ldl * 4 >= (int64_t)1 << 31) return MGP_ERR_UNSUPPORTED;
+  if (M == 0 || N == 0) return MGP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (tg_bn(N) == 256) return dispatch_trsm<256>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, s);
+  return dispatch_trsm<128>(LinvT, ldl, Kuf, ldk, M, N, q_mu, ldq, K, A, lda, stats, lds, s);
 }
 
 int mgp::mgp_launch_cond_finalize(const float* stats, int64_t lds, int nTs, const float* part, int64_t ldp,

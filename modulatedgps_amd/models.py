@@ -9,12 +9,14 @@ arguments and method names).  The SMGP ELBO hot path
     K3 mgp_potrf_trtri      L, L^-1 (both layers    models.py:141 (cholesky)
                             batched in one sweep)
     K1 mgp_rbf_kuf          Kuf [M, N]              models.py:139
-    K4 mgp_trsm_stats_x6    A = L^-1 Kuf + stats    models.py:141-143 (triangular_solve, A^T q_mu)
-                            (A as a split-bf16 image)
-    K5 mgp_split_lower_x6 + mgp_expert_conditional_x6
-                            fmean, fvar [K, N]      models.py:141-143 (LTA, fvar)
-    (config.set_conditional_mode("f32"): K4 mgp_trsm_stats + K5 mgp_expert_conditional
-     on the exact-f32 MFMA instead)
+    (default "x6" mode: K1 writes Kuf as a split-bf16 image, K4/K5 run on the
+     bf16 matrix cores with f32 accuracy -- csrc/split3.hip)
+    K1 mgp_rbf_kuf_x6       Kuf image               models.py:139
+       mgp_split_upper_x6 / mgp_split_lower_x6   images of L^-T and tril(q_sqrt)
+    K4 mgp_trsm_stats_x6    A image + stats         models.py:141-143 (triangular_solve, A^T q_mu)
+    K5 mgp_expert_conditional_x6  fmean, fvar [K, N]  models.py:141-143 (LTA, fvar)
+    (config.set_conditional_mode("f32"): K1 mgp_rbf_kuf + K4 mgp_trsm_stats +
+     K5 mgp_expert_conditional on the exact-f32 MFMA instead)
     K7 mgp_gauss_kl_white   KL                      models.py:79 (prior_kl)
   K6 mgp_elbo_terms         sum_n lse_s(...)        models.py:55-67,73-76
   mgp_elbo_combine          ELBO scalar             models.py:76,79
@@ -157,9 +159,14 @@ class SVGPModified:
             self._last_info = info
             LinvT = LinvT[0]
         bufs = bufs or {}
-        with _Stage(timing, "rbf_kuf"):
-            Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
-                              out=bufs.get("Kuf"))
+        if conditional_mode() == "x6":
+            with _Stage(timing, "rbf_kuf"):
+                Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
+                                     out=bufs.get("Kfr"))
+        else:
+            with _Stage(timing, "rbf_kuf"):
+                Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
+                                  out=bufs.get("Kuf"))
         if conditional_mode() == "f32":
             with _Stage(timing, "trsm_stats"):
                 A, stats = ops.trsm_stats(LinvT, Kuf, self.q_mu, A=bufs.get("A"),
@@ -169,11 +176,12 @@ class SVGPModified:
                                               fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
                                               workspace=bufs.get("ws_expert"))
         M, N, K = self.num_inducing, X.shape[0], self.num_latent_gps
-        with _Stage(timing, "trsm_stats"):
-            Afr, stats = ops.trsm_stats_x6(LinvT, Kuf, self.q_mu, Afr=bufs.get("Afr"),
-                                           stats=bufs.get("stats"))
-        with _Stage(timing, "split_lower"):
+        with _Stage(timing, "split_tri"):
+            Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"))
             Lfr = ops.split_lower_x6(self.q_sqrt, out=bufs.get("Lfr"))
+        with _Stage(timing, "trsm_stats"):
+            Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, M, N, Afr=bufs.get("Afr"),
+                                           stats=bufs.get("stats"))
         with _Stage(timing, "expert_cond"):
             return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, K,
                                              fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
@@ -246,13 +254,13 @@ class SMGP(SGP):
         Mf, Ma, K = self.pred_layer.num_inducing, self.assign_layer.num_inducing, self.K
         Mx = max(Mf, Ma)
         T = ops.stats_tiles(Mx)
-        kuf = ops.padded(Mx, N, dev)
         x6 = conditional_mode() == "x6"
+        kuf = None if x6 else ops.padded(Mx, N, dev)
         a = None if x6 else ops.padded(Mx, N, dev)
         st = ops.padded(T * (K + 1), N, dev)
         cond = ops.padded(4 * K, N, dev)          # mu_f, var_f, mu_a, var_a
         b = {
-            "Kuf_f": kuf[:Mf], "Kuf_a": kuf[:Ma],
+            "Kuf_f": None if x6 else kuf[:Mf], "Kuf_a": None if x6 else kuf[:Ma],
             "A_f": None if x6 else a[:Mf], "A_a": None if x6 else a[:Ma],
             "stats_f": st[:ops.stats_tiles(Mf) * (K + 1)].unflatten(0, (-1, K + 1)),
             "stats_a": st[:ops.stats_tiles(Ma) * (K + 1)].unflatten(0, (-1, K + 1)),
@@ -267,7 +275,9 @@ class SMGP(SGP):
                                      device=dev),
         }
         if x6:  # split-bf16 images, shared by the two layers (processed in turn)
+            b["Kfr"] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
             b["Afr"] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
+            b["Tfr"] = torch.empty(ops.x6_lower_bytes(Mx, 1), dtype=torch.uint8, device=dev)
             b["Lfr"] = torch.empty(ops.x6_lower_bytes(Mx, K), dtype=torch.uint8, device=dev)
         b["x6"] = x6
         if Mf == Ma and self.pred_layer.Z.shape[1] == self.assign_layer.Z.shape[1]:
@@ -303,7 +313,8 @@ class SMGP(SGP):
         b = self._buffers(N)
         with _Stage(timing, "kuu_chol"):
             LinvT_f, LinvT_a = self._factorise(b)
-        shared = {"ws_expert": b["ws_expert"], "Afr": b.get("Afr"), "Lfr": b.get("Lfr")}
+        shared = {"ws_expert": b["ws_expert"], "Afr": b.get("Afr"), "Lfr": b.get("Lfr"),
+                  "Kfr": b.get("Kfr"), "Tfr": b.get("Tfr")}
         self.pred_layer.conditional_kn(X, LinvT_f, bufs={"Kuf": b["Kuf_f"], "A": b["A_f"],
                                                          "stats": b["stats_f"], "fmean": b["mu_f"],
                                                          "fvar": b["var_f"], **shared}, timing=timing)

@@ -186,22 +186,43 @@ def trsm_stats(LinvT, Kuf, q_mu, A=None, stats=None):
     return A, stats
 
 
-def trsm_stats_x6(LinvT, Kuf, q_mu, Afr=None, stats=None, A=None):
-    """K4 writing the split-bf16 image Afr of A = L^-1 Kuf (and the stats; the f32
-    A only when `A` is given).  Returns (Afr, stats)."""
-    _check(LinvT, "LinvT", 2), _check(Kuf, "Kuf", 2), _check(q_mu, "q_mu", 2)
-    M, N = Kuf.shape
+def rbf_kuf_x6(X, Z, variance, lengthscales, out=None):
+    """K1 writing the split-bf16 image of Kuf = K(Z, X) (uint8 device tensor)."""
+    _check(X, "X", 2), _check(Z, "Z", 2)
+    N, D = X.shape
+    M = Z.shape[0]
+    nbytes = _lib.load().mgp_x6_cols_bytes(M, N)
+    if out is None or out.numel() < nbytes:
+        out = _ws(nbytes, X.device)
+    _lib.call("mgp_rbf_kuf_x6", X.data_ptr(), _ld(X), Z.data_ptr(), _ld(Z), N, M, D, variance.data_ptr(),
+              lengthscales.data_ptr(), lengthscales.numel(), out.data_ptr(), out.numel(), _stream())
+    return out
+
+
+def split_upper_x6(LinvT, out=None):
+    """Split-bf16 image of (L^-1)^T [M, M] (upper triangle) as K4's T operand."""
+    _check(LinvT, "LinvT", 2)
+    M = LinvT.shape[0]
+    nbytes = _lib.load().mgp_x6_lower_bytes(M, 1)
+    if out is None or out.numel() < nbytes:
+        out = _ws(nbytes, LinvT.device)
+    _lib.call("mgp_split_upper_x6", LinvT.data_ptr(), _ld(LinvT), M, out.data_ptr(), out.numel(), _stream())
+    return out
+
+
+def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None):
+    """K4 on images: A's image (for expert_conditional_x6) and the stats [T, K+1, N]."""
+    _check(q_mu, "q_mu", 2)
     K = q_mu.shape[1]
-    dev = Kuf.device
+    dev = q_mu.device
     nbytes = _lib.load().mgp_x6_cols_bytes(M, N)
     if Afr is None or Afr.numel() < nbytes:
         Afr = _ws(nbytes, dev)
     if stats is None:
         T = stats_tiles(M)
         stats = padded(T * (K + 1), N, dev).unflatten(0, (T, K + 1))
-    _lib.call("mgp_trsm_stats_x6", LinvT.data_ptr(), _ld(LinvT), Kuf.data_ptr(), _ld(Kuf), M, N,
-              q_mu.data_ptr(), _ld(q_mu), K, A.data_ptr() if A is not None else None,
-              _ld(A) if A is not None else N, Afr.data_ptr(), Afr.numel(), stats.data_ptr(), _ld(stats),
+    _lib.call("mgp_trsm_stats_x6", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
+              q_mu.data_ptr(), _ld(q_mu), K, Afr.data_ptr(), Afr.numel(), stats.data_ptr(), _ld(stats),
               _stream())
     return Afr, stats
 

@@ -51,3 +51,19 @@ def to_np(t):
 def dev_noise(z, u, device):
     return (torch.as_tensor(z, dtype=torch.float32, device=device),
             torch.as_tensor(u, dtype=torch.float32, device=device))
+
+
+def decode_cols_image(img, M, N):
+    """Split-bf16 column image (modulatedgps_amd/csrc/split3.hip layout
+    [nb][mk][plane][lane][8]) -> float64 [M, N] = hi + mid + lo."""
+    Mp, Np = -(-M // 128) * 128, -(-N // 256) * 256
+    nb, nmk = Np // 32, Mp // 16
+    u16 = img.detach().cpu().numpy().view(np.uint16)[: nb * nmk * 3 * 64 * 8].reshape(nb, nmk, 3, 64, 8)
+    f = (u16.astype(np.uint32) << 16).view(np.float32).astype(np.float64).sum(axis=2)  # [nb][mk][64][8]
+    lane, j = np.arange(64), np.arange(8)
+    kp = (j[None, :] & 3) + 8 * (j[None, :] >> 2) + 4 * (lane[:, None] >> 5)          # [64][8]
+    rows = 16 * np.arange(nmk)[None, :, None, None] + kp[None, None]
+    cols = 32 * np.arange(nb)[:, None, None, None] + (lane & 31)[None, None, :, None]
+    out = np.zeros((Mp, Np))
+    out[np.broadcast_to(rows, f.shape), np.broadcast_to(cols, f.shape)] = f
+    return out[:M, :N]

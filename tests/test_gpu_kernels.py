@@ -228,23 +228,47 @@ def test_split_bf16_layout_exact(device):
     assert np.array_equal(to_np(fv)[:, :N].astype(np.float64), ref)
 
 
-@pytest.mark.parametrize("N,M", [(8192, 256), (1000, 25), (777, 300), (4096, 1024)])
-def test_trsm_writes_split_image(device, N, M):
-    """K4's fused split-bf16 epilogue produces the same image (bit for bit) as
-    splitting its f32 A afterwards, including the zero padding."""
+@pytest.mark.parametrize("N,M,D,K", [(8192, 256, 2, 4), (1000, 25, 1, 3), (777, 300, 3, 16),
+                                     (4096, 1024, 8, 8)])
+def test_kuf_and_trsm_images(device, N, M, D, K):
+    """K1 -> Kuf image and K4 on images (x6).  Kuf: the decoded image equals the
+    f32 kernel's Kuf to the split's representation error.  A = L^-1 Kuf and the
+    stats: against float64 (oracle Kuu, LAPACK), the x6 error is no larger than
+    the exact-f32 MFMA K4's (A is ill-conditioned: cond(L) amplifies any
+    rounding, so "equal to the f32 kernel" is not a meaningful bound).  The
+    padding of the A image is zero."""
     from modulatedgps_amd import ops
-    X, Y, p = R.synthetic_problem(N, M, 3, 2, 0.7, state="perturbed", S=2)
+    from tests.helpers import decode_cols_image
+    X, Y, p = R.synthetic_problem(N, M, K, D, 0.7, state="perturbed", S=2)
     L = p.pred
-    _, LinvT, _ = ops.kuu_potrf_trtri([_t(L["Z"], device)], [_t([L["variance"]], device)],
-                                      [_t([0.7], device)], 1e-6)
-    Kuf = ops.rbf_kuf(_t(X, device), _t(L["Z"], device), _t([L["variance"]], device), _t([0.7], device))
+    Xt, Zt, var, ls = _t(X, device), _t(L["Z"], device), _t([L["variance"]], device), _t([0.7], device)
+    _, LinvT, _ = ops.kuu_potrf_trtri([Zt], [var], [ls], 1e-6)
+    Kuf = ops.rbf_kuf(Xt, Zt, var, ls)
     A, st = ops.trsm_stats(LinvT[0], Kuf, _t(L["q_mu"], device))
-    ref = ops.split_cols_x6(A)
-    A2 = ops.padded(M, N, device)
-    img = torch.full_like(ref, 0x7F)  # garbage: every byte must be written
-    img, st2 = ops.trsm_stats_x6(LinvT[0], Kuf, _t(L["q_mu"], device), Afr=img, A=A2)
-    assert torch.equal(img, ref)
-    assert torch.equal(st2, st)
-    assert torch.equal(A2, A)
-    img3, _ = ops.trsm_stats_x6(LinvT[0], Kuf, _t(L["q_mu"], device))
-    assert torch.equal(img3, ref)
+    Kfr = torch.full((ops.x6_cols_bytes(M, N),), 0x7F, dtype=torch.uint8, device=device)
+    Kfr = ops.rbf_kuf_x6(Xt, Zt, var, ls, out=Kfr)
+    kd = decode_cols_image(Kfr, M, N)
+    kf = to_np(Kuf)
+    assert np.max(np.abs(kd - kf)) <= 2.0 ** -22 * L["variance"]
+    Tfr = ops.split_upper_x6(LinvT[0])
+    Afr, st6 = ops.trsm_stats_x6(Tfr, Kfr, _t(L["q_mu"], device), M, N)
+    L64 = np.linalg.cholesky(R.rbf_Kuu(L["Z"].astype(np.float32).astype(np.float64), L["variance"], 0.7))
+    A64 = sla.solve_triangular(L64, R.rbf_K(L["Z"].astype(np.float32).astype(np.float64),
+                                            X.astype(np.float32).astype(np.float64), L["variance"], 0.7),
+                               lower=True)
+    e32 = normwise(to_np(A), A64)
+    e6 = normwise(decode_cols_image(Afr, M, N), A64)
+    assert e6 <= max(1.5 * e32, 2e-6), (e6, e32)
+    T = st.shape[0]
+    q64 = L["q_mu"].astype(np.float32).astype(np.float64)
+    ref = np.zeros((T, K + 1, N))
+    for t in range(T):
+        rows = slice(64 * t, min(64 * t + 64, M))
+        ref[t, 0] = np.sum(A64[rows] ** 2, axis=0)
+        ref[t, 1:] = q64[rows].T @ A64[rows]
+    s32 = normwise(to_np(st)[:, :, :N], ref)
+    s6 = normwise(to_np(st6)[:, :, :N], ref)
+    assert s6 <= max(1.5 * s32, 2e-6), (s6, s32)
+    Mp, Np = -(-M // 128) * 128, -(-N // 256) * 256
+    full = decode_cols_image(Afr, Mp, Np)
+    assert not full[M:].any() and not full[:, N:].any()

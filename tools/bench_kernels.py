@@ -48,7 +48,9 @@ def main():
     Kuf = ops.rbf_kuf(X, Z, var, lsc)
     A, stats = ops.trsm_stats(LinvT[0], Kuf, q_mu)
     fm, fv = ops.expert_conditional(A, q_sqrt, stats, var)
-    Afr = ops.split_cols_x6(A)
+    Kfr = ops.rbf_kuf_x6(X, Z, var, lsc)
+    Tfr = ops.split_upper_x6(LinvT[0])
+    Afr, st6 = ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N)
     Lfr = ops.split_lower_x6(q_sqrt)
     fm6, fv6 = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K)
     torch.cuda.synchronize()
@@ -57,7 +59,9 @@ def main():
         "rbf_kuf": lambda: ops.rbf_kuf(X, Z, var, lsc, out=Kuf),
         "trsm_stats": lambda: ops.trsm_stats(LinvT[0], Kuf, q_mu, A=A, stats=stats),
         "expert_cond": lambda: ops.expert_conditional(A, q_sqrt, stats, var, fmean=fm, fvar=fv),
-        "split_cols_x6": lambda: ops.split_cols_x6(A, out=Afr),
+        "rbf_kuf_x6": lambda: ops.rbf_kuf_x6(X, Z, var, lsc, out=Kfr),
+        "split_upper_x6": lambda: ops.split_upper_x6(LinvT[0], out=Tfr),
+        "trsm_stats_x6": lambda: ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Afr, stats=st6),
         "split_lower_x6": lambda: ops.split_lower_x6(q_sqrt, out=Lfr),
         "expert_cond_x6": lambda: ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmean=fm6, fvar=fv6),
     }
@@ -74,6 +78,10 @@ def main():
         out["expert_cond"]["tflops"] = K * M * M * N / (out["expert_cond"]["median_ms"] * 1e-3) / 1e12
     if "expert_cond_x6" in out:
         out["expert_cond_x6"]["tflops"] = K * M * M * N / (out["expert_cond_x6"]["median_ms"] * 1e-3) / 1e12
+    if "trsm_stats_x6" in out:
+        out["trsm_stats_x6"]["tflops"] = M * M * N / (out["trsm_stats_x6"]["median_ms"] * 1e-3) / 1e12
+    if "rbf_kuf_x6" in out:
+        out["rbf_kuf_x6"]["GBps"] = (4 * (N * D + M * D) + 6 * M * N) / (out["rbf_kuf_x6"]["median_ms"] * 1e-3) / 1e9
     if "trsm_stats" in out:
         out["trsm_stats"]["tflops"] = M * M * N / (out["trsm_stats"]["median_ms"] * 1e-3) / 1e12
     if "rbf_kuf" in out:
