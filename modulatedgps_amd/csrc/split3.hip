@@ -38,6 +38,8 @@
 // straight from global into registers one k-step ahead; 48 MFMAs per wave.
 // The triangle is exploited at row-tile granularity (k-steps start at 128 t);
 // the zero blocks inside the diagonal tile come from Lfr's zero fill.
+#include <type_traits>
+
 #include "mgp_common.hpp"
 
 namespace mgp {
@@ -135,6 +137,15 @@ __device__ __forceinline__ void x6_item(int b, int nTn, int K, int& t, int& tn, 
 // (shared by the 4 waves), B fragments go global -> registers one k-step ahead.
 //   tbase: byte offset of T block (mb = 4 t, mk = 0) of this matrix
 //   sB0:   byte offset of B block (nb0, mk = 0)
+template <int V>
+using ic = std::integral_constant<int, V>;
+
+// DIAG_FIRST (K5, T lower: block (mb, mk) zero for 16 mk + 15 < 32 mb): the
+// first 8 k-steps meet the diagonal and only sub-tiles i <= p of k-step pair p
+// are non-zero.  Otherwise (K4, T upper: zero for 16 mk > 32 mb + 31) the last
+// 8 k-steps do, with sub-tiles i >= p of pair p.  Those MFMAs are skipped
+// (8% of the work), everything else is unchanged.
+template <bool DIAG_FIRST>
 __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[4 * 3 * 64],
                                             __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
                                             __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
@@ -175,9 +186,10 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[
 #pragma unroll
     for (int s = 0; s < 3; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
   };
-  auto compute = [&](int buf, const bf16x8 (&b)[2][3]) {
+  auto compute = [&](int buf, const bf16x8 (&b)[2][3], auto ilo, auto ihi) {
+    constexpr int ILO = decltype(ilo)::value, IHI = decltype(ihi)::value;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = ILO; i < IHI; ++i) {
       bf16x8 a[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) a[p] = sL[buf][(i * 3 + p) * 64 + lane];
@@ -193,19 +205,39 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[
   store_t(0, st);
   __syncthreads();
   // two k-steps per iteration: LDS buffers and fragment sets alternate
-#pragma nounroll
-  for (int mk = mk_begin; mk < mk_end; mk += 2) {
+  // one pair of k-steps (mk, mk + 1) on sub-tiles [ilo, ihi); sched_barrier(0)
+  // pins the prefetch loads ahead of the MFMA block
+  auto pair = [&](int mk, auto ilo, auto ihi) {
     load_t(st, mk + 1);
     load_b(b1, mk + 1);
-    compute(0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0, b0, ilo, ihi);
+    __builtin_amdgcn_sched_barrier(0);
     store_t(1, st);
     __syncthreads();
     const int m2 = mk + 2 < nmk ? mk + 2 : nmk - 1;  // after the last pair: harmless reload
     load_t(st, m2);
     load_b(b0, m2);
-    compute(1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1, b1, ilo, ihi);
+    __builtin_amdgcn_sched_barrier(0);
     store_t(0, st);
     __syncthreads();
+  };
+  if constexpr (DIAG_FIRST) {
+    pair(mk_begin, ic<0>{}, ic<1>{});
+    pair(mk_begin + 2, ic<0>{}, ic<2>{});
+    pair(mk_begin + 4, ic<0>{}, ic<3>{});
+    pair(mk_begin + 6, ic<0>{}, ic<4>{});
+#pragma nounroll
+    for (int mk = mk_begin + 8; mk < mk_end; mk += 2) pair(mk, ic<0>{}, ic<4>{});
+  } else {
+#pragma nounroll
+    for (int mk = mk_begin; mk < mk_end - 8; mk += 2) pair(mk, ic<0>{}, ic<4>{});
+    pair(mk_end - 8, ic<0>{}, ic<4>{});
+    pair(mk_end - 6, ic<1>{}, ic<4>{});
+    pair(mk_end - 4, ic<2>{}, ic<4>{});
+    pair(mk_end - 2, ic<3>{}, ic<4>{});
   }
 }
 
@@ -227,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   floatx16 acc[4][2];
-  x6_mainloop(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+  x6_mainloop<true>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
               img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
@@ -276,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nmb = nmk / 2;
   floatx16 acc[4][2];
-  x6_mainloop(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
+  x6_mainloop<false>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
               img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8,
               nmk);
   (void)nmb;
