@@ -191,25 +191,36 @@ __device__ __forceinline__ double rcp_f64(double p) {
   return fma(r, fma(-p, r, 1.0), r);
 }
 
+// Quad-broadcast of a double from lane (4q + G) to lanes 4q..4q+3 (DPP quad_perm).
+template <int G>
+__device__ __forceinline__ double quad_bcast_f64(double v) {
+  constexpr int ctrl = G * 0x55;  // quad_perm [G, G, G, G]
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, ctrl, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), ctrl, 0xF, 0xF, true);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // Factor the symmetric 64x64 tile in sF (lower part used) in place: sF <- L
-// (zeros above), sX <- L^-1 (zeros above).  Wave 0 only; the other waves return.
+// (zeros above), sX <- L^-1 (zeros above).  Called by all 256 threads.
 //
-// Factorisation: square-root-free right-looking sweep.  Lane r keeps row r in
-// registers; at column c the pivot p_c is read from lane c, column c is
-// broadcast through LDS, and every lane updates a[s] -= (a[c]/p_c) a_s[c]
-// (s > c).  Afterwards L[r][c] = a[c] / sqrt(p_c) (c <= r).  The critical path
-// per column is one readlane, one reciprocal and one LDS round trip; no sqrt or
-// division sits on it.
-// Inverse: X = L^-1 by a right-looking forward substitution, lane c keeping
-// column c of X; column I of L is read as a broadcast from L^T staged in sX.
+// Factorisation (wave 0): square-root-free right-looking sweep.  Lane r keeps
+// row r in registers; at column c the pivot p_c is read from lane c, column c
+// is broadcast through LDS, and every lane updates a[s] -= (a[c]/p_c) a_s[c]
+// (s > c).  Afterwards L[r][c] = a[c] / sqrt(p_c) (c <= r).  No sqrt or
+// division sits on the per-column critical path.
+// Inverse (all 4 waves): X = L^-1 by right-looking forward substitution in a
+// quad layout: wave w, lane l owns column c = 16 w + (l >> 2) and rows
+// 16 g + k (g = l & 3, k = 0..15).  Step I scales x_I (held by group I >> 4),
+// broadcasts it across the quad with DPP and updates the 16 rows of every
+// lane with column I of L (read from L^T staged in sX, diagonal zeroed).
 // Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0) {
-  if (threadIdx.x >= 64) return;
-  const int r = threadIdx.x;
-  double* bc = sX;  // column broadcast buffer (row 0 of sX, free until L^T is staged)
-  int bad = 0;
-  {
+  if (threadIdx.x < 64) {
+    const int r = threadIdx.x;
+    double* bc = sX;  // column broadcast buffer (row 0 of sX, free until L^T is staged)
+    int bad = 0;
     double a[CB];
 #pragma unroll
     for (int t = 0; t < CB; ++t) a[t] = sF[r * LDT + t];
@@ -223,27 +234,43 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
 #pragma unroll
       for (int s = c + 1; s < CB; ++s) a[s] = fma(-t, bc[s], a[s]);
     }
-    // L = a[c] / sqrt(p_c) below and on the diagonal; stage L (row-major) and L^T.
+    // L = a[c] / sqrt(p_c) below and on the diagonal: stage L (row-major) and
+    // L^T with a zero diagonal (the inverse scales by col[] = 1 / L[c][c]).
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
       const double l = (c <= r) ? a[c] * col[c] : 0.0;
       sF[r * LDT + c] = l;
-      sX[c * LDT + r] = l;
+      sX[c * LDT + r] = (c < r) ? l : 0.0;
     }
+    if (bad && r == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
   }
-  if (bad && r == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
+  __syncthreads();
   STAMP((int)(gcol0 / CB) - 1, 5);
-  double x[CB];
+  const int lane = threadIdx.x & 63, g = lane & 3;
+  const int c = 16 * (threadIdx.x >> 6) + (lane >> 2);
+  double x[16];
 #pragma unroll
-  for (int t = 0; t < CB; ++t) x[t] = (t == r) ? 1.0 : 0.0;
+  for (int k = 0; k < 16; ++k) x[k] = (16 * g + k == c) ? 1.0 : 0.0;
+  const double* sT = sX + 16 * g;
 #pragma unroll
   for (int I = 0; I < CB; ++I) {
-    x[I] *= col[I];  // 1 / L[I][I]
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int GI = I >> 4, KI = I & 15;
+    double xi = x[KI] * col[I];
+    switch (GI) {  // compile-time after unrolling
+      case 0: xi = quad_bcast_f64<0>(xi); break;
+      case 1: xi = quad_bcast_f64<1>(xi); break;
+      case 2: xi = quad_bcast_f64<2>(xi); break;
+      default: xi = quad_bcast_f64<3>(xi); break;
+    }
+    if (g == GI) x[KI] = xi;
 #pragma unroll
-    for (int J = I + 1; J < CB; ++J) x[J] = fma(-sX[I * LDT + J], x[I], x[J]);
+    for (int k = 0; k < 16; ++k) x[k] = fma(-sT[I * LDT + k], xi, x[k]);
   }
+  __syncthreads();  // every wave is done reading L^T before X overwrites sX
 #pragma unroll
-  for (int i = 0; i < CB; ++i) sX[i * LDT + r] = x[i];
+  for (int k = 0; k < 16; ++k) sX[(16 * g + k) * LDT + c] = x[k];
 }
 
 // Write the factored diagonal tile j: L block (f32, guarded to M; optional) and D_j (f64).

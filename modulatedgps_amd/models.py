@@ -148,11 +148,25 @@ class SVGPModified:
         """GPflow SVGP.prior_kl -> gauss_kl(q_mu, q_sqrt) whitened (models.py:79); float64 [1]."""
         return ops.gauss_kl_white(self.q_mu, self.q_sqrt, out=out)
 
-    def conditional_kn(self, X, LinvT=None, bufs=None, timing=None):
+    def operand_images(self, X, bufs=None, timing=None):
+        """x6 mode: the split-bf16 images that do not depend on the Cholesky --
+        Kuf (K1) and tril(q_sqrt) -- so a caller can build them on a side
+        stream while K3 runs.  Returns (Kfr, Lfr)."""
+        bufs = bufs or {}
+        X = self.kernel._x(X)
+        with _Stage(timing, "rbf_kuf"):
+            Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
+                                 out=bufs.get("Kfr"))
+        with _Stage(timing, "split_tri"):
+            Lfr = ops.split_lower_x6(self.q_sqrt, out=bufs.get("Lfr"))
+        return Kfr, Lfr
+
+    def conditional_kn(self, X, LinvT=None, bufs=None, timing=None, images=None):
         """Whitened conditional for X [N, D]: fmean, fvar as expert-major [K, N] views.
 
         LinvT: (L^-1)^T of this layer's Kuu if already factorised (the SMGP
-        factorises both layers in one batched sweep)."""
+        factorises both layers in one batched sweep).  images: (Kfr, Lfr) from
+        operand_images (x6 mode), if already built."""
         X = self.kernel._x(X)
         if LinvT is None:
             _, LinvT, info = self.factorise()
@@ -160,9 +174,7 @@ class SVGPModified:
             LinvT = LinvT[0]
         bufs = bufs or {}
         if conditional_mode() == "x6":
-            with _Stage(timing, "rbf_kuf"):
-                Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
-                                     out=bufs.get("Kfr"))
+            Kfr, Lfr = images if images is not None else self.operand_images(X, bufs, timing)
         else:
             with _Stage(timing, "rbf_kuf"):
                 Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
@@ -178,7 +190,6 @@ class SVGPModified:
         M, N, K = self.num_inducing, X.shape[0], self.num_latent_gps
         with _Stage(timing, "split_tri"):
             Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"))
-            Lfr = ops.split_lower_x6(self.q_sqrt, out=bufs.get("Lfr"))
         with _Stage(timing, "trsm_stats"):
             Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, M, N, Afr=bufs.get("Afr"),
                                            stats=bufs.get("stats"))
@@ -274,11 +285,13 @@ class SMGP(SGP):
                                          ops.expert_x6_workspace_bytes(Mx, N, K)), dtype=torch.uint8,
                                      device=dev),
         }
-        if x6:  # split-bf16 images, shared by the two layers (processed in turn)
-            b["Kfr"] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
+        if x6:  # split-bf16 images: Kuf / tril(q_sqrt) per layer (built on the side
+            # stream while K3 runs), A and L^-T shared by the layers (processed in turn)
+            for L in ("f", "a"):
+                b["Kfr_" + L] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
+                b["Lfr_" + L] = torch.empty(ops.x6_lower_bytes(Mx, K), dtype=torch.uint8, device=dev)
             b["Afr"] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
             b["Tfr"] = torch.empty(ops.x6_lower_bytes(Mx, 1), dtype=torch.uint8, device=dev)
-            b["Lfr"] = torch.empty(ops.x6_lower_bytes(Mx, K), dtype=torch.uint8, device=dev)
         b["x6"] = x6
         if Mf == Ma and self.pred_layer.Z.shape[1] == self.assign_layer.Z.shape[1]:
             b["LinvT2"] = ops.padded(Mf, Mf, dev, batch=2)
@@ -306,21 +319,48 @@ class SMGP(SGP):
         self.last_info = torch.cat(infos)
         return outs[0], outs[1]
 
-    def conditionals(self, X, timing=None):
-        """(mu_f, var_f, mu_a, var_a), each an expert-major [K, N] device view."""
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def conditionals(self, X, timing=None, kl_out=None):
+        """(mu_f, var_f, mu_a, var_a), each an expert-major [K, N] device view.
+
+        x6 mode: K1 and the tril(q_sqrt) images of both layers (and, when kl_out
+        is given, both KL terms) run on a side stream concurrently with the
+        latency-bound K3 sweep, which occupies only a few CUs."""
         X = self.pred_layer.kernel._x(X)
         N = X.shape[0]
         b = self._buffers(N)
+        layers = (("f", self.pred_layer), ("a", self.assign_layer))
+        images = {}
+        if b["x6"]:
+            main = torch.cuda.current_stream(self.device)
+            side = self._side_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for L, layer in layers:
+                    images[L] = layer.operand_images(X, {"Kfr": b["Kfr_" + L], "Lfr": b["Lfr_" + L]},
+                                                     timing)
+                if kl_out is not None:
+                    with _Stage(timing, "gauss_kl"):
+                        self.pred_layer.prior_kl(out=kl_out[0:1])
+                        self.assign_layer.prior_kl(out=kl_out[1:2])
         with _Stage(timing, "kuu_chol"):
             LinvT_f, LinvT_a = self._factorise(b)
-        shared = {"ws_expert": b["ws_expert"], "Afr": b.get("Afr"), "Lfr": b.get("Lfr"),
-                  "Kfr": b.get("Kfr"), "Tfr": b.get("Tfr")}
-        self.pred_layer.conditional_kn(X, LinvT_f, bufs={"Kuf": b["Kuf_f"], "A": b["A_f"],
-                                                         "stats": b["stats_f"], "fmean": b["mu_f"],
-                                                         "fvar": b["var_f"], **shared}, timing=timing)
-        self.assign_layer.conditional_kn(X, LinvT_a, bufs={"Kuf": b["Kuf_a"], "A": b["A_a"],
-                                                           "stats": b["stats_a"], "fmean": b["mu_a"],
-                                                           "fvar": b["var_a"], **shared}, timing=timing)
+        if b["x6"]:
+            main.wait_stream(side)
+        LinvT = {"f": LinvT_f, "a": LinvT_a}
+        for L, layer in layers:
+            bufs = {"Kuf": b["Kuf_" + L], "A": b["A_" + L], "stats": b["stats_" + L],
+                    "fmean": b["mu_" + L], "fvar": b["var_" + L], "ws_expert": b["ws_expert"],
+                    "Afr": b.get("Afr"), "Tfr": b.get("Tfr")}
+            layer.conditional_kn(X, LinvT[L], bufs=bufs, timing=timing, images=images.get(L))
+        if kl_out is not None and not b["x6"]:
+            with _Stage(timing, "gauss_kl"):
+                self.pred_layer.prior_kl(out=kl_out[0:1])
+                self.assign_layer.prior_kl(out=kl_out[1:2])
         return b["mu_f"], b["var_f"], b["mu_a"], b["var_a"]
 
     def next_seed(self):
@@ -343,11 +383,8 @@ class SMGP(SGP):
         if Yd.numel() != N:
             raise ValueError("X and Y must have the same number of rows")
         b = self._buffers(N)
-        mu_f, var_f, mu_a, var_a = self.conditionals(X, timing=timing)
         kl = b["kl"]
-        with _Stage(timing, "gauss_kl"):
-            self.pred_layer.prior_kl(out=kl[0:1])
-            self.assign_layer.prior_kl(out=kl[1:2])
+        mu_f, var_f, mu_a, var_a = self.conditionals(X, timing=timing, kl_out=kl)
         lik_var = self.likelihood.likelihood.variance.reshape(-1)
         if seed is None and noise is None:
             seed = self.next_seed()
