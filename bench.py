@@ -49,8 +49,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, nargs=2, default=(2048, 4096),
-                    help="two N sizes of the CPU oracle sample (linear fit in N)")
+    ap.add_argument("--cpu-sample", type=int, nargs=2, default=(8192, 65536),
+                    help="two N sizes of the CPU oracle sample (linear fit in N; the full N "
+                         "is timed directly when it is one of them)")
     return ap.parse_args()
 
 
@@ -125,12 +126,16 @@ def cpu_baseline(cfg, sizes):
         ts.append(time.perf_counter() - t0)
     b = (ts[1] - ts[0]) / (sizes[1] - sizes[0])
     a = max(ts[0] - b * sizes[0], 0.0)
-    t_full = a + b * Nfull
+    if Nfull in sizes:
+        t_full = ts[list(sizes).index(Nfull)]
+        how = f"timed directly at N={Nfull}"
+    else:
+        t_full = a + b * Nfull
+        how = f"t = a + b N extrapolated to N={Nfull}"
     return {"value": 1.0 / t_full, "unit": "ELBO steps/s", "cores": int(cores), "kind": "port",
-            "sample": (f"float64 oracle (oracle/cpu_ref.py; reference semantics, S-deduplicated, "
-                       f"TF2 unavailable) at M={M},K={K},D={D},S={S} with N={sizes[0]} "
-                       f"({ts[0]:.2f}s) and N={sizes[1]} ({ts[1]:.2f}s), t = a + b N "
-                       f"extrapolated to N={Nfull}: {t_full:.2f}s per ELBO"),
+            "sample": (f"one float64 ELBO of the oracle (oracle/cpu_ref.py; reference semantics, "
+                       f"S-deduplicated, TF2 unavailable) at M={M},K={K},D={D},S={S}: N={sizes[0]} "
+                       f"took {ts[0]:.2f}s, N={sizes[1]} took {ts[1]:.2f}s; {how}: {t_full:.2f}s per ELBO"),
             "seconds_per_step": t_full}
 
 

@@ -1,0 +1,13 @@
+# Round-end measurement on the GPU box (run from the repo root via gpurun):
+#   GPU tests, the bench line (with CPU baseline), the rocprofv3 kernel-trace
+#   summary of the same bench command, and the PMC passes for HBM traffic.
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+tail -c 300 gpurun_out/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
+ONLY=${ONLY:-expert_cond_x6,trsm_stats_x6,rbf_kuf_x6} bash tools/pmc_pass.sh
