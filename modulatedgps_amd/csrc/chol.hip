@@ -201,76 +201,174 @@ __device__ __forceinline__ double quad_bcast_f64(double v) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// 1/sqrt(p) to full f64 precision: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rsqrt_f64(double p) {
+  double r = __builtin_amdgcn_rsq(p);
+  const double h = 0.5 * p;
+  r = r * fma(-h * r, r, 1.5);
+  return r * fma(-h * r, r, 1.5);
+}
+
+// 16x16 f64 block product on v_mfma_f64_16x16x4_f64 (one wave):
+// acc += sign * opA(sa) . opB(sb), opA(X)[i][k] = X[i][k], opB(X)[k][j] = TB ? X[j][k] : X[k][j].
+// Lane l supplies A[l & 15][k0 + (l >> 4)], B[k0 + (l >> 4)][l & 15]; register r of
+// acc holds row (l >> 4) + 4 r, column l & 15.
+template <bool TB>
+__device__ __forceinline__ void blk_mma(doublex4& acc, const double* __restrict__ sa,
+                                        const double* __restrict__ sb, double sign) {
+  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    const double av = sign * sa[i * LDT + k0 + kq];
+    const double bv = TB ? sb[i * LDT + k0 + kq] : sb[(k0 + kq) * LDT + i];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ doublex4 blk_load(const double* __restrict__ s) {
+  const int lane = threadIdx.x & 63;
+  doublex4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = s[((lane >> 4) + 4 * r) * LDT + (lane & 15)];
+  return v;
+}
+
+__device__ __forceinline__ void blk_store(double* __restrict__ s, const doublex4& v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s[((lane >> 4) + 4 * r) * LDT + (lane & 15)] = v[r];
+}
+
+// Panel P (columns 16P..16P+15) of the diagonal tile, wave 0: lane r keeps the
+// 16 panel entries of row r; square-root-free right-looking sweep whose column
+// broadcasts are readlanes from the owning lane (no LDS round trip on the
+// critical path).  Writes L's panel (zeros above the diagonal) and
+// col[16P + c] = 1 / L[16P + c][16P + c].
+template <int P>
+__device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __restrict__ col, int r, int& bad) {
+  constexpr int C0 = 16 * P;
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + C0 + j];
+  double rs[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double piv = read_lane_f64(a[c], C0 + c);
+    if (!(piv > 0.0) && bad == 0) bad = C0 + c + 1;
+    const double t = a[c] * rcp_f64(piv);
+    rs[c] = rsqrt_f64(piv);
+#pragma unroll
+    for (int s2 = c + 1; s2 < 16; ++s2) a[s2] = fma(-t, read_lane_f64(a[c], C0 + s2), a[s2]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + C0 + c] = (r >= C0 + c) ? a[c] * rs[c] : 0.0;
+  if (r == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) col[C0 + c] = rs[c];  // uniform across lanes
+  }
+}
+
+// Trailing update after panel P (all waves): W[I][J] -= L[I][panel] L[J][panel]^T
+// for the 16x16 blocks I >= J > P (lower triangle of blocks incl. the diagonal).
+template <int P>
+__device__ __forceinline__ void panel_update(double* __restrict__ sF) {
+  constexpr int NB = 3 - P, NBLK = NB * (NB + 1) / 2;
+  const int w = threadIdx.x >> 6;
+  for (int q = w; q < NBLK; q += 4) {
+    int bi = 0;
+    while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+    const int bj = q - bi * (bi + 1) / 2;
+    const int R0 = 16 * (P + 1 + bi), C1 = 16 * (P + 1 + bj);
+    doublex4 acc = blk_load(sF + R0 * LDT + C1);
+    blk_mma<true>(acc, sF + R0 * LDT + 16 * P, sF + C1 * LDT + 16 * P, -1.0);
+    blk_store(sF + R0 * LDT + C1, acc);
+  }
+}
+
 // Factor the symmetric 64x64 tile in sF (lower part used) in place: sF <- L
 // (zeros above), sX <- L^-1 (zeros above).  Called by all 256 threads.
 //
-// Factorisation (wave 0): square-root-free right-looking sweep.  Lane r keeps
-// row r in registers; at column c the pivot p_c is read from lane c, column c
-// is broadcast through LDS, and every lane updates a[s] -= (a[c]/p_c) a_s[c]
-// (s > c).  Afterwards L[r][c] = a[c] / sqrt(p_c) (c <= r).  No sqrt or
-// division sits on the per-column critical path.
-// Inverse (all 4 waves): X = L^-1 by right-looking forward substitution in a
-// quad layout: wave w, lane l owns column c = 16 w + (l >> 2) and rows
-// 16 g + k (g = l & 3, k = 0..15).  Step I scales x_I (held by group I >> 4),
-// broadcasts it across the quad with DPP and updates the 16 rows of every
-// lane with column I of L (read from L^T staged in sX, diagonal zeroed).
-// Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
+// Blocked in four 16-column panels: wave 0 factors a panel (register rows,
+// readlane broadcasts, no sqrt/division on the per-column chain), then the four
+// waves apply its rank-16 update to the trailing blocks on the f64 MFMA.
+// Inverse, by 16x16 blocks: wave p inverts L_pp (quad layout: lane = column x
+// row group, DPP broadcast of the pivot row), then the block diagonals
+// d = 1..3: X_{j+d,j} = -X_{j+d,j+d} sum_{k=j}^{j+d-1} L_{j+d,k} X_{k,j} on the
+// f64 MFMA (the product's accumulator registers are directly the B operand of
+// the second product).  Records the first non-positive pivot (LAPACK info,
+// 1-based, + gcol0).
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0) {
-  if (threadIdx.x < 64) {
-    const int r = threadIdx.x;
-    double* bc = sX;  // column broadcast buffer (row 0 of sX, free until L^T is staged)
-    int bad = 0;
-    double a[CB];
-#pragma unroll
-    for (int t = 0; t < CB; ++t) a[t] = sF[r * LDT + t];
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      const double piv = read_lane_f64(a[c], c);
-      if (!(piv > 0.0) && bad == 0) bad = c + 1;
-      const double t = a[c] * rcp_f64(piv);
-      bc[r] = a[c];
-      col[c] = 1.0 / sqrt(piv);
-#pragma unroll
-      for (int s = c + 1; s < CB; ++s) a[s] = fma(-t, bc[s], a[s]);
-    }
-    // L = a[c] / sqrt(p_c) below and on the diagonal: stage L (row-major) and
-    // L^T with a zero diagonal (the inverse scales by col[] = 1 / L[c][c]).
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      const double l = (c <= r) ? a[c] * col[c] : 0.0;
-      sF[r * LDT + c] = l;
-      sX[c * LDT + r] = (c < r) ? l : 0.0;
-    }
-    if (bad && r == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int bad = 0;
+  if (w == 0) panel_factor<0>(sF, col, lane, bad);
+  __syncthreads();
+  panel_update<0>(sF);
+  __syncthreads();
+  if (w == 0) panel_factor<1>(sF, col, lane, bad);
+  __syncthreads();
+  panel_update<1>(sF);
+  __syncthreads();
+  if (w == 0) panel_factor<2>(sF, col, lane, bad);
+  __syncthreads();
+  panel_update<2>(sF);
+  __syncthreads();
+  if (w == 0) {
+    panel_factor<3>(sF, col, lane, bad);
+    if (bad && lane == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
   }
   __syncthreads();
   STAMP((int)(gcol0 / CB) - 1, 5);
-  const int lane = threadIdx.x & 63, g = lane & 3;
-  const int c = 16 * (threadIdx.x >> 6) + (lane >> 2);
-  double x[16];
+  // ---- inverse: diagonal blocks (wave p -> X_pp), upper blocks zero
+  {
+    const int p = w, cc = lane >> 2, g = lane & 3;
+    const double* L = sF + 16 * p * LDT + 16 * p;
+    double x[4];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) x[k] = (16 * g + k == c) ? 1.0 : 0.0;
-  const double* sT = sX + 16 * g;
+    for (int k = 0; k < 4; ++k) x[k] = (4 * g + k == cc) ? 1.0 : 0.0;
 #pragma unroll
-  for (int I = 0; I < CB; ++I) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int GI = I >> 4, KI = I & 15;
-    double xi = x[KI] * col[I];
-    switch (GI) {  // compile-time after unrolling
-      case 0: xi = quad_bcast_f64<0>(xi); break;
-      case 1: xi = quad_bcast_f64<1>(xi); break;
-      case 2: xi = quad_bcast_f64<2>(xi); break;
-      default: xi = quad_bcast_f64<3>(xi); break;
+    for (int I = 0; I < 16; ++I) {
+      const int GI = I >> 2, KI = I & 3;
+      double xi = x[KI] * col[16 * p + I];
+      switch (GI) {  // compile-time after unrolling
+        case 0: xi = quad_bcast_f64<0>(xi); break;
+        case 1: xi = quad_bcast_f64<1>(xi); break;
+        case 2: xi = quad_bcast_f64<2>(xi); break;
+        default: xi = quad_bcast_f64<3>(xi); break;
+      }
+      if (g == GI) x[KI] = xi;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int row = 4 * g + k;
+        const double l = L[row * LDT + I];
+        x[k] = (row > I) ? fma(-l, xi, x[k]) : x[k];
+      }
     }
-    if (g == GI) x[KI] = xi;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = fma(-sT[I * LDT + k], xi, x[k]);
+    for (int k = 0; k < 4; ++k) sX[(16 * p + 4 * g + k) * LDT + 16 * p + cc] = x[k];
+    // upper blocks (i < j) of X are zero: wave p clears row block p to its right
+    for (int j = p + 1; j < 4; ++j) blk_store(sX + 16 * p * LDT + 16 * j, doublex4{0.0, 0.0, 0.0, 0.0});
   }
-  __syncthreads();  // every wave is done reading L^T before X overwrites sX
+  __syncthreads();
+  // ---- block diagonals d = 1..3
 #pragma unroll
-  for (int k = 0; k < 16; ++k) sX[(16 * g + k) * LDT + c] = x[k];
+  for (int d = 1; d < 4; ++d) {
+    if (w < 4 - d) {
+      const int j = w, i = j + d;
+      doublex4 y = {0.0, 0.0, 0.0, 0.0};
+      for (int k = j; k < i; ++k) blk_mma<false>(y, sF + 16 * i * LDT + 16 * k, sX + 16 * k * LDT + 16 * j, 1.0);
+      // X_ij = -X_ii Y: register s of y is the B operand of k-step s
+      doublex4 xv = {0.0, 0.0, 0.0, 0.0};
+      const double* Xii = sX + 16 * i * LDT + 16 * i;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const double av = -Xii[(lane & 15) * LDT + 4 * s4 + (lane >> 4)];
+        xv = __builtin_amdgcn_mfma_f64_16x16x4f64(av, y[s4], xv, 0, 0, 0);
+      }
+      blk_store(sX + 16 * i * LDT + 16 * j, xv);
+    }
+    __syncthreads();
+  }
 }
 
 // Write the factored diagonal tile j: L block (f32, guarded to M; optional) and D_j (f64).
