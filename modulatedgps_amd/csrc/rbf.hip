@@ -79,52 +79,76 @@ __global__ __launch_bounds__(kRbfThreads) void rbf_kernel(
   }
 }
 
-// K1 writing Kuf's split-bf16 image (split3.hip layout) instead of f32 Kuf:
-// workgroup = 4 waves = 4 column blocks of 32 (128 columns) x a chunk of 16
-// k-steps (256 rows); lane (r, h) owns column n = 32 nb + r and, per k-step,
-// rows 16 mk + kperm(h, j).  Each wave writes 16 x 3 KiB contiguous.
+// K1 writing Kuf's split-bf16 image (split3.hip layout) instead of f32 Kuf.
+// The cross term z'.x' (scaled inputs) is a [32 x D] x [D x 32] product on
+// v_mfma_f32_32x32x2_f32 (exact f32), and the accumulator of that MFMA holds
+// row (r & 3) + 8 (r >> 2) + 4 h of column l & 31 in register r -- exactly the
+// order of an image fragment: registers 0..7 / 8..15 of a 32x32 tile are the
+// lane's 8 elements of k-steps 2 mb / 2 mb + 1.  So each lane finishes its 16
+// values in registers (r2 = |z'|^2 + |x'|^2 - 2 z'.x', var * exp2(-r2) -- the
+// expanded form GPflow's square_distance uses), splits them and stores 6 x 16 B.
+// Workgroup = 4 waves x 32 columns x 128 rows (4 row tiles per wave).
 // Rows >= M and columns >= N of the padded image are written as zeros.
 template <int DMAX>
 __global__ __launch_bounds__(kRbfThreads) void rbf_kuf_x6_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ Z, int64_t ldz, int64_t N,
     int64_t M, int D, const float* __restrict__ variance, const float* __restrict__ ls, int n_ls, int nmk,
     bf16x8* __restrict__ Kfr) {
-  __shared__ float zs[256][DMAX];
-  __shared__ float cs[DMAX];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
+  constexpr int KS = (DMAX + 1) / 2;     // MFMA k-steps (2 dims each)
+  constexpr int DP = 2 * KS + 1;         // LDS row pitch (odd: spreads banks)
+  __shared__ float zs[128 * DP];
+  __shared__ float zz[128];
+  __shared__ float cs[2 * KS];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c32 = lane & 31;
   const int64_t nb = (int64_t)blockIdx.x * 4 + w;
-  const int64_t n = 32 * nb + r;
-  const int mk0 = blockIdx.y * 16;
-  const int64_t m0 = 16 * (int64_t)mk0;
+  const int64_t n = 32 * nb + c32;
+  const int64_t m0 = 128 * (int64_t)blockIdx.y;
   const float kHalfLog2e = 0.8493218002880191f;  // sqrt(0.5 * log2(e))
-  if (t < DMAX) cs[t] = (t < D) ? kHalfLog2e / ls[n_ls == 1 ? 0 : t] : 0.f;
+  if (t < 2 * KS) cs[t] = (t < D) ? kHalfLog2e / ls[n_ls == 1 ? 0 : t] : 0.f;
   __syncthreads();
-  for (int i = t; i < 256 * DMAX; i += kRbfThreads) {
-    const int rr = i / DMAX, d = i % DMAX;
-    const int64_t m = m0 + rr;
-    zs[rr][d] = (m < M && d < D) ? Z[m * ldz + d] * cs[d] : 0.f;
+  for (int i = t; i < 128 * 2 * KS; i += kRbfThreads) {
+    const int r = i / (2 * KS), d = i % (2 * KS);
+    const int64_t m = m0 + r;
+    zs[r * DP + d] = (m < M && d < D) ? Z[m * ldz + d] * cs[d] : 0.f;
   }
-  float xs[DMAX];
+  float xk[KS], xx = 0.f;
 #pragma unroll
-  for (int d = 0; d < DMAX; ++d) xs[d] = (n < N && d < D) ? X[n * ldx + d] * cs[d] : 0.f;
-  const float var = variance[0];
+  for (int s = 0; s < KS; ++s) {
+    const int d = 2 * s + h;
+    xk[s] = (n < N && d < D) ? X[n * ldx + d] * cs[d] : 0.f;
+    xx = fmaf(xk[s], xk[s], xx);
+  }
+  xx += __shfl_xor(xx, 32, 64);  // the two lane halves hold the even / odd dims
   __syncthreads();
-  const int nk = (nmk - mk0) < 16 ? (nmk - mk0) : 16;
-  bf16x8* dst = Kfr + ((nb * nmk + mk0) * 3) * 64 + lane;
-  for (int q = 0; q < nk; ++q) {
-    float v[8];
+  if (t < 128) {
+    float a = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int row = 16 * q + kperm(h, j);
-      float acc = 0.f;
+    for (int d = 0; d < 2 * KS; ++d) a = fmaf(zs[t * DP + d], zs[t * DP + d], a);
+    zz[t] = a;
+  }
+  __syncthreads();
+  const float var = variance[0];
+  const bool colok = n < N;
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        const float diff = zs[row][d] - xs[d];
-        acc = fmaf(diff, diff, acc);
+  for (int i = 0; i < 4; ++i) {
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      acc = mfma32x32x2(zs[(32 * i + c32) * DP + 2 * s + h], xk[s], acc);
+    const int64_t mb = (m0 >> 5) + i;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = 32 * i + acc_row(8 * half + j, lane);
+        const float r2 = fmaf(-2.f, acc[8 * half + j], zz[row] + xx);
+        v[j] = (colok && m0 + row < M) ? var * exp2f(-r2) : 0.f;
       }
-      v[j] = (m0 + row < M && n < N) ? var * exp2f(-acc) : 0.f;
+      store_split(Kfr + ((nb * nmk + 2 * mb + half) * 3) * 64 + lane, v);
     }
-    store_split(dst + q * 3 * 64, v);
   }
 }
 
@@ -215,7 +239,7 @@ extern "C" int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64
   if (!aligned16(Kfr)) return MGP_ERR_ALIGN;
   const int64_t Mp = (M + 127) / 128 * 128, Np = (N + 255) / 256 * 256;
   const int nmk = (int)(Mp / 16);
-  const dim3 grid((unsigned)(Np / 128), (unsigned)((nmk + 15) / 16)), block(kRbfThreads);
+  const dim3 grid((unsigned)(Np / 128), (unsigned)(Mp / 128)), block(kRbfThreads);
   hipStream_t s = (hipStream_t)stream;
 #define MGP_RBF_X6_CASE(DM)                                                                          \
   if (D <= DM) {                                                                                     \

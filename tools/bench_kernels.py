@@ -14,16 +14,20 @@ from modulatedgps_amd import ops  # noqa: E402
 CFG = {"c2": (8192, 256, 4, 2, 0.15), "c3": (65536, 1024, 8, 8, 1.0), "c5": (262144, 2048, 16, 16, 2.0)}
 
 
-def timeit(fn, reps):
+def timeit(fn, reps, inner=10):
+    """Median / min over `reps` of the mean time of `inner` back-to-back calls
+    (amortises the host launch latency of short kernels)."""
     ts = []
     for _ in range(reps):
+        fn()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        fn()
+        for _ in range(inner):
+            fn()
         e1.record()
         torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1))
+        ts.append(e0.elapsed_time(e1) / inner)
     return float(np.median(ts)), float(np.min(ts))
 
 
