@@ -192,6 +192,17 @@ int mgp_elbo_terms(const float* mu_f, const float* var_f, const float* mu_a, con
                    uint64_t seed, int64_t n_offset, double* data_sum, void* workspace,
                    size_t workspace_bytes, mgp_stream_t stream);
 
+/* SMGPModified.E_log_p_Y (models.py:106-123): as mgp_elbo_terms, plus the
+ * assignment layer's own Gaussian var-exp (likelihood variances
+ * assign_lik_var [K], device) weighted by the same W, with its own logsumexp:
+ *   data_sum = sum_n [lse_s(sum_k W ve_a) - log S + lse_s(sum_k W ve_f) - log S]. */
+int mgp_elbo_terms_modified(const float* mu_f, const float* var_f, const float* mu_a,
+                            const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
+                            const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                            const float* noise_z, const float* noise_u, uint64_t seed,
+                            int64_t n_offset, double* data_sum, void* workspace,
+                            size_t workspace_bytes, mgp_stream_t stream);
+
 /* elbo = data_sum / n_batch - (kl_f + kl_a) / num_data   (models.py:76,79)
  * All pointers device; elbo_out float32 and elbo_out64 (nullable) double. */
 int mgp_elbo_combine(const double* data_sum, const double* kl_f, const double* kl_a,

@@ -24,11 +24,15 @@ namespace mgp {
 
 constexpr int kElboThreads = 256;
 
-template <int KMAX>
+// MOD: SMGPModified.E_log_p_Y (models.py:112-123) -- a second Gaussian
+// var-exp of the assignment layer (likelihood variances lik_var_a) weighted by
+// the same W, with its own logsumexp over S: lse_S(sum_k W ve_a) + lse_S(sum_k W ve_f) - 2 log S.
+template <int KMAX, bool MOD>
 __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
-    const float* __restrict__ lik_var, int64_t N, int K, int S, float inv_tau,
+    const float* __restrict__ lik_var, const float* __restrict__ lik_var_a, int64_t N, int K, int S,
+    float inv_tau,
     const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
     uint32_t key1, int64_t n_offset, double* __restrict__ partials) {
   __shared__ double scratch[16];
@@ -36,7 +40,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
   float val = 0.f;
   if (n < N) {
     const float kHalfLog2Pi = 0.91893853320467274f;
-    float ve[KMAX], ma[KMAX], sa[KMAX];
+    float ve[KMAX], ma[KMAX], sa[KMAX], vea[MOD ? KMAX : 1];
     const float y = Y[n];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -45,13 +49,20 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
         const float d = y - mu_f[(int64_t)k * ldf + n];
         ve[k] = -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + n]) / s2;
         ma[k] = mu_a[(int64_t)k * ldf + n];
-        sa[k] = sqrtf(var_a[(int64_t)k * ldf + n] + 1e-6f);
+        const float va = var_a[(int64_t)k * ldf + n];
+        sa[k] = sqrtf(va + 1e-6f);
+        if constexpr (MOD) {
+          const float s2a = lik_var_a[k];
+          const float da = y - ma[k];
+          vea[k] = -kHalfLog2Pi - 0.5f * logf(s2a) - 0.5f * (da * da + va) / s2a;
+        }
       } else {
         ve[k] = 0.f; ma[k] = 0.f; sa[k] = 0.f;
+        if constexpr (MOD) vea[k] = 0.f;
       }
     }
     const uint32_t ng = (uint32_t)(n + n_offset);
-    float run_max = -INFINITY, run_sum = 0.f;
+    float run_max = -INFINITY, run_sum = 0.f, run_max_a = -INFINITY, run_sum_a = 0.f;
     for (int s = 0; s < S; ++s) {
       float z[KMAX], u[KMAX];
       if (noise_z != nullptr) {
@@ -89,13 +100,14 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
           xm = fmaxf(xm, x[k]);
         }
       }
-      float den = 0.f, num = 0.f;
+      float den = 0.f, num = 0.f, numa = 0.f;
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
         if (k < K) {
           const float e = __expf(x[k] - xm);
           den += e;
           num = fmaf(e, ve[k], num);
+          if constexpr (MOD) numa = fmaf(e, vea[k], numa);
         }
       }
       const float l = num / den;
@@ -105,8 +117,18 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
       } else {
         run_sum += __expf(l - run_max);
       }
+      if constexpr (MOD) {
+        const float la = numa / den;
+        if (la > run_max_a) {
+          run_sum_a = run_sum_a * __expf(run_max_a - la) + 1.f;
+          run_max_a = la;
+        } else {
+          run_sum_a += __expf(la - run_max_a);
+        }
+      }
     }
     val = run_max + logf(run_sum) - logf((float)S);
+    if constexpr (MOD) val += run_max_a + logf(run_sum_a) - logf((float)S);
   }
   const double bs = block_sum<double>((double)val, scratch);
   if (threadIdx.x == 0) partials[blockIdx.x] = bs;
@@ -364,6 +386,37 @@ extern "C" size_t mgp_elbo_workspace_bytes(int64_t N) {
   return (size_t)(elbo_blocks(N) > 0 ? elbo_blocks(N) : 1) * sizeof(double);
 }
 
+static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
+                          int64_t ldf, const float* Y, const float* lik_var, const float* lik_var_a,
+                          int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
+                          const float* noise_u, uint64_t seed, int64_t n_offset, double* data_sum,
+                          void* workspace, size_t workspace_bytes, hipStream_t s) {
+  if (!workspace || workspace_bytes < mgp_elbo_workspace_bytes(N)) return MGP_ERR_WORKSPACE;
+  double* partials = (double*)workspace;
+  const int nb = (int)elbo_blocks(N);
+  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+  if (nb > 0) {
+#define MGP_ELBO_CASE(KM)                                                                               \
+  if (K <= KM) {                                                                                         \
+    if (lik_var_a)                                                                                       \
+      hipLaunchKernelGGL((elbo_terms_kernel<KM, true>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, \
+                         mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, noise_z, noise_u,   \
+                         k0, k1, n_offset, partials);                                                    \
+    else                                                                                                 \
+      hipLaunchKernelGGL((elbo_terms_kernel<KM, false>), dim3(nb), dim3(kElboThreads), 0, s, mu_f,       \
+                         var_f, mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, noise_z,     \
+                         noise_u, k0, k1, n_offset, partials);                                           \
+  } else
+    MGP_ELBO_CASE(1) MGP_ELBO_CASE(2) MGP_ELBO_CASE(4) MGP_ELBO_CASE(8) MGP_ELBO_CASE(16)
+    MGP_ELBO_CASE(32) {}
+#undef MGP_ELBO_CASE
+    int st = launch_status();
+    if (st) return st;
+  }
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, nb, data_sum);
+  return launch_status();
+}
+
 extern "C" int mgp_elbo_terms(const float* mu_f, const float* var_f, const float* mu_a,
                               const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
                               int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
@@ -385,26 +438,35 @@ extern "C" int mgp_elbo_terms(const float* mu_f, const float* var_f, const float
   if ((noise_z == nullptr) != (noise_u == nullptr)) return -12;
   if (n_offset < 0) return -15;
   if (!data_sum) return -16;
-  if (!workspace || workspace_bytes < mgp_elbo_workspace_bytes(N)) return MGP_ERR_WORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
-  double* partials = (double*)workspace;
-  const int nb = (int)elbo_blocks(N);
-  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
-  if (nb > 0) {
-#define MGP_ELBO_CASE(KM)                                                                            \
-  if (K <= KM) {                                                                                      \
-    hipLaunchKernelGGL(elbo_terms_kernel<KM>, dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a, \
-                       var_a, ldf, Y, lik_var, N, K, S, 1.f / tau, noise_z, noise_u, k0, k1,         \
-                       n_offset, partials);                                                           \
-  } else
-    MGP_ELBO_CASE(1) MGP_ELBO_CASE(2) MGP_ELBO_CASE(4) MGP_ELBO_CASE(8) MGP_ELBO_CASE(16)
-    MGP_ELBO_CASE(32) {}
-#undef MGP_ELBO_CASE
-    int st = launch_status();
-    if (st) return st;
-  }
-  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, s, partials, nb, data_sum);
-  return launch_status();
+  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, nullptr, N, K, S, tau, noise_z, noise_u,
+                        seed, n_offset, data_sum, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int mgp_elbo_terms_modified(const float* mu_f, const float* var_f, const float* mu_a,
+                                       const float* var_a, int64_t ldf, const float* Y,
+                                       const float* lik_var, const float* assign_lik_var, int64_t N,
+                                       int32_t K, int32_t S, float tau, const float* noise_z,
+                                       const float* noise_u, uint64_t seed, int64_t n_offset,
+                                       double* data_sum, void* workspace, size_t workspace_bytes,
+                                       mgp_stream_t stream) {
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (!mu_a) return -3;
+  if (!var_a) return -4;
+  if (ldf < N) return -5;
+  if (!Y) return -6;
+  if (!lik_var) return -7;
+  if (!assign_lik_var) return -8;
+  if (N < 0) return -9;
+  if (K < 1) return -10;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -11;
+  if (!(tau > 0.f)) return -12;
+  if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
+  if (n_offset < 0) return -16;
+  if (!data_sum) return -17;
+  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, tau, noise_z,
+                        noise_u, seed, n_offset, data_sum, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 extern "C" int mgp_elbo_combine(const double* data_sum, const double* kl_f, const double* kl_a,

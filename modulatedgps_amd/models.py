@@ -363,6 +363,9 @@ class SMGP(SGP):
                 self.assign_layer.prior_kl(out=kl_out[1:2])
         return b["mu_f"], b["var_f"], b["mu_a"], b["var_a"]
 
+    def _assign_lik_var(self):
+        return None  # SMGPModified: the assignment likelihood's variances
+
     def next_seed(self):
         """Fresh Philox key per evaluation (TF's stateful RNG advances per call)."""
         self._draws += 1
@@ -390,7 +393,8 @@ class SMGP(SGP):
             seed = self.next_seed()
         with _Stage(timing, "elbo_terms"):
             ops.elbo_terms(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU,
-                           noise=noise, seed=seed or 0, n_offset=n_offset, out=b["data_sum"])
+                           noise=noise, seed=seed or 0, n_offset=n_offset, out=b["data_sum"],
+                           assign_lik_var=self._assign_lik_var())
         if process_group is not None:
             import torch.distributed as dist
             with _Stage(timing, "allreduce"):
@@ -434,14 +438,16 @@ class SMGP(SGP):
 
 
 class SMGPModified(SMGP):
-    """SMGP with a second (assignment) likelihood (models.py:106-123).  Round-1
-    scope: the constructor and API exist; the fused kernel variant of its
-    E_log_p_Y is the next §8(f) item and is not implemented yet."""
+    """SMGP with a second (assignment) Gaussian likelihood on the assign layer
+    (models.py:106-123): E_log_p_Y = lse_S(sum_k W ve_a) + lse_S(sum_k W ve_f) - 2 log S,
+    both weighted by the same W.  The assign-layer conditional feeds both W and
+    ve_a (the reference computes it twice, :113 and in W_dist); the data term is
+    the MOD variant of K6 (mgp_elbo_terms_modified)."""
 
     def __init__(self, likelihood, assign_likelihood, pred_layer, assign_layer, K=3, num_samples=1,
                  num_data=None, seed=0):
         SMGP.__init__(self, likelihood, pred_layer, assign_layer, K, num_samples, num_data, seed)
         self.assign_likelihood = BroadcastingLikelihood(assign_likelihood)
 
-    def _build_likelihood(self, *a, **kw):
-        raise NotImplementedError("SMGPModified ELBO kernel is not built yet (SURVEY §8f item 3)")
+    def _assign_lik_var(self):
+        return self.assign_likelihood.likelihood.variance.reshape(-1)

@@ -327,8 +327,9 @@ def gauss_kl_white(q_mu, q_sqrt, out=None, workspace=None):
 
 # --------------------------------------------------------------------------- K6
 def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0, n_offset=0,
-               out=None, workspace=None):
-    """Sum over local points of logsumexp_s(sum_k W ve) - log S (float64 [1])."""
+               out=None, workspace=None, assign_lik_var=None):
+    """Sum over local points of logsumexp_s(sum_k W ve) - log S (float64 [1]).
+    With assign_lik_var: the SMGPModified data term (models.py:112-123)."""
     for t, n in ((mu_f, "mu_f"), (var_f, "var_f"), (mu_a, "mu_a"), (var_a, "var_a")):
         _check(t, n, 2)
     ldf = _ld(mu_f)
@@ -353,6 +354,13 @@ def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, se
             raise ValueError("explicit noise must be [S, N, K]")
         z, u = z.contiguous(), u.contiguous()
         zp, up = z.data_ptr(), u.data_ptr()
+    if assign_lik_var is not None:
+        _check(assign_lik_var, "assign_lik_var")
+        _lib.call("mgp_elbo_terms_modified", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
+                  var_a.data_ptr(), ldf, Y.data_ptr(), lik_var.data_ptr(), assign_lik_var.data_ptr(), N, K,
+                  S, float(tau), zp, up, int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(),
+                  workspace.data_ptr(), workspace.numel(), _stream())
+        return out
     _lib.call("mgp_elbo_terms", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(), var_a.data_ptr(),
               ldf, Y.data_ptr(), lik_var.data_ptr(), N, K, S, float(tau), zp, up,
               int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(), workspace.data_ptr(),

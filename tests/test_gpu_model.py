@@ -124,3 +124,24 @@ def test_native_library_is_loaded(device):
     assert b"gfx950" in lib.mgp_version()
     maps = open("/proc/self/maps").read()
     assert "libmgp_hip.so" in maps
+
+
+@pytest.mark.parametrize("N,M,K,D,ls,S", [(1000, 25, 3, 1, 0.5, 25), (8192, 256, 4, 2, 0.15, 25),
+                                           (1001, 33, 2, 3, 0.8, 7)])
+def test_smgp_modified_elbo(device, N, M, K, D, ls, S):
+    """SMGPModified (models.py:106-123, demo_tf2_modified.py): the MOD variant of
+    K6 against the oracle's smgp_modified_elbo, same explicit noise."""
+    from modulatedgps_amd.likelihoods import GaussianModified
+    from modulatedgps_amd.models import SMGPModified
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
+    a_var = np.linspace(0.3, 0.9, K)[None, :]
+    z, u = R.explicit_noise(S, N, K, seed=5)
+    ref = R.smgp_modified_elbo(X, Y, p, a_var, z, u)
+    base = build_model(p, device)
+    model = SMGPModified(base.likelihood.likelihood, GaussianModified(variance=a_var, device=device),
+                         base.pred_layer, base.assign_layer, K=K, num_samples=S, num_data=p.num_data)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    e = float(model._build_likelihood(Xd, Y, noise=dev_noise(z, u, device)).cpu())
+    assert e == pytest.approx(ref, rel=1e-4)
+    # the plain SMGP term on the same model state is different (the extra term is live)
+    assert abs(float(base._build_likelihood(Xd, Y, noise=dev_noise(z, u, device)).cpu()) - e) > 1e-3 * abs(e)
