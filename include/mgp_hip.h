@@ -203,6 +203,24 @@ int mgp_elbo_terms_modified(const float* mu_f, const float* var_f, const float* 
                             int64_t n_offset, double* data_sum, void* workspace,
                             size_t workspace_bytes, mgp_stream_t stream);
 
+/* ---------------------------------------------------------------- K6 backward
+ * Gradient of the data term (of mgp_elbo_terms, or of mgp_elbo_terms_modified
+ * when assign_lik_var is not NULL) with respect to the conditionals and the
+ * likelihood variances, for the same noise (explicit or Philox seed/n_offset):
+ *   G [4][K][ldg] (float, device) = scale * d(sum_n DT_n)/d(mu_f, var_f, mu_a, var_a)
+ *   g_lik_var[K], g_assign_lik_var[K] (double, device) = scale * d(sum_n DT_n)/d(sigma^2)
+ * (scale = 1 / N_total gives the ELBO's batch-mean gradient).  Replaces the
+ * GradientTape pass through models.py:55-67,73-76 and likelihoods.py:39-41.
+ * Workspace: mgp_elbo_backward_workspace_bytes(N, K). */
+size_t mgp_elbo_backward_workspace_bytes(int64_t N, int32_t K);
+int mgp_elbo_terms_backward(const float* mu_f, const float* var_f, const float* mu_a,
+                            const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
+                            const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                            const float* noise_z, const float* noise_u, uint64_t seed,
+                            int64_t n_offset, float scale, float* G, int64_t ldg, double* g_lik_var,
+                            double* g_assign_lik_var, void* workspace, size_t workspace_bytes,
+                            mgp_stream_t stream);
+
 /* elbo = data_sum / n_batch - (kl_f + kl_a) / num_data   (models.py:76,79)
  * All pointers device; elbo_out float32 and elbo_out64 (nullable) double. */
 int mgp_elbo_combine(const double* data_sum, const double* kl_f, const double* kl_a,

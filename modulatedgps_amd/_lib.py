@@ -80,6 +80,11 @@ SIGNATURES = {
     "mgp_elbo_terms_modified": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64,
                                                c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64,
                                                c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_elbo_backward_workspace_bytes": (c_size, [c_i64, c_i32]),
+    "mgp_elbo_terms_backward": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64,
+                                               c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64,
+                                               ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size,
+                                               c_ptr]),
     "mgp_elbo_combine": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, ctypes.c_double, ctypes.c_double, c_ptr,
                                         c_ptr, c_ptr]),
     "mgp_predict_epilogue": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr,

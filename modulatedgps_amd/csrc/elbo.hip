@@ -24,6 +24,40 @@ namespace mgp {
 
 constexpr int kElboThreads = 256;
 
+// z ~ N(0,1), u ~ U(0,1) of sample s, point n: explicit arrays [S][N][K] or
+// Philox4x32-10 keyed by (global n, s, k / 4, stream 0 = z / 1 = u).
+template <int KMAX>
+__device__ __forceinline__ void draw_noise(float (&z)[KMAX], float (&u)[KMAX], const float* __restrict__ noise_z,
+                                           const float* __restrict__ noise_u, int64_t N, int K, int64_t n, int s,
+                                           uint32_t ng, uint32_t key0, uint32_t key1) {
+  if (noise_z != nullptr) {
+    const float* pz = noise_z + ((int64_t)s * N + n) * K;
+    const float* pu = noise_u + ((int64_t)s * N + n) * K;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      z[k] = (k < K) ? pz[k] : 0.f;
+      u[k] = (k < K) ? pu[k] : 0.5f;
+    }
+  } else {
+#pragma unroll
+    for (int kb = 0; kb < (KMAX + 3) / 4; ++kb) {
+      if (4 * kb >= K) break;
+      const u32x4 wz = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 0u}, key0, key1);
+      const u32x4 wu = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 1u}, key0, key1);
+      float zz[4];
+      box_muller4(wz, zz);
+      const uint32_t uw[4] = {wu.x, wu.y, wu.z, wu.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (4 * kb + e < KMAX) {
+          z[4 * kb + e] = zz[e];
+          u[4 * kb + e] = u01(uw[e]);
+        }
+      }
+    }
+  }
+}
+
 // MOD: SMGPModified.E_log_p_Y (models.py:112-123) -- a second Gaussian
 // var-exp of the assignment layer (likelihood variances lik_var_a) weighted by
 // the same W, with its own logsumexp over S: lse_S(sum_k W ve_a) + lse_S(sum_k W ve_f) - 2 log S.
@@ -65,32 +99,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
     float run_max = -INFINITY, run_sum = 0.f, run_max_a = -INFINITY, run_sum_a = 0.f;
     for (int s = 0; s < S; ++s) {
       float z[KMAX], u[KMAX];
-      if (noise_z != nullptr) {
-        const float* pz = noise_z + ((int64_t)s * N + n) * K;
-        const float* pu = noise_u + ((int64_t)s * N + n) * K;
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-          z[k] = (k < K) ? pz[k] : 0.f;
-          u[k] = (k < K) ? pu[k] : 0.5f;
-        }
-      } else {
-#pragma unroll
-        for (int kb = 0; kb < (KMAX + 3) / 4; ++kb) {
-          if (4 * kb >= K) break;
-          const u32x4 wz = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 0u}, key0, key1);
-          const u32x4 wu = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 1u}, key0, key1);
-          float zz[4];
-          box_muller4(wz, zz);
-          const uint32_t uw[4] = {wu.x, wu.y, wu.z, wu.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (4 * kb + e < KMAX) {
-              z[4 * kb + e] = zz[e];
-              u[4 * kb + e] = u01(uw[e]);
-            }
-          }
-        }
-      }
+      draw_noise<KMAX>(z, u, noise_z, noise_u, N, K, n, s, ng, key0, key1);
       float x[KMAX], xm = -INFINITY;
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
@@ -132,6 +141,178 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
   }
   const double bs = block_sum<double>((double)val, scratch);
   if (threadIdx.x == 0) partials[blockIdx.x] = bs;
+}
+
+// ------------------------------------------------------------------ K6 backward
+// Gradient of the data term of one point, DT_n = lse_s(l_s) - log S with
+// l_s = sum_k W_sk ve_k (MOD: + lse_s(la_s) - log S, la_s = sum_k W_sk ve^a_k),
+// W_s = softmax_k(x_s), x_sk = (g_sk + mu_a,k + z_sk sqrt(v_a,k + 1e-6)) / tau:
+//   dDT/dve_k   = om_k = sum_s pi_s W_sk,            pi_s = exp(l_s - lse)
+//   dDT/dx_sk   = pi_s W_sk (ve_k - l_s)             (softmax Jacobian)
+//   dDT/dmu_f   = om_k (y - mu_f,k) / s2_k,  dDT/dvar_f = -om_k / (2 s2_k)
+//   dDT/dmu_a   = sum_s dDT/dx_sk / tau,     dDT/dvar_a = sum_s dDT/dx_sk z_sk / (2 tau sqrt(v_a,k + 1e-6))
+//   dDT/ds2_k   = om_k (-1/(2 s2_k) + ((y - mu_f,k)^2 + var_f,k) / (2 s2_k^2))
+// (MOD adds the same terms of the assignment var-exp to the mu_a / var_a / s2^a
+// gradients).  Two passes over the samples with the noise redrawn (Philox is
+// counter-based): the first finds lse, the second accumulates.  Outputs are
+// multiplied by `scale` (1 / N_total for the ELBO's batch mean).
+template <int KMAX, bool MOD>
+__global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
+    const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
+    const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
+    const float* __restrict__ lik_var, const float* __restrict__ lik_var_a, int64_t N, int K, int S,
+    float inv_tau, const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
+    uint32_t key1, int64_t n_offset, float scale, float* __restrict__ G, int64_t ldg,
+    double* __restrict__ partials) {
+  __shared__ double scratch[16];
+  const int64_t n = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
+  float glv[KMAX], glva[MOD ? KMAX : 1];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) glv[k] = 0.f;
+  if constexpr (MOD) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) glva[k] = 0.f;
+  }
+  if (n < N) {
+    const float kHalfLog2Pi = 0.91893853320467274f;
+    const float y = Y[n];
+    float ve[KMAX], ma[KMAX], sa[KMAX], vea[MOD ? KMAX : 1];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        const float s2 = lik_var[k];
+        const float d = y - mu_f[(int64_t)k * ldf + n];
+        ve[k] = -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + n]) / s2;
+        ma[k] = mu_a[(int64_t)k * ldf + n];
+        const float va = var_a[(int64_t)k * ldf + n];
+        sa[k] = sqrtf(va + 1e-6f);
+        if constexpr (MOD) {
+          const float s2a = lik_var_a[k];
+          const float da = y - ma[k];
+          vea[k] = -kHalfLog2Pi - 0.5f * logf(s2a) - 0.5f * (da * da + va) / s2a;
+        }
+      } else {
+        ve[k] = 0.f; ma[k] = 0.f; sa[k] = 1.f;
+        if constexpr (MOD) vea[k] = 0.f;
+      }
+    }
+    const uint32_t ng = (uint32_t)(n + n_offset);
+    // sample s: softmax weights W and the two mixtures l, la
+    auto sample = [&](int s, float (&z)[KMAX], float (&W)[KMAX], float& l, float& la) {
+      float u[KMAX];
+      draw_noise<KMAX>(z, u, noise_z, noise_u, N, K, n, s, ng, key0, key1);
+      float xm = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {
+          const float g = -logf(-logf(u[k]));
+          W[k] = (g + fmaf(z[k], sa[k], ma[k])) * inv_tau;
+          xm = fmaxf(xm, W[k]);
+        }
+      }
+      float den = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {
+          W[k] = __expf(W[k] - xm);
+          den += W[k];
+        } else {
+          W[k] = 0.f;
+        }
+      }
+      const float rden = 1.f / den;
+      l = 0.f;
+      la = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        W[k] *= rden;
+        l = fmaf(W[k], ve[k], l);
+        if constexpr (MOD) la = fmaf(W[k], vea[k], la);
+      }
+    };
+    // pass 1: log-sum-exp over the samples
+    float mx = -INFINITY, sm = 0.f, mxa = -INFINITY, sma = 0.f;
+    for (int s = 0; s < S; ++s) {
+      float z[KMAX], W[KMAX], l, la;
+      sample(s, z, W, l, la);
+      if (l > mx) { sm = sm * __expf(mx - l) + 1.f; mx = l; } else { sm += __expf(l - mx); }
+      if constexpr (MOD) {
+        if (la > mxa) { sma = sma * __expf(mxa - la) + 1.f; mxa = la; } else { sma += __expf(la - mxa); }
+      }
+    }
+    const float lse = mx + logf(sm), lsea = MOD ? mxa + logf(sma) : 0.f;
+    // pass 2: accumulate
+    float om[KMAX], oma[MOD ? KMAX : 1], gx[KMAX], gxz[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      om[k] = 0.f; gx[k] = 0.f; gxz[k] = 0.f;
+      if constexpr (MOD) oma[k] = 0.f;
+    }
+    for (int s = 0; s < S; ++s) {
+      float z[KMAX], W[KMAX], l, la;
+      sample(s, z, W, l, la);
+      const float pi = __expf(l - lse);
+      const float pia = MOD ? __expf(la - lsea) : 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        const float pw = pi * W[k];
+        om[k] += pw;
+        float t = pw * (ve[k] - l);
+        if constexpr (MOD) {
+          const float pwa = pia * W[k];
+          oma[k] += pwa;
+          t = fmaf(pwa, vea[k] - la, t);
+        }
+        gx[k] += t;
+        gxz[k] = fmaf(t, z[k], gxz[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        const float s2 = lik_var[k];
+        const float mf = mu_f[(int64_t)k * ldf + n], vf = var_f[(int64_t)k * ldf + n];
+        const float d = y - mf;
+        float gma = gx[k] * inv_tau;
+        float gva = gxz[k] * inv_tau * 0.5f / sa[k];
+        glv[k] = scale * om[k] * (-0.5f / s2 + 0.5f * (d * d + vf) / (s2 * s2));
+        if constexpr (MOD) {
+          const float s2a = lik_var_a[k];
+          const float da = y - ma[k];
+          const float va = var_a[(int64_t)k * ldf + n];
+          gma = fmaf(oma[k], da / s2a, gma);
+          gva -= 0.5f * oma[k] / s2a;
+          glva[k] = scale * oma[k] * (-0.5f / s2a + 0.5f * (da * da + va) / (s2a * s2a));
+        }
+        G[(int64_t)(0 * K + k) * ldg + n] = scale * om[k] * d / s2;
+        G[(int64_t)(1 * K + k) * ldg + n] = -0.5f * scale * om[k] / s2;
+        G[(int64_t)(2 * K + k) * ldg + n] = scale * gma;
+        G[(int64_t)(3 * K + k) * ldg + n] = scale * gva;
+      }
+    }
+  }
+  // block partials of the likelihood-variance gradients: [block][2 * KMAX]
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (k >= K) break;
+    const double v = block_sum<double>((double)glv[k], scratch);
+    if (threadIdx.x == 0) partials[(int64_t)blockIdx.x * 2 * KMAX + k] = v;
+    if constexpr (MOD) {
+      const double va = block_sum<double>((double)glva[k], scratch);
+      if (threadIdx.x == 0) partials[(int64_t)blockIdx.x * 2 * KMAX + KMAX + k] = va;
+    }
+  }
+}
+
+// out[c] = sum_b p[b * stride + c] for c < C (one workgroup per c).
+__global__ __launch_bounds__(256) void column_sums_kernel(const double* __restrict__ p, int nb, int64_t stride,
+                                                          double* __restrict__ out, int64_t out_stride) {
+  __shared__ double scratch[16];
+  const int c = blockIdx.x;
+  double v = 0.0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) v += p[(int64_t)b * stride + c];
+  v = block_sum<double>(v, scratch);
+  if (threadIdx.x == 0) out[(int64_t)c * out_stride] = v;
 }
 
 __global__ __launch_bounds__(1024) void sum_partials_kernel(const double* __restrict__ p, int n,
@@ -554,4 +735,72 @@ extern "C" const char* mgp_status_string(int status) {
   if (status == MGP_ERR_UNSUPPORTED) return "size outside the supported range";
   if (status >= MGP_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(status - MGP_ERR_HIP_BASE));
   return "unknown status";
+}
+
+static int elbo_kmax(int K) { return K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32; }
+
+extern "C" size_t mgp_elbo_backward_workspace_bytes(int64_t N, int32_t K) {
+  const int64_t nb = elbo_blocks(N) > 0 ? elbo_blocks(N) : 1;
+  return (size_t)nb * 2 * (size_t)elbo_kmax(K) * sizeof(double);
+}
+
+extern "C" int mgp_elbo_terms_backward(const float* mu_f, const float* var_f, const float* mu_a,
+                                       const float* var_a, int64_t ldf, const float* Y,
+                                       const float* lik_var, const float* assign_lik_var, int64_t N,
+                                       int32_t K, int32_t S, float tau, const float* noise_z,
+                                       const float* noise_u, uint64_t seed, int64_t n_offset,
+                                       float scale, float* G, int64_t ldg, double* g_lik_var,
+                                       double* g_assign_lik_var, void* workspace,
+                                       size_t workspace_bytes, mgp_stream_t stream) {
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (!mu_a) return -3;
+  if (!var_a) return -4;
+  if (ldf < N) return -5;
+  if (!Y) return -6;
+  if (!lik_var) return -7;
+  if (N < 0) return -9;
+  if (K < 1) return -10;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -11;
+  if (!(tau > 0.f)) return -12;
+  if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
+  if (n_offset < 0) return -16;
+  if (!G) return -18;
+  if (ldg < N) return -19;
+  if (!g_lik_var) return -20;
+  if (assign_lik_var && !g_assign_lik_var) return -21;
+  if (!workspace || workspace_bytes < mgp_elbo_backward_workspace_bytes(N, K)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  double* partials = (double*)workspace;
+  const int nb = (int)elbo_blocks(N);
+  const int km = elbo_kmax(K);
+  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+  if (nb == 0) {
+    hipMemsetAsync(g_lik_var, 0, (size_t)K * sizeof(double), s);
+    if (assign_lik_var) hipMemsetAsync(g_assign_lik_var, 0, (size_t)K * sizeof(double), s);
+    return launch_status();
+  }
+#define MGP_ELBO_BWD_CASE(KM)                                                                             \
+  if (km == KM) {                                                                                         \
+    if (assign_lik_var)                                                                                   \
+      hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, true>), dim3(nb), dim3(kElboThreads), 0, s, mu_f,     \
+                         var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, 1.f / tau, noise_z, \
+                         noise_u, k0, k1, n_offset, scale, G, ldg, partials);                             \
+    else                                                                                                  \
+      hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, false>), dim3(nb), dim3(kElboThreads), 0, s, mu_f,    \
+                         var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, 1.f / tau, noise_z, \
+                         noise_u, k0, k1, n_offset, scale, G, ldg, partials);                             \
+  } else
+  MGP_ELBO_BWD_CASE(1) MGP_ELBO_BWD_CASE(2) MGP_ELBO_BWD_CASE(4) MGP_ELBO_BWD_CASE(8) MGP_ELBO_BWD_CASE(16)
+  MGP_ELBO_BWD_CASE(32) {}
+#undef MGP_ELBO_BWD_CASE
+  int st = launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(column_sums_kernel, dim3(K), dim3(256), 0, s, partials, nb, (int64_t)2 * km, g_lik_var,
+                     (int64_t)1);
+  if (assign_lik_var)
+    hipLaunchKernelGGL(column_sums_kernel, dim3(K), dim3(256), 0, s, partials + km, nb, (int64_t)2 * km,
+                       g_assign_lik_var, (int64_t)1);
+  return launch_status();
 }

@@ -308,6 +308,40 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
     return fmean, fvar
 
 
+def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0,
+                        n_offset=0, scale=1.0, assign_lik_var=None, G=None, workspace=None):
+    """Gradient of the data term: G [4, K, N] = scale * d/d(mu_f, var_f, mu_a, var_a) and the
+    likelihood-variance gradients (float64 [K]; second one for SMGPModified, else None)."""
+    for t, n in ((mu_f, "mu_f"), (var_f, "var_f"), (mu_a, "mu_a"), (var_a, "var_a")):
+        _check(t, n, 2)
+    ldf = _ld(mu_f)
+    if not (_ld(var_f) == _ld(mu_a) == _ld(var_a) == ldf):
+        raise ValueError("conditional outputs must share a leading dimension")
+    K, N = mu_f.shape
+    dev = mu_f.device
+    Y = Y.reshape(-1)
+    _check(Y, "Y"), _check(lik_var, "lik_var")
+    if G is None:
+        G = padded(4 * K, N, dev).unflatten(0, (4, K))
+    glv = torch.empty(K, dtype=torch.float64, device=dev)
+    glva = torch.empty(K, dtype=torch.float64, device=dev) if assign_lik_var is not None else None
+    nbytes = _lib.load().mgp_elbo_backward_workspace_bytes(N, K)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    zp = up = None
+    if noise is not None:
+        z, u = noise
+        z, u = z.contiguous(), u.contiguous()
+        zp, up = z.data_ptr(), u.data_ptr()
+    _lib.call("mgp_elbo_terms_backward", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
+              var_a.data_ptr(), ldf, Y.data_ptr(), lik_var.data_ptr(),
+              assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau), zp, up,
+              int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), G.stride(1),
+              glv.data_ptr(), glva.data_ptr() if glva is not None else None, workspace.data_ptr(),
+              workspace.numel(), _stream())
+    return G, glv, glva
+
+
 # --------------------------------------------------------------------------- K7
 def gauss_kl_white(q_mu, q_sqrt, out=None, workspace=None):
     """Whitened KL (models.py:79) as a float64 device tensor of shape [1]."""

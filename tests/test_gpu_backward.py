@@ -1,0 +1,67 @@
+"""GPU parity of the backward kernels against the float64 autograd oracle
+(oracle/grad_ref.py, itself checked against cpu_ref's ELBO in test_oracle.py).
+
+Tolerance: normwise ||g - g_ref|| / ||g_ref|| <= 1e-4 for every gradient block
+(float32 kernels against float64 autograd, same explicit noise)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref as R
+from oracle import grad_ref as GR
+from tests.helpers import normwise, to_np
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_grads(X, Y, p, z, u, a_var=None):  # end-to-end (used by the parameter-gradient tests)
+    pred, assign, lik = GR.params_from_oracle(p)
+    keep = {}
+    zt = torch.tensor(np.asarray(z, np.float32).astype(np.float64))
+    ut = torch.tensor(np.asarray(u, np.float32).astype(np.float64))
+    av = torch.tensor(np.asarray(a_var, np.float64).reshape(-1).astype(np.float32),
+                      requires_grad=True) if a_var is not None else None
+    e = GR.elbo(torch.tensor(X.astype(np.float32).astype(np.float64)),
+                torch.tensor(Y.astype(np.float32).astype(np.float64)), pred, assign, lik, zt, ut,
+                p.num_data, assign_lik_var=av, keep=keep)
+    e.backward()
+    return e, keep, pred, assign, lik, av
+
+
+@pytest.mark.parametrize("N,M,K,D,ls,S,modified", [(1000, 25, 3, 1, 0.5, 25, False),
+                                                    (777, 33, 5, 2, 0.8, 7, False),
+                                                    (1000, 25, 3, 1, 0.5, 25, True),
+                                                    (513, 16, 8, 3, 0.9, 4, True)])
+def test_elbo_terms_backward(device, N, M, K, D, ls, S, modified):
+    """K6 backward: d(data term)/d(mu_f, var_f, mu_a, var_a, lik variances) at the
+    device's own conditionals, against float64 autograd of the data term at the
+    same (float32) values.  The conditionals enter the Gumbel-softmax at
+    temperature 0.01, so the comparison is made at identical inputs."""
+    from modulatedgps_amd import ops
+    from tests.helpers import build_model
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
+    z, u = R.explicit_noise(S, N, K, seed=5)
+    z32, u32 = np.asarray(z, np.float32), np.asarray(u, np.float32)
+    a_var = np.linspace(0.3, 0.9, K).astype(np.float32) if modified else None
+    model = build_model(p, device)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    conds = [c.clone() for c in model.conditionals(Xd)]
+    Y32 = Y[:, 0].astype(np.float32)
+    lv = model.likelihood.likelihood.variance.reshape(-1)
+    # oracle at the same float32 inputs
+    leaves = [torch.tensor(to_np(c)[:, :N].T, requires_grad=True) for c in conds]
+    lik = torch.tensor(lv.cpu().numpy().astype(np.float64), requires_grad=True)
+    av = torch.tensor(a_var.astype(np.float64), requires_grad=True) if modified else None
+    dt = GR.data_term(*leaves, torch.tensor(Y32.astype(np.float64)), lik,
+                      torch.tensor(z32.astype(np.float64)), torch.tensor(u32.astype(np.float64)),
+                      assign_lik_var=av)
+    (dt / N).backward()
+    noise = (torch.as_tensor(z32, device=device), torch.as_tensor(u32, device=device))
+    avd = torch.as_tensor(a_var, device=device) if modified else None
+    G, glv, glva = ops.elbo_terms_backward(*conds, torch.as_tensor(Y32, device=device), lv, S, noise=noise,
+                                           scale=1.0 / N, assign_lik_var=avd)
+    for i, name in enumerate(("mu_f", "var_f", "mu_a", "var_a")):
+        assert normwise(to_np(G[i])[:, :N].T, leaves[i].grad.numpy()) < 1e-4, name
+    assert normwise(glv.cpu().numpy(), lik.grad.numpy()) < 1e-4
+    if modified:
+        assert normwise(glva.cpu().numpy(), av.grad.numpy()) < 1e-4

@@ -158,3 +158,30 @@ def test_golden_faithful_matches():
     for case in ("case_demo_init", "case_demo_perturbed"):
         d = _load(case + ".npz")
         assert float(d["elbo_faithful"]) == pytest.approx(float(d["elbo"]), rel=1e-12)
+
+
+@pytest.mark.parametrize("modified", [False, True])
+def test_grad_oracle_value_matches_cpu_oracle(modified):
+    """oracle/grad_ref.py (torch float64 autograd) evaluates the same ELBO as
+    cpu_ref.smgp_elbo / smgp_modified_elbo, so its gradients are the gradients
+    of the pinned forward restatement."""
+    import torch
+    from oracle import grad_ref as G
+    X, Y, p = R.synthetic_problem(300, 12, 3, 2, 0.6, state="perturbed", S=4)
+    # the grad oracle holds float32-rounded parameters, as the device does
+    for L in (p.pred, p.assign):
+        for k in ("Z", "q_mu", "q_sqrt"):
+            L[k] = np.asarray(L[k]).astype(np.float32).astype(np.float64)
+    z, u = R.explicit_noise(4, 300, 3)
+    pred, assign, lik = G.params_from_oracle(p)
+    a_var = np.array([[0.4, 0.6, 0.8]])
+    e = G.elbo(torch.tensor(X), torch.tensor(Y), pred, assign, lik, torch.tensor(z), torch.tensor(u),
+               p.num_data, assign_lik_var=torch.tensor(a_var[0]) if modified else None)
+    p.lik_variance = lik.detach().numpy().reshape(1, -1)
+    for L, T in ((p.pred, pred), (p.assign, assign)):
+        L["variance"] = float(T["variance"].detach())
+        L["lengthscales"] = T["lengthscales"].detach().numpy()
+    ref = R.smgp_modified_elbo(X, Y, p, a_var, z, u) if modified else R.smgp_elbo(X, Y, p, z, u)
+    assert float(e) == pytest.approx(ref, rel=1e-10)
+    e.backward()
+    assert pred["q_sqrt"].grad is not None and torch.isfinite(pred["q_sqrt"].grad).all()
