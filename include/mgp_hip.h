@@ -154,15 +154,47 @@ int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64_t ldz, int
                    void* Kfr, size_t kfr_bytes, mgp_stream_t stream);
 /* K4 on images: A = LinvT^T Kuf from Tfr (mgp_split_upper_x6) and Kfr
  * (mgp_rbf_kuf_x6 / mgp_split_cols_x6), writing A's image Afr (for
- * mgp_expert_conditional_x6) and the stats exactly as mgp_trsm_stats. */
+ * mgp_expert_conditional_x6) and the stats exactly as mgp_trsm_stats; also
+ * the f32 A [M][lda] when A is not NULL (kept for the backward pass). */
 int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
                       int64_t N, const float* q_mu, int64_t ldq, int32_t K, void* Afr, size_t afr_bytes,
-                      float* stats, int64_t lds, mgp_stream_t stream);
+                      float* stats, int64_t lds, float* A, int64_t lda, mgp_stream_t stream);
 size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K);
 int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
                               const float* stats, int64_t lds, const float* variance, int64_t M,
                               int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
                               void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+
+/* ---------------------------------------------------------------- backward of K1-K5
+ * Gram products over the data dimension (float32 MFMA, deterministic split-K):
+ *   out[i][j] = alpha * sum_n X[i][n] Y[j][n]   (tri != 0: j <= i only, zeros above)
+ * X [MI][ldx], Y [MJ][ldy]; workspace mgp_gram_workspace_bytes(MI, MJ, N, tri). */
+size_t mgp_gram_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t tri);
+int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ldy, int64_t MJ, int64_t N,
+             float alpha, int32_t tri, float* out, int64_t ldo, void* workspace, size_t workspace_bytes,
+             mgp_stream_t stream);
+
+/* Backward of one layer's whitened conditional (the GradientTape pass through
+ * GPflow base_conditional, models.py:141-143, and SVGP's Knn = var,
+ * models.py:133), given G_mu = d/d fmean and G_v = d/d fvar ([K][ldg]):
+ *   g_q_mu [M][ldgq]       = A G_mu^T
+ *   g_q_sqrt[k] [M][ldgs]  = 2 tril(A diag(G_v,k) (L_k^T A)^T)
+ *   g_Kuf [M][ldk]         = L^-T gA,  gA = q_mu G_mu - 2 A sum_k G_v,k + 2 sum_k L_k (L_k^T A) diag(G_v,k)
+ *   g_Lm [M][ldgl]         = -tril(g_Kuf A^T)          (gradient w.r.t. chol(Kuu))
+ *   g_var (double)         = sum G_v                   (through Knn)
+ * Inputs: A's split image and f32 A (both from mgp_trsm_stats_x6), the
+ * tril(q_sqrt) image (mgp_split_lower_x6) and q_sqrt itself, q_mu, LinvT.
+ * The N-scaled products run on the split-bf16 x6 path (f32 accuracy) and the
+ * f32 MFMA (grams).  Workspace: mgp_conditional_backward_workspace_bytes. */
+size_t mgp_conditional_backward_workspace_bytes(int64_t M, int64_t N, int32_t K);
+int mgp_conditional_backward_x6(const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+                                const void* Lfr, size_t lfr_bytes, const float* q_sqrt, int64_t ldqs,
+                                int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+                                int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M,
+                                int64_t N, int32_t K, float* g_q_mu, int64_t ldgq, float* g_q_sqrt,
+                                int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm,
+                                int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
+                                mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K7
  * Whitened Gaussian KL (GPflow gauss_kl(q_mu, q_sqrt, K=None), reached through

@@ -59,7 +59,15 @@ SIGNATURES = {
                                               c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
                                               c_ptr]),
     "mgp_trsm_stats_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
-                                         c_ptr, c_size, c_ptr, c_i64, c_ptr]),
+                                         c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "mgp_gram_workspace_bytes": (c_size, [c_i64, c_i64, c_i64, c_i32]),
+    "mgp_gram": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, ctypes.c_float, c_i32, c_ptr,
+                                c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_conditional_backward_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
+    "mgp_conditional_backward_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_i64, c_ptr, c_size, c_ptr, c_i64,
+                                                   c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                                   c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64,
+                                                   c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
     "mgp_split_upper_x6": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_rbf_kuf_x6": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i32,
                                       c_ptr, c_size, c_ptr]),

@@ -52,7 +52,8 @@ constexpr int kFragBytes = 1024;
 // = S_b[m][m'] kept where m >= m' (LOWER: L_k = tril(q_sqrt[k]), K5) or m <= m'
 // (upper: LinvT, K4's T[k][i] = L^-T[k][i]).  One wave per fragment block
 // (b, mb, mk): grid.x = batch * nmb * nmk / 4.
-template <bool LOWER>
+// TRANS: the source is stored transposed (element (m, m') read at S[m' ld + m]).
+template <bool LOWER, bool TRANS = false>
 __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict__ src, int64_t ld,
                                                         int64_t stride, int64_t M, int nmb, int nmk,
                                                         int64_t nfrag, bf16x8* __restrict__ img) {
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
   for (int j = 0; j < 8; ++j) {
     const int64_t m = 16 * (int64_t)mk + kperm(h, j);
     const bool keep = LOWER ? (m >= mc) : (m <= mc);
-    v[j] = (m < M && mc < M && keep) ? S[m * ld + mc] : 0.f;
+    v[j] = (m < M && mc < M && keep) ? S[TRANS ? mc * ld + m : m * ld + mc] : 0.f;
   }
   store_split(img + f * 3 * 64 + lane, v);
 }
@@ -149,7 +150,7 @@ template <bool DIAG_FIRST>
 __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[4 * 3 * 64],
                                             __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
                                             __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
-                                            int mk_end, int nmk) {
+                                            int mk_end, int nmk, bool init = true) {
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t vB = 16u * lane;
   const uint32_t sB1 = sB0 + (uint32_t)nmk * 3u * kFragBytes;
@@ -162,12 +163,14 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[
     const int e = tid + 256 * s;
     vT[s] = (uint32_t)(((e / 192) * nmk * 192 + (e % 192)) * 16);
   }
+  if (init) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][c][e] = 0.f;
+        for (int e = 0; e < 16; ++e) acc[i][c][e] = 0.f;
+  }
 
   auto load_b = [&](bf16x8 (&b)[2][3], int mk) {
     const uint32_t o = (uint32_t)mk * 3u * kFragBytes;
@@ -278,6 +281,186 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   }
 }
 
+// ------------------------------------------------------------------ backward (x6)
+// Store a 128 x 256 item's accumulators (wave w: 128 rows x 64 columns) as f32
+// rows [i0 + .][n0 + .] of out (M rows, leading dimension ld), each column n
+// scaled by colscale[n] (if given).  Buffer stores with 32-bit offsets: rows
+// beyond M fall outside the resource and are dropped.
+__device__ __forceinline__ void store_acc_f32(const floatx16 (&acc)[4][2], float* __restrict__ out, int64_t ld,
+                                              int64_t i0, int64_t n0, int64_t M, int64_t N,
+                                              const float* __restrict__ colscale) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, (int)(uint32_t)(M * ld * 4), 0x00020000);
+  const uint32_t soff = (uint32_t)((i0 * ld + n0) * 4);
+  const uint32_t ld32 = (uint32_t)ld;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int nl = 64 * w + 32 * c + (lane & 31);
+    const int64_t n = n0 + nl;
+    if (n < N) {
+      const float cs = colscale ? colscale[n] : 1.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[i][c][e] * cs), r,
+                                                (rl * ld32 + (uint32_t)nl) * 4u, soff, 0);
+        }
+    }
+  }
+}
+
+// Store the accumulators as the split image [nb][mk] of the item's 128 x 256
+// block (as K4 does for A), columns scaled by colscale[n] (0 beyond N).
+__device__ __forceinline__ void store_acc_image(const floatx16 (&acc)[4][2], bf16x8* __restrict__ img, int nmk,
+                                                int t, int tn, int64_t N, const float* __restrict__ colscale) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int64_t nb = 8 * (int64_t)tn + 2 * w + c;
+    const int64_t n = 32 * nb + (lane & 31);
+    const float cs = colscale ? (n < N ? colscale[n] : 0.f) : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t mk = 8 * (int64_t)t + 2 * i;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s + j] * cs;
+        store_split(img + ((nb * nmk + mk + s) * 3) * 64 + lane, v);
+      }
+    }
+  }
+}
+
+// B-a: CG_k = (L_k^T A) diag(Gv_k) for every expert, as f32 [K][M][ldc] (for
+// the q_sqrt gradient) and as split images [K][image] (for the A gradient).
+// Items and main loop as K5.
+__global__ __launch_bounds__(256, 2) void expert_bwd_c_kernel(const bf16x8* __restrict__ Afr,
+                                                             const bf16x8* __restrict__ Lfr, uint32_t afr_bytes,
+                                                             uint32_t lfr_bytes, int nmk, int nmb, int nTn, int K,
+                                                             int64_t M, int64_t N, const float* __restrict__ Gv,
+                                                             int64_t ldg, float* __restrict__ CG, int64_t ldc,
+                                                             int64_t strideC, bf16x8* __restrict__ CGfr,
+                                                             int64_t img_elems) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];
+  int t, tn, k;
+  x6_item(blockIdx.x, nTn, K, t, tn, k);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  floatx16 acc[4][2];
+  x6_mainloop<true>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+                    img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
+  const float* g = Gv + (int64_t)k * ldg;
+  store_acc_f32(acc, CG + (int64_t)k * strideC, ldc, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, g);
+  store_acc_image(acc, CGfr + (int64_t)k * img_elems, nmk, t, tn, N, g);
+}
+
+// gA0[m][n] = sum_k q_mu[m][k] G_mu[k][n] - 2 A[m][n] sum_k Gv[k][n]: the part
+// of the A gradient that needs no GEMM (one thread per column n, looping rows).
+template <int KMAX>
+__global__ __launch_bounds__(256) void grad_a_base_kernel(const float* __restrict__ A, int64_t lda,
+                                                          const float* __restrict__ q_mu, int64_t ldq,
+                                                          const float* __restrict__ Gmu,
+                                                          const float* __restrict__ Gv, int64_t ldg, int64_t M,
+                                                          int64_t N, int K, int rows_per_block,
+                                                          float* __restrict__ out, int64_t ldo) {
+  __shared__ float sq[64][KMAX];
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  float gmu[KMAX], gvs = 0.f;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    gmu[k] = (k < K && n < N) ? Gmu[(int64_t)k * ldg + n] : 0.f;
+    if (k < K && n < N) gvs += Gv[(int64_t)k * ldg + n];
+  }
+  for (int64_t rb = r0; rb < r0 + rows_per_block && rb < M; rb += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * KMAX; i += 256) {
+      const int rr = i / KMAX, k = i % KMAX;
+      sq[rr][k] = (rb + rr < M && k < K) ? q_mu[(rb + rr) * ldq + k] : 0.f;
+    }
+    __syncthreads();
+    if (n < N) {
+      const int rows = (int)((M - rb) < 64 ? (M - rb) : 64);
+      for (int rr = 0; rr < rows; ++rr) {
+        float v = -2.f * A[(rb + rr) * lda + n] * gvs;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) v = fmaf(sq[rr][k], gmu[k], v);
+        out[(rb + rr) * ldo + n] = v;
+      }
+    }
+  }
+}
+
+// B-b: gA = 2 sum_k L_k CG_k + gA0, written as the split image of gA (the B
+// operand of B-d).  T images: L_k^T (upper in (k, i)); the contraction runs
+// over (expert, m') into one accumulator; item (t, tn) as K4, heavy first.
+__global__ __launch_bounds__(256, 2) void expert_bwd_a_kernel(
+    const bf16x8* __restrict__ LTfr, uint32_t ltfr_bytes, const bf16x8* __restrict__ CGfr, uint32_t cgfr_bytes,
+    int64_t img_elems, int nmk, int nTn, int K, int64_t M, int64_t N, const float* __restrict__ gA0,
+    int64_t ld0, bf16x8* __restrict__ gAfr) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];
+  const int nT = nmk / 8, nmb = nmk / 2;
+  int t, tn;
+  {
+    const int b = blockIdx.x;
+    if (nTn % 8 == 0) {
+      const int x = b & 7, j = b >> 3, per = nTn / 8;
+      t = nT - 1 - j / per;
+      tn = (j % per) * 8 + x;
+    } else {
+      t = nT - 1 - b / nTn;
+      tn = b % nTn;
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  floatx16 acc[4][2];
+  const int64_t t_elems = (int64_t)nmb * nmk * 3 * 64;  // one expert's T image (bf16x8 units)
+  for (int k = 0; k < K; ++k)
+    x6_mainloop<false>(acc, sL, img_rsrc(LTfr + k * t_elems, ltfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
+                       img_rsrc(CGfr + k * img_elems, cgfr_bytes),
+                       (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8, nmk, k == 0);
+  const int64_t i0 = 128 * (int64_t)t, n0 = (int64_t)tn * kX6BN;
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)gA0, (short)0, (int)(uint32_t)(M * ld0 * 4), 0x00020000);
+  const uint32_t soff = (uint32_t)((i0 * ld0 + n0) * 4), ld32 = (uint32_t)ld0;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int nl = 64 * w + 32 * c + (lane & 31);
+    const bool ok = n0 + nl < N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
+        const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
+        acc[i][c][e] = ok ? fmaf(2.f, acc[i][c][e], b0) : 0.f;   // rows >= M read 0 (outside the resource)
+      }
+  }
+  store_acc_image(acc, gAfr, nmk, t, tn, N, nullptr);
+}
+
+// B-d: gKuf = L^-T gA = Linv^T gA as f32 [M][ld]; T image = Linv (lower in
+// (k, i)), B image = gA; items and main loop as K5 (one "expert").
+__global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restrict__ gAfr,
+                                                         const bf16x8* __restrict__ LIfr, uint32_t gafr_bytes,
+                                                         uint32_t lifr_bytes, int nmk, int nmb, int nTn,
+                                                         int64_t M, int64_t N, float* __restrict__ gKuf,
+                                                         int64_t ldk) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];
+  int t, tn, k;
+  x6_item(blockIdx.x, nTn, 1, t, tn, k);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  floatx16 acc[4][2];
+  x6_mainloop<true>(acc, sL, img_rsrc(LIfr, lifr_bytes), (uint32_t)((4 * t) * nmk) * 3u * kFragBytes,
+                    img_rsrc(gAfr, gafr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
+  store_acc_f32(acc, gKuf, ldk, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
+}
+
 // ------------------------------------------------------------------ K4 (x6)
 // A = LinvT^T Kuf from the images Tfr (LinvT, upper) and Kfr (Kuf): item =
 // (row tile t of 128 rows, heavy = large t first; column tile tn of 256), the
@@ -289,7 +472,7 @@ template <int KMAX>
 __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
     const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
     int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
-    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_) {
+    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   const int nT = nmk / 8;
   int t, tn;
@@ -328,6 +511,7 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
         store_split(Afr + ((nb * nmk + mk + s) * 3) * 64 + lane, v);
       }
     }
+  if (Af32) store_acc_f32(acc, Af32, lda, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
   // ---- stats (rows beyond M are zero in A; tiles starting at or beyond M are not stored)
   const int64_t i0 = 128 * (int64_t)t;
   float* sQ = reinterpret_cast<float*>(&sL[0][0]);  // [128][KMAX]; the main loop ended on a barrier
@@ -485,19 +669,19 @@ extern "C" int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, cons
 template <int KMAX>
 static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb, int64_t M, int64_t N,
                           const float* q_mu, int64_t ldq, int K, void* Afr, float* stats, int64_t lds,
-                          hipStream_t s) {
+                          float* A, int64_t lda, hipStream_t s) {
   const int64_t Mp = x6_mp(M);
   const int nmk = (int)(Mp / 16), nT = (int)(Mp / kX6BM), nTn = (int)(x6_np(N) / kX6BN);
   hipLaunchKernelGGL(trsm_stats_x6_kernel<KMAX>, dim3((unsigned)(nT * nTn)), dim3(256), 0, s,
                      (const bf16x8*)Tfr, (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu,
-                     ldq, K, (bf16x8*)Afr, stats, lds);
+                     ldq, K, (bf16x8*)Afr, stats, lds, A, lda);
   return launch_status();
 }
 
 extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes,
                                  int64_t M, int64_t N, const float* q_mu, int64_t ldq, int32_t K,
-                                 void* Afr, size_t afr_bytes, float* stats, int64_t lds,
-                                 mgp_stream_t stream) {
+                                 void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A,
+                                 int64_t lda, mgp_stream_t stream) {
   if (!Tfr) return -1;
   if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return -2;
   if (!Kfr) return -3;
@@ -512,13 +696,163 @@ extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* 
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -11;
   if (!stats) return -12;
   if (lds < N) return -13;
+  if (A && lda < N) return -15;
   if (!aligned16(Tfr) || !aligned16(Kfr) || !aligned16(Afr)) return MGP_ERR_ALIGN;
   if (mgp_x6_cols_bytes(M, N) >= ((size_t)1 << 32) || mgp_x6_lower_bytes(M, 1) >= ((size_t)1 << 32))
     return MGP_ERR_UNSUPPORTED;
   if (M == 0 || N == 0) return MGP_OK;
   hipStream_t s = (hipStream_t)stream;
   const size_t tb = mgp_x6_lower_bytes(M, 1), kb = mgp_x6_cols_bytes(M, N);
-  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, s);
-  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, s);
-  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, s);
+  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s);
+  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s);
+  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s);
+}
+
+// ------------------------------------------------------------------ conditional backward (x6)
+extern "C" size_t mgp_gram_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t tri);
+extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ldy, int64_t MJ,
+                        int64_t N, float alpha, int32_t tri, float* out, int64_t ldo, void* workspace,
+                        size_t workspace_bytes, mgp_stream_t stream);
+
+namespace {
+struct CondBwdWs {  // workspace carve-up (256-B aligned pieces)
+  size_t cg, cgfr, ltfr, ga0, gafr, lifr, gram, total;
+};
+size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
+  CondBwdWs w;
+  const int64_t ldn = (N + 3) / 4 * 4;
+  size_t o = 0;
+  w.cg = o;   o += al256((size_t)K * M * ldn * 4);
+  w.cgfr = o; o += al256((size_t)K * mgp_x6_cols_bytes(M, N));
+  w.ltfr = o; o += al256(mgp_x6_lower_bytes(M, K));
+  w.ga0 = o;  o += al256((size_t)M * ldn * 4);
+  w.gafr = o; o += al256(mgp_x6_cols_bytes(M, N));
+  w.lifr = o; o += al256(mgp_x6_lower_bytes(M, 1));
+  w.gram = o;
+  size_t g = mgp_gram_workspace_bytes(M, M, N, 1);
+  const size_t g2 = mgp_gram_workspace_bytes(M, K, N, 0);
+  o += al256(g > g2 ? g : g2);
+  w.total = o;
+  return w;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void sum_all_kernel(const float* __restrict__ x, int64_t rows, int64_t cols,
+                                                      int64_t ld, double* __restrict__ out) {
+  __shared__ double scratch[16];
+  double v = 0.0;
+  for (int64_t i = threadIdx.x; i < rows * cols; i += 256) v += (double)x[(i / cols) * ld + i % cols];
+  v = mgp::block_sum<double>(v, scratch);
+  if (threadIdx.x == 0) *out = v;
+}
+
+extern "C" size_t mgp_conditional_backward_workspace_bytes(int64_t M, int64_t N, int32_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 256;
+  return cond_bwd_layout(M, N, K).total;
+}
+
+extern "C" int mgp_conditional_backward_x6(
+    const void* Afr, size_t afr_bytes, const float* A, int64_t lda, const void* Lfr, size_t lfr_bytes,
+    const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+    int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
+    float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
+    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  if (!Afr) return -1;
+  if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
+  if (!A) return -3;
+  if (lda < N) return -4;
+  if (!Lfr) return -5;
+  if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return -6;
+  if (!q_sqrt) return -7;
+  if (ldqs < M) return -8;
+  if (!q_mu) return -10;
+  if (ldq < K) return -11;
+  if (!LinvT) return -12;
+  if (ldl < M) return -13;
+  if (!Gmu) return -14;
+  if (!Gv) return -15;
+  if (ldg < N) return -16;
+  if (M <= 0) return -17;
+  if (N <= 0) return -18;
+  if (K < 1) return -19;
+  if (K > 16) return MGP_ERR_UNSUPPORTED;
+  if (!g_q_mu) return -20;
+  if (!g_q_sqrt) return -22;
+  if (!g_Kuf) return -25;
+  if (!g_Lm) return -27;
+  if (!g_var) return -29;
+  if (!workspace || workspace_bytes < mgp_conditional_backward_workspace_bytes(M, N, K)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(workspace) || !aligned16(Afr) || !aligned16(Lfr)) return MGP_ERR_ALIGN;
+  const size_t img = mgp_x6_cols_bytes(M, N);
+  if (img >= ((size_t)1 << 32) || (size_t)M * ((N + 3) / 4 * 4) * 4 >= ((size_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const CondBwdWs L = cond_bwd_layout(M, N, K);
+  char* ws = (char*)workspace;
+  const int64_t ldn = (N + 3) / 4 * 4;
+  float* CG = (float*)(ws + L.cg);
+  bf16x8* CGfr = (bf16x8*)(ws + L.cgfr);
+  bf16x8* LTfr = (bf16x8*)(ws + L.ltfr);
+  float* gA0 = (float*)(ws + L.ga0);
+  bf16x8* gAfr = (bf16x8*)(ws + L.gafr);
+  bf16x8* LIfr = (bf16x8*)(ws + L.lifr);
+  void* gws = ws + L.gram;
+  const size_t gwsb = L.total - L.gram;
+  const int64_t Mp = x6_mp(M);
+  const int nmk = (int)(Mp / 16), nmb = (int)(Mp / 32), nT = (int)(Mp / kX6BM);
+  const int nTn = (int)(x6_np(N) / kX6BN);
+  const int64_t img_elems = (int64_t)(img / 16);
+  int st;
+  // 1. images of L_k^T (T operand of B-b) and of Linv (T operand of B-d)
+  {
+    const int64_t nfrag = (int64_t)K * nmb * nmk;
+    hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
+                       ldqs, strideq, M, nmb, nmk, nfrag, LTfr);
+    const int64_t nf1 = (int64_t)nmb * nmk;
+    hipLaunchKernelGGL((split_tri_kernel<true, true>), dim3((unsigned)((nf1 + 3) / 4)), dim3(256), 0, s, LinvT, ldl,
+                       (int64_t)0, M, nmb, nmk, nf1, LIfr);
+    if ((st = launch_status())) return st;
+  }
+  // 2. CG_k = (L_k^T A) diag(Gv_k)
+  hipLaunchKernelGGL(expert_bwd_c_kernel, dim3((unsigned)(K * nT * nTn)), dim3(256), 0, s, (const bf16x8*)Afr,
+                     (const bf16x8*)Lfr, (uint32_t)afr_bytes, (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K,
+                     M, N, Gv, ldg, CG, ldn, M * ldn, CGfr, img_elems);
+  if ((st = launch_status())) return st;
+  // 3. gA0 = q_mu G_mu - 2 A sum_k Gv_k
+  {
+    const int rows = 128;
+    const dim3 grid((unsigned)((N + 255) / 256), (unsigned)((M + rows - 1) / rows));
+    if (K <= 4)
+      hipLaunchKernelGGL(grad_a_base_kernel<4>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, rows,
+                         gA0, ldn);
+    else if (K <= 8)
+      hipLaunchKernelGGL(grad_a_base_kernel<8>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, rows,
+                         gA0, ldn);
+    else
+      hipLaunchKernelGGL(grad_a_base_kernel<16>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K,
+                         rows, gA0, ldn);
+    if ((st = launch_status())) return st;
+  }
+  // 4. gA (image) = 2 sum_k L_k CG_k + gA0
+  hipLaunchKernelGGL(expert_bwd_a_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)LTfr,
+                     (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)CGfr, (uint32_t)img, img_elems, nmk, nTn, K, M,
+                     N, gA0, ldn, gAfr);
+  if ((st = launch_status())) return st;
+  // 5. gKuf = Linv^T gA
+  hipLaunchKernelGGL(trsm_bwd_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)gAfr,
+                     (const bf16x8*)LIfr, (uint32_t)img, (uint32_t)mgp_x6_lower_bytes(M, 1), nmk, nmb, nTn, M, N, g_Kuf,
+                     ldk);
+  if ((st = launch_status())) return st;
+  // 6. grams over N
+  for (int k = 0; k < K; ++k) {
+    st = mgp_gram(A, lda, M, CG + (int64_t)k * M * ldn, ldn, M, N, 2.f, 1, g_q_sqrt + (int64_t)k * strideg, ldgs,
+                  gws, gwsb, stream);
+    if (st) return st;
+  }
+  st = mgp_gram(g_Kuf, ldk, M, A, lda, M, N, -1.f, 1, g_Lm, ldgl, gws, gwsb, stream);
+  if (st) return st;
+  st = mgp_gram(A, lda, M, Gmu, ldg, K, N, 1.f, 0, g_q_mu, ldgq, gws, gwsb, stream);
+  if (st) return st;
+  hipLaunchKernelGGL(sum_all_kernel, dim3(1), dim3(256), 0, s, Gv, (int64_t)K, N, ldg, g_var);
+  return launch_status();
 }

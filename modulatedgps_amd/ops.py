@@ -210,8 +210,9 @@ def split_upper_x6(LinvT, out=None):
     return out
 
 
-def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None):
-    """K4 on images: A's image (for expert_conditional_x6) and the stats [T, K+1, N]."""
+def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None):
+    """K4 on images: A's image (for expert_conditional_x6) and the stats [T, K+1, N];
+    also the f32 A when a buffer `A` [M, N] is given (training)."""
     _check(q_mu, "q_mu", 2)
     K = q_mu.shape[1]
     dev = q_mu.device
@@ -223,7 +224,7 @@ def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None):
         stats = padded(T * (K + 1), N, dev).unflatten(0, (T, K + 1))
     _lib.call("mgp_trsm_stats_x6", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
               q_mu.data_ptr(), _ld(q_mu), K, Afr.data_ptr(), Afr.numel(), stats.data_ptr(), _ld(stats),
-              _stream())
+              A.data_ptr() if A is not None else None, _ld(A) if A is not None else N, _stream())
     return Afr, stats
 
 
@@ -340,6 +341,46 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
               glv.data_ptr(), glva.data_ptr() if glva is not None else None, workspace.data_ptr(),
               workspace.numel(), _stream())
     return G, glv, glva
+
+
+def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):
+    """out[i][j] = alpha * sum_n X[i][n] Y[j][n] (tri: lower triangle, zeros above)."""
+    _check(X, "X", 2), _check(Y, "Y", 2)
+    MI, MJ = X.shape[0], Y.shape[0]
+    N = X.shape[1] if N is None else N
+    dev = X.device
+    if out is None:
+        out = padded(MI, MJ, dev)
+    nbytes = _lib.load().mgp_gram_workspace_bytes(MI, MJ, N, int(tri))
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    _lib.call("mgp_gram", X.data_ptr(), _ld(X), MI, Y.data_ptr(), _ld(Y), MJ, N, float(alpha), int(tri),
+              out.data_ptr(), _ld(out), workspace.data_ptr(), workspace.numel(), _stream())
+    return out
+
+
+def conditional_backward_x6(Afr, A, Lfr, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None):
+    """Backward of one layer's conditional (see include/mgp_hip.h): returns dict of
+    g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1])."""
+    K = q_mu.shape[1]
+    dev = q_mu.device
+    if out is None:
+        out = {"g_q_mu": padded(M, K, dev), "g_q_sqrt": padded(M, M, dev, batch=K),
+               "g_Kuf": padded(M, N, dev), "g_Lm": padded(M, M, dev),
+               "g_var": torch.empty(1, dtype=torch.float64, device=dev)}
+    nbytes = _lib.load().mgp_conditional_backward_workspace_bytes(M, N, K)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    if _ld(Gmu) != _ld(Gv):
+        raise ValueError("Gmu and Gv must share a leading dimension")
+    o = out
+    _lib.call("mgp_conditional_backward_x6", Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A), Lfr.data_ptr(),
+              Lfr.numel(), q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), q_mu.data_ptr(), _ld(q_mu),
+              LinvT.data_ptr(), _ld(LinvT), Gmu.data_ptr(), Gv.data_ptr(), _ld(Gmu), M, N, K,
+              o["g_q_mu"].data_ptr(), _ld(o["g_q_mu"]), o["g_q_sqrt"].data_ptr(), _ld(o["g_q_sqrt"]),
+              o["g_q_sqrt"].stride(0), o["g_Kuf"].data_ptr(), _ld(o["g_Kuf"]), o["g_Lm"].data_ptr(),
+              _ld(o["g_Lm"]), o["g_var"].data_ptr(), workspace.data_ptr(), workspace.numel(), _stream())
+    return out
 
 
 # --------------------------------------------------------------------------- K7

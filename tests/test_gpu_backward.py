@@ -65,3 +65,51 @@ def test_elbo_terms_backward(device, N, M, K, D, ls, S, modified):
     assert normwise(glv.cpu().numpy(), lik.grad.numpy()) < 1e-4
     if modified:
         assert normwise(glva.cpu().numpy(), av.grad.numpy()) < 1e-4
+
+
+@pytest.mark.parametrize("N,M,K,D,ls", [(2000, 64, 3, 2, 1.0), (4097, 200, 4, 3, 1.2), (8192, 256, 8, 8, 2.0)])
+def test_conditional_backward(device, N, M, K, D, ls):
+    """Backward of one layer's conditional: for loss = sum(G_mu * fmean + G_v * fvar)
+    with random cotangents, the gradients w.r.t. q_mu, tril(q_sqrt), A (-> Kuf =
+    L^-T gA and chol(Kuu) = -tril(gKuf A^T)) and the kernel variance (through
+    Knn) against float64 autograd at the same A and L^-1."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(7)
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
+    L = p.pred
+    f32 = lambda a: np.asarray(a, np.float32)
+    Xt, Zt = torch.as_tensor(f32(X), device=device), torch.as_tensor(f32(L["Z"]), device=device)
+    var = torch.as_tensor([L["variance"]], dtype=torch.float32, device=device)
+    lst = torch.as_tensor([ls], dtype=torch.float32, device=device)
+    qmu = torch.as_tensor(f32(L["q_mu"]), device=device)
+    qs = ops.as_padded(torch.as_tensor(f32(L["q_sqrt"])), device=device)
+    Gmu = ops.padded(K, N, device)
+    Gv = ops.padded(K, N, device)
+    Gmu.copy_(torch.as_tensor(rng.standard_normal((K, N)).astype(np.float32)))
+    Gv.copy_(torch.as_tensor(rng.standard_normal((K, N)).astype(np.float32)))
+    _, LinvT, _ = ops.kuu_potrf_trtri([Zt], [var], [lst], 1e-6)
+    Kfr = ops.rbf_kuf_x6(Xt, Zt, var, lst)
+    Tfr = ops.split_upper_x6(LinvT[0])
+    A = ops.padded(M, N, device)
+    Afr, _ = ops.trsm_stats_x6(Tfr, Kfr, qmu, M, N, A=A)
+    Lfr = ops.split_lower_x6(qs)
+    g = ops.conditional_backward_x6(Afr, A, Lfr, qs, qmu, LinvT[0], Gmu, Gv, M, N)
+    # float64 autograd at the device's own A and L^-1 (the kernels under test see
+    # exactly these inputs; A's own f32 error is a forward property, tested there)
+    A64 = torch.tensor(to_np(A)[:, :N], requires_grad=True)
+    Linv = to_np(LinvT[0]).T
+    q_mu = torch.tensor(f32(L["q_mu"]).astype(np.float64), requires_grad=True)
+    q_sqrt = torch.tensor(f32(L["q_sqrt"]).astype(np.float64), requires_grad=True)
+    v = torch.tensor(float(np.float32(L["variance"])), dtype=torch.float64, requires_grad=True)
+    fmean = (A64.T @ q_mu).T
+    LTA = torch.tril(q_sqrt).transpose(1, 2) @ A64
+    fvar = v - (A64 ** 2).sum(0)[None, :] + (LTA ** 2).sum(1)
+    loss = (torch.tensor(to_np(Gmu)[:, :N]) * fmean).sum() + (torch.tensor(to_np(Gv)[:, :N]) * fvar).sum()
+    loss.backward()
+    gKuf_ref = Linv.T @ A64.grad.numpy()                   # A = L^-1 Kuf
+    gLm_ref = -np.tril(gKuf_ref @ A64.detach().numpy().T)
+    assert normwise(to_np(g["g_Kuf"])[:, :N], gKuf_ref) < 1e-4
+    assert normwise(to_np(g["g_Lm"]), gLm_ref) < 1e-4
+    assert normwise(to_np(g["g_q_mu"]), q_mu.grad.numpy()) < 1e-4
+    assert normwise(to_np(g["g_q_sqrt"]), np.tril(q_sqrt.grad.numpy())) < 1e-4
+    assert float(g["g_var"].cpu()) == pytest.approx(float(v.grad), rel=1e-5)
