@@ -196,6 +196,28 @@ int mgp_conditional_backward_x6(const void* Afr, size_t afr_bytes, const float* 
                                 int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
                                 mgp_stream_t stream);
 
+/* Reverse mode of Lm = chol(Kuu) (models.py:141): gKuu = sym(Lm^-T Phi(Lm^T gL) Lm^-1),
+ * Phi = lower triangle with halved diagonal, in float64 from the float32 L,
+ * LinvT = (Lm^-1)^T (both from mgp_potrf_trtri / mgp_kuu_potrf_trtri) and gL
+ * (lower).  Output gKuu [M][ldo] float32, symmetric.
+ * Workspace: mgp_chol_backward_workspace_bytes(M). */
+size_t mgp_chol_backward_workspace_bytes(int64_t M);
+int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT, int64_t ldli, const float* gL,
+                      int64_t ldg, int64_t M, float* gKuu, int64_t ldo, void* workspace,
+                      size_t workspace_bytes, mgp_stream_t stream);
+
+/* Reverse mode of K(Z, X) (models.py:135,139) for a cotangent gK [M][ldg]:
+ * gZ [M][ldgz] (float), g_var and g_ls[n_ls] (double, device).  symmetric = 1
+ * for Kuu (X = Z, symmetric gK: Z enters both arguments).  accumulate = 1 adds
+ * to the outputs (to combine the Kuf and Kuu contributions).
+ * Workspace: mgp_rbf_backward_workspace_bytes(N, M, D). */
+size_t mgp_rbf_backward_workspace_bytes(int64_t N, int64_t M, int32_t D);
+int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                     int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                     const float* gK, int64_t ldg, int32_t symmetric, int32_t accumulate, float* gZ,
+                     int64_t ldgz, double* g_var, double* g_ls, void* workspace, size_t workspace_bytes,
+                     mgp_stream_t stream);
+
 /* ---------------------------------------------------------------- K7
  * Whitened Gaussian KL (GPflow gauss_kl(q_mu, q_sqrt, K=None), reached through
  * SVGP.prior_kl at models.py:79):

@@ -521,6 +521,64 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   quad_to_global(Bt(i, c), Mp, u);
 }
 
+// ------------------------------------------------------------------ Cholesky backward
+// Reverse mode of Lm = chol(Kuu) (GPflow base_conditional's cholesky,
+// models.py:141), as in PyTorch / Murray (2016):
+//   P = Phi(Lm^T gL)  (lower triangle, diagonal halved),  S = Lm^-T P Lm^-1,
+//   gKuu = (S + S^T) / 2,
+// all in float64 (M^3 work; Kuu is badly conditioned).  dgemm: C = op(A) op(B),
+// 64 x 64 tiles, 256 threads x 4 x 4 outputs, 16-deep LDS chunks.
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A, int64_t lda,
+                                                    const double* __restrict__ B, int64_t ldb,
+                                                    double* __restrict__ C, int64_t ldc, int64_t M) {
+  __shared__ double sa[16][64 + 1], sb[16][64 + 1];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
+  double acc[4][4] = {};
+  for (int64_t k0 = 0; k0 < M; k0 += 16) {
+    for (int idx = threadIdx.x; idx < 16 * 64; idx += 256) {
+      const int kk = idx / 64, r = idx % 64;
+      const int64_t k = k0 + kk, i = i0 + r, j = j0 + r;
+      sa[kk][r] = (k < M && i < M) ? (TA ? A[k * lda + i] : A[i * lda + k]) : 0.0;
+      sb[kk][r] = (k < M && j < M) ? (TB ? B[j * ldb + k] : B[k * ldb + j]) : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { a[q] = sa[kk][ty + 16 * q]; b[q] = sb[kk][tx + 16 * q]; }
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi)
+#pragma unroll
+        for (int qj = 0; qj < 4; ++qj) acc[qi][qj] = fma(a[qi], b[qj], acc[qi][qj]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qi = 0; qi < 4; ++qi)
+#pragma unroll
+    for (int qj = 0; qj < 4; ++qj) {
+      const int64_t i = i0 + ty + 16 * qi, j = j0 + tx + 16 * qj;
+      if (i < M && j < M) C[i * ldc + j] = acc[qi][qj];
+    }
+}
+
+// mode 0: dst = f64(src) (src f32);  1: dst = f64(src^T);  2: Phi (tril, diag / 2) in place on f64;
+// 3: out32 = (S + S^T) / 2 -> f32 and out64 (optional)
+__global__ __launch_bounds__(256) void chol_bwd_elem_kernel(int mode, const float* __restrict__ src32,
+                                                            int64_t lds, double* __restrict__ d, int64_t M,
+                                                            float* __restrict__ out32, int64_t ldo) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= M * M) return;
+  const int64_t i = idx / M, j = idx % M;
+  if (mode == 0) d[idx] = (double)src32[i * lds + j];
+  else if (mode == 1) d[idx] = (double)src32[j * lds + i];
+  else if (mode == 2) d[idx] = (j < i) ? d[idx] : (j == i ? 0.5 * d[idx] : 0.0);
+  else out32[i * ldo + j] = (float)(0.5 * (d[i * M + j] + d[j * M + i]));
+}
+
 }  // namespace mgp
 
 using namespace mgp;
@@ -612,4 +670,39 @@ extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M
   a.L = L; a.LinvT = LinvT; a.ldl = ldl; a.strideL = strideL;
   a.info = info; a.M = M;
   return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" size_t mgp_chol_backward_workspace_bytes(int64_t M) {
+  return (size_t)(M > 0 ? M : 1) * (size_t)(M > 0 ? M : 1) * 4 * sizeof(double);
+}
+
+extern "C" int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT, int64_t ldli, const float* gL,
+                                 int64_t ldg, int64_t M, float* gKuu, int64_t ldo, void* workspace,
+                                 size_t workspace_bytes, mgp_stream_t stream) {
+  if (!L) return -1;
+  if (ldl < M) return -2;
+  if (!LinvT) return -3;
+  if (ldli < M) return -4;
+  if (!gL) return -5;
+  if (ldg < M) return -6;
+  if (M < 0) return -7;
+  if (!gKuu) return -8;
+  if (ldo < M) return -9;
+  if (M == 0) return MGP_OK;
+  if (!workspace || workspace_bytes < mgp_chol_backward_workspace_bytes(M)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  double* Ld = (double*)workspace;
+  double* Li = Ld + M * M;   // Linv = LinvT^T
+  double* G = Li + M * M;
+  double* T = G + M * M;
+  const dim3 eg((unsigned)((M * M + 255) / 256)), gg((unsigned)((M + 63) / 64), (unsigned)((M + 63) / 64));
+  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, L, ldl, Ld, M, nullptr, (int64_t)0);
+  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 1, LinvT, ldli, Li, M, nullptr, (int64_t)0);
+  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, gL, ldg, G, M, nullptr, (int64_t)0);
+  hipLaunchKernelGGL((dgemm_kernel<true, false>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M);      // L^T gL
+  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 2, nullptr, (int64_t)0, T, M, nullptr, (int64_t)0);
+  hipLaunchKernelGGL((dgemm_kernel<false, false>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M);     // P Linv
+  hipLaunchKernelGGL((dgemm_kernel<true, false>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M);      // Linv^T (.)
+  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 3, nullptr, (int64_t)0, T, M, gKuu, ldo);
+  return launch_status();
 }

@@ -174,6 +174,126 @@ static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, 
   return MGP_ERR_UNSUPPORTED;
 }
 
+// ------------------------------------------------------------------ RBF backward
+// Reverse mode of K(Z, X) = var exp(-1/2 sum_d c_d^2 (z_d - x_d)^2), c = 1 / l
+// (models.py:135,139) for a cotangent gK [M][N]: with w_mn = gK_mn k_mn
+//   g_var = sum w / var,   g_z_md = -c_d^2 (z_md S0_m - S1_md),
+//   g_l_d = c_d^3 sum_m (z_md^2 S0_m - 2 z_md S1_md + S2_md),
+//   S0_m = sum_n w_mn, S1_md = sum_n w_mn x_nd, S2_md = sum_n w_mn x_nd^2  (float64).
+// For Kuu (X = Z, symmetric gK) z enters both arguments: g_z doubles.
+// Kernel 1: 4 waves x 4 rows of Z per block, lanes stride over an n-chunk;
+// per-(chunk, row) partials.  Kernel 2 folds the chunks and writes the grads.
+template <int DMAX>
+__global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restrict__ X, int64_t ldx,
+                                                           const float* __restrict__ Z, int64_t ldz, int64_t N,
+                                                           int64_t M, int D, const float* __restrict__ variance,
+                                                           const float* __restrict__ ls, int n_ls,
+                                                           const float* __restrict__ gK, int64_t ldg,
+                                                           int64_t nchunk, double* __restrict__ part) {
+  constexpr int NS = 1 + 2 * DMAX;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * 16 + 4 * w;
+  const int64_t nb = (int64_t)blockIdx.y * nchunk;
+  const int64_t ne = (nb + nchunk < N) ? nb + nchunk : N;
+  float c2[DMAX], z[4][DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    const float c = (d < D) ? 1.f / ls[n_ls == 1 ? 0 : d] : 0.f;
+    c2[d] = c * c;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) z[r][d] = (m0 + r < M && d < D) ? Z[(m0 + r) * ldz + d] : 0.f;
+  const float var = variance[0];
+  double acc[4][NS];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) acc[r][j] = 0.0;
+  for (int64_t n = nb + lane; n < ne; n += 64) {
+    float x[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[n * ldx + d] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (m0 + r >= M) break;
+      float q = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        const float df = z[r][d] - x[d];
+        q = fmaf(c2[d] * df, df, q);
+      }
+      const double wv = (double)gK[(m0 + r) * ldg + n] * (double)(var * __expf(-0.5f * q));
+      acc[r][0] += wv;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        const double xd = (double)x[d];
+        acc[r][1 + d] = fma(wv, xd, acc[r][1 + d]);
+        acc[r][1 + DMAX + d] = fma(wv * xd, xd, acc[r][1 + DMAX + d]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      double v = acc[r][j];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0 && m0 + r < M) part[((int64_t)blockIdx.y * M + m0 + r) * NS + j] = v;
+    }
+}
+
+template <int DMAX>
+__global__ __launch_bounds__(256) void rbf_bwd_finish_kernel(const double* __restrict__ part, int nchunks, int64_t M,
+                                                             int D, const float* __restrict__ Z, int64_t ldz,
+                                                             const float* __restrict__ variance,
+                                                             const float* __restrict__ ls, int n_ls, float zfactor,
+                                                             int accumulate, float* __restrict__ gZ, int64_t ldgz,
+                                                             double* __restrict__ g_var, double* __restrict__ g_ls) {
+  constexpr int NS = 1 + 2 * DMAX;
+  __shared__ double scratch[16];
+  double gl[DMAX], s0tot = 0.0;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) gl[d] = 0.0;
+  double c[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) c[d] = (d < D) ? 1.0 / (double)ls[n_ls == 1 ? 0 : d] : 0.0;
+  for (int64_t m = threadIdx.x; m < M; m += 256) {
+    double S[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) S[j] = 0.0;
+    for (int ch = 0; ch < nchunks; ++ch)
+#pragma unroll
+      for (int j = 0; j < NS; ++j) S[j] += part[((int64_t)ch * M + m) * NS + j];
+    s0tot += S[0];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      if (d >= D) break;
+      const double zd = (double)Z[m * ldz + d];
+      const double gz = -zfactor * c[d] * c[d] * (zd * S[0] - S[1 + d]);
+      gZ[m * ldgz + d] = (float)(accumulate ? (double)gZ[m * ldgz + d] + gz : gz);
+      gl[d] += c[d] * c[d] * c[d] * (zd * zd * S[0] - 2.0 * zd * S[1 + d] + S[1 + DMAX + d]);
+    }
+  }
+  const double var = (double)variance[0];
+  const double gv = block_sum<double>(s0tot, scratch) / var;
+  if (threadIdx.x == 0) *g_var = accumulate ? *g_var + gv : gv;
+  double giso = 0.0;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    if (d >= D) break;
+    __syncthreads();
+    const double v = block_sum<double>(gl[d], scratch);
+    if (threadIdx.x == 0) {
+      if (n_ls == 1) giso += v;
+      else g_ls[d] = accumulate ? g_ls[d] + v : v;
+    }
+  }
+  if (threadIdx.x == 0 && n_ls == 1) g_ls[0] = accumulate ? g_ls[0] + giso : giso;
+}
+
 }  // namespace mgp
 
 using namespace mgp;
@@ -254,5 +374,64 @@ extern "C" int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64
   MGP_RBF_X6_CASE(16)
   MGP_RBF_X6_CASE(32)
 #undef MGP_RBF_X6_CASE
+  return MGP_ERR_UNSUPPORTED;
+}
+
+static int64_t rbf_bwd_chunk(int64_t N) { return 4096; }
+
+extern "C" size_t mgp_rbf_backward_workspace_bytes(int64_t N, int64_t M, int32_t D) {
+  int dm = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16 : 32;
+  const int64_t nch = (N + rbf_bwd_chunk(N) - 1) / rbf_bwd_chunk(N);
+  return (size_t)((nch > 0 ? nch : 1) * (M > 0 ? M : 1) * (1 + 2 * dm)) * sizeof(double);
+}
+
+extern "C" int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                                int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                                const float* gK, int64_t ldg, int32_t symmetric, int32_t accumulate, float* gZ,
+                                int64_t ldgz, double* g_var, double* g_ls, void* workspace,
+                                size_t workspace_bytes, mgp_stream_t stream) {
+  if (!X) return -1;
+  if (ldx < D) return -2;
+  if (!Z) return -3;
+  if (ldz < D) return -4;
+  if (N < 0) return -5;
+  if (M < 0) return -6;
+  if (D < 1) return -7;
+  if (D > 32) return MGP_ERR_UNSUPPORTED;
+  if (!variance) return -8;
+  if (!lengthscales) return -9;
+  if (n_ls != 1 && n_ls != D) return -10;
+  if (!gK) return -11;
+  if (ldg < N) return -12;
+  if (!gZ) return -15;
+  if (ldgz < D) return -16;
+  if (!g_var) return -17;
+  if (!g_ls) return -18;
+  if (M == 0) return MGP_OK;
+  if (!workspace || workspace_bytes < mgp_rbf_backward_workspace_bytes(N, M, D)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t chunk = rbf_bwd_chunk(N);
+  const int nch = (int)((N + chunk - 1) / chunk);
+  double* part = (double*)workspace;
+  const float zf = symmetric ? 2.f : 1.f;
+  const dim3 grid((unsigned)((M + 15) / 16), (unsigned)(nch > 0 ? nch : 1));
+#define MGP_RBF_BWD_CASE(DM)                                                                                  \
+  if (D <= DM) {                                                                                              \
+    if (nch > 0)                                                                                              \
+      hipLaunchKernelGGL(rbf_bwd_rows_kernel<DM>, grid, dim3(256), 0, s, X, ldx, Z, ldz, N, M, D, variance,    \
+                         lengthscales, n_ls, gK, ldg, chunk, part);                                           \
+    else                                                                                                      \
+      hipMemsetAsync(part, 0, mgp_rbf_backward_workspace_bytes(N, M, D), s);                                  \
+    hipLaunchKernelGGL(rbf_bwd_finish_kernel<DM>, dim3(1), dim3(256), 0, s, part, nch > 0 ? nch : 1, M, D, Z,  \
+                       ldz, variance, lengthscales, n_ls, zf, accumulate, gZ, ldgz, g_var, g_ls);             \
+    return launch_status();                                                                                   \
+  }
+  MGP_RBF_BWD_CASE(1)
+  MGP_RBF_BWD_CASE(2)
+  MGP_RBF_BWD_CASE(4)
+  MGP_RBF_BWD_CASE(8)
+  MGP_RBF_BWD_CASE(16)
+  MGP_RBF_BWD_CASE(32)
+#undef MGP_RBF_BWD_CASE
   return MGP_ERR_UNSUPPORTED;
 }

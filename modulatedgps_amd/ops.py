@@ -343,6 +343,44 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
     return G, glv, glva
 
 
+def rbf_backward(X, Z, variance, lengthscales, gK, symmetric=False, accumulate=False, gZ=None, g_var=None,
+                 g_ls=None, workspace=None):
+    """Reverse mode of K(Z, X): (gZ [M, D] float32, g_var float64 [1], g_ls float64 [n_ls])."""
+    _check(X, "X", 2), _check(Z, "Z", 2), _check(gK, "gK", 2)
+    N, D = X.shape
+    M = Z.shape[0]
+    dev = X.device
+    n_ls = lengthscales.numel()
+    if gZ is None:
+        gZ = torch.zeros(M, D, dtype=torch.float32, device=dev)
+    if g_var is None:
+        g_var = torch.zeros(1, dtype=torch.float64, device=dev)
+    if g_ls is None:
+        g_ls = torch.zeros(n_ls, dtype=torch.float64, device=dev)
+    nbytes = _lib.load().mgp_rbf_backward_workspace_bytes(N, M, D)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    _lib.call("mgp_rbf_backward", X.data_ptr(), _ld(X), Z.data_ptr(), _ld(Z), N, M, D, variance.data_ptr(),
+              lengthscales.data_ptr(), n_ls, gK.data_ptr(), _ld(gK), int(symmetric), int(accumulate),
+              gZ.data_ptr(), _ld(gZ), g_var.data_ptr(), g_ls.data_ptr(), workspace.data_ptr(), workspace.numel(),
+              _stream())
+    return gZ, g_var, g_ls
+
+
+def chol_backward(L, LinvT, gL, out=None, workspace=None):
+    """gKuu [M, M] (float32, symmetric) from the gradient w.r.t. Lm = chol(Kuu)."""
+    _check(L, "L", 2), _check(LinvT, "LinvT", 2), _check(gL, "gL", 2)
+    M = L.shape[0]
+    if out is None:
+        out = padded(M, M, L.device)
+    nbytes = _lib.load().mgp_chol_backward_workspace_bytes(M)
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, L.device)
+    _lib.call("mgp_chol_backward", L.data_ptr(), _ld(L), LinvT.data_ptr(), _ld(LinvT), gL.data_ptr(), _ld(gL), M,
+              out.data_ptr(), _ld(out), workspace.data_ptr(), workspace.numel(), _stream())
+    return out
+
+
 def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):
     """out[i][j] = alpha * sum_n X[i][n] Y[j][n] (tri: lower triangle, zeros above)."""
     _check(X, "X", 2), _check(Y, "Y", 2)

@@ -113,3 +113,51 @@ def test_conditional_backward(device, N, M, K, D, ls):
     assert normwise(to_np(g["g_q_mu"]), q_mu.grad.numpy()) < 1e-4
     assert normwise(to_np(g["g_q_sqrt"]), np.tril(q_sqrt.grad.numpy())) < 1e-4
     assert float(g["g_var"].cpu()) == pytest.approx(float(v.grad), rel=1e-5)
+
+
+@pytest.mark.parametrize("M,D,ls", [(64, 2, 0.8), (200, 3, 1.0), (1024, 8, 1.0)])
+def test_chol_backward(device, M, D, ls):
+    """Reverse mode of Lm = chol(Kuu) against float64 autograd."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(11)
+    Z = rng.standard_normal((M, D)).astype(np.float32)
+    Zt = torch.as_tensor(Z, device=device)
+    var = torch.tensor([0.7], device=device)
+    lst = torch.tensor([ls], dtype=torch.float32, device=device)
+    L, LinvT, info = ops.kuu_potrf_trtri([Zt], [var], [lst], 1e-6, want_L=True)
+    gL = ops.padded(M, M, device)
+    gL.copy_(torch.as_tensor(np.tril(rng.standard_normal((M, M))).astype(np.float32)))
+    g = ops.chol_backward(L[0], LinvT[0], gL)
+    z64 = torch.tensor(Z.astype(np.float64))
+    Kuu = (GR.rbf(z64, z64, 0.7, float(np.float32(ls))) + 1e-6 * torch.eye(M, dtype=torch.float64))
+    Kuu = Kuu.detach().requires_grad_(True)
+    (torch.linalg.cholesky(Kuu) * torch.tensor(to_np(gL))).sum().backward()
+    ref = 0.5 * (Kuu.grad + Kuu.grad.T).numpy()
+    assert normwise(to_np(g), ref) < 1e-4
+
+
+@pytest.mark.parametrize("N,M,D,ard,sym", [(3000, 64, 2, False, False), (5000, 200, 3, True, False),
+                                            (200, 200, 3, True, True), (1024, 1024, 8, False, True)])
+def test_rbf_backward(device, N, M, D, ard, sym):
+    """Reverse mode of K(Z, X) (and of K(Z, Z) with a symmetric cotangent) w.r.t.
+    Z, the variance and the lengthscales against float64 autograd."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(12)
+    Z = rng.standard_normal((M, D)).astype(np.float32)
+    X = Z if sym else rng.standard_normal((N, D)).astype(np.float32)
+    N = X.shape[0]
+    lsv = (np.linspace(0.7, 1.3, D) if ard else np.array([0.9])).astype(np.float32)
+    gK = rng.standard_normal((M, N)).astype(np.float32)
+    if sym:
+        gK = 0.5 * (gK + gK.T)
+    dev = lambda a: torch.as_tensor(a, device=device)
+    gZ, gv, gl = ops.rbf_backward(dev(X), dev(Z), dev(np.float32([0.6])), dev(lsv), ops.as_padded(dev(gK)),
+                                  symmetric=sym)
+    z64 = torch.tensor(Z.astype(np.float64), requires_grad=True)
+    v64 = torch.tensor(float(np.float32(0.6)), dtype=torch.float64, requires_grad=True)
+    l64 = torch.tensor(lsv.astype(np.float64), requires_grad=True)
+    x64 = z64 if sym else torch.tensor(X.astype(np.float64))
+    (GR.rbf(z64, x64, v64, l64) * torch.tensor(gK.astype(np.float64))).sum().backward()
+    assert normwise(to_np(gZ), z64.grad.numpy()) < 1e-4
+    assert float(gv.cpu()) == pytest.approx(float(v64.grad), rel=1e-4)
+    assert normwise(gl.cpu().numpy(), l64.grad.numpy()) < 1e-4
