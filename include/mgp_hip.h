@@ -311,6 +311,23 @@ int mgp_philox_noise(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int3
 int mgp_philox_normal2(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S, float* z,
                        mgp_stream_t stream);
 
+/* ---------------------------------------------------------------- optimizer
+ * KL gradient folded into the ELBO gradient: g_q_mu -= q_mu / num_data,
+ * g_q_sqrt[k] -= tril(L_k - diag(1 / L_k[m,m])) / num_data (models.py:79). */
+int mgp_kl_grad(const float* q_mu, int64_t ldq, const float* q_sqrt, int64_t ldqs, int64_t strideq,
+                int64_t M, int32_t K, double num_data, float* g_q_mu, int64_t ldgq, float* g_q_sqrt,
+                int64_t ldgs, int64_t strideg, mgp_stream_t stream);
+
+/* One TF-legacy Adam step (tf.optimizers.Adam, utils/training_utils.py:6,10;
+ * eps outside the bias correction) on a [rows][cols] block (leading dimension
+ * ld) of parameter theta; g = d ELBO / d theta times grad_sign (-1 minimises
+ * -ELBO), float or double (grad_is_double); m1, m2, u: rows * cols dense.
+ * u != NULL: theta = softplus(u) is a positive parameter and Adam runs on u
+ * (GPflow positive()).  t = 1-based step count. */
+int mgp_adam_step(float* theta, float* u, const void* g, int32_t grad_is_double, int64_t ldg, float* m1,
+                  float* m2, int64_t rows, int64_t cols, int64_t ld, float lr, float beta1, float beta2,
+                  float eps, int64_t t, float grad_sign, mgp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,11 @@ SIGNATURES = {
                                               c_ptr]),
     "mgp_trsm_stats_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                          c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "mgp_kl_grad": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, ctypes.c_double, c_ptr,
+                                   c_i64, c_ptr, c_i64, c_i64, c_ptr]),
+    "mgp_adam_step": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_i32, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_i64,
+                                     ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, c_i64,
+                                     ctypes.c_float, c_ptr]),
     "mgp_rbf_backward_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
     "mgp_rbf_backward": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i32,
                                         c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size,

@@ -192,7 +192,7 @@ class SVGPModified:
             Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"))
         with _Stage(timing, "trsm_stats"):
             Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, M, N, Afr=bufs.get("Afr"),
-                                           stats=bufs.get("stats"))
+                                           stats=bufs.get("stats"), A=bufs.get("A32"))
         with _Stage(timing, "expert_cond"):
             return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, K,
                                              fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
@@ -256,8 +256,8 @@ class SMGP(SGP):
         self.last_info = None
 
     # ------------------------------------------------------------------ internals
-    def _buffers(self, N):
-        key = (N, conditional_mode())
+    def _buffers(self, N, train=False):
+        key = (N, conditional_mode(), bool(train))
         b = self._bufs.get(key)
         if b is not None:
             return b
@@ -295,27 +295,48 @@ class SMGP(SGP):
         b["x6"] = x6
         if Mf == Ma and self.pred_layer.Z.shape[1] == self.assign_layer.Z.shape[1]:
             b["LinvT2"] = ops.padded(Mf, Mf, dev, batch=2)
+        b["train"] = bool(train)
+        if train:
+            if not x6:
+                raise NotImplementedError("the training step runs on the x6 conditional path")
+            if "LinvT2" in b:
+                b["L2"] = ops.padded(Mf, Mf, dev, batch=2)
+            for L, M in (("f", Mf), ("a", Ma)):  # kept for the backward pass
+                b["Afr_" + L] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
+                b["A32_" + L] = ops.padded(M, N, dev)
+            b["G"] = ops.padded(4 * K, N, dev).unflatten(0, (4, K))
+            b["ws_cbwd"] = torch.empty(ops.conditional_backward_workspace_bytes(Mx, N, K), dtype=torch.uint8,
+                                       device=dev)
         self._bufs[key] = b
         return b
 
     def _factorise(self, b):
-        """Kuu of both layers and their batched Cholesky + inverse (one K3 sweep)."""
+        """Kuu of both layers and their batched Cholesky + inverse (one K3 sweep).
+        Training buffers also keep L (b["L_f"], b["L_a"]) for the backward pass."""
         pf, pa = self.pred_layer, self.assign_layer
+        train = b.get("train", False)
         if "LinvT2" in b:
             if pf.Z.stride(0) != pa.Z.stride(0):
                 pa.Z = pa.Z.contiguous()
                 pf.Z = pf.Z.contiguous()
-            _, LinvT, info = ops.kuu_potrf_trtri(
+            Lo, LinvT, info = ops.kuu_potrf_trtri(
                 [pf.Z, pa.Z], [pf.kernel.variance, pa.kernel.variance],
-                [pf.kernel.lengthscales, pa.kernel.lengthscales], default_jitter(), LinvT=b["LinvT2"])
+                [pf.kernel.lengthscales, pa.kernel.lengthscales], default_jitter(), LinvT=b["LinvT2"],
+                L=b.get("L2"), want_L=train)
             self.last_info = info
+            if train:
+                b["L_f"], b["L_a"] = Lo[0], Lo[1]
+            b["LinvT_f"], b["LinvT_a"] = LinvT[0], LinvT[1]
             return LinvT[0], LinvT[1]
         outs = []
         infos = []
-        for layer in (pf, pa):
-            _, LinvT, info = layer.factorise()
+        for name, layer in (("f", pf), ("a", pa)):
+            Lo, LinvT, info = layer.factorise(want_L=train)
             outs.append(LinvT[0])
             infos.append(info)
+            if train:
+                b["L_" + name] = Lo[0]
+            b["LinvT_" + name] = LinvT[0]
         self.last_info = torch.cat(infos)
         return outs[0], outs[1]
 
@@ -324,7 +345,7 @@ class SMGP(SGP):
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
-    def conditionals(self, X, timing=None, kl_out=None):
+    def conditionals(self, X, timing=None, kl_out=None, train=False):
         """(mu_f, var_f, mu_a, var_a), each an expert-major [K, N] device view.
 
         x6 mode: K1 and the tril(q_sqrt) images of both layers (and, when kl_out
@@ -332,7 +353,7 @@ class SMGP(SGP):
         latency-bound K3 sweep, which occupies only a few CUs."""
         X = self.pred_layer.kernel._x(X)
         N = X.shape[0]
-        b = self._buffers(N)
+        b = self._buffers(N, train)
         layers = (("f", self.pred_layer), ("a", self.assign_layer))
         images = {}
         if b["x6"]:
@@ -355,7 +376,7 @@ class SMGP(SGP):
         for L, layer in layers:
             bufs = {"Kuf": b["Kuf_" + L], "A": b["A_" + L], "stats": b["stats_" + L],
                     "fmean": b["mu_" + L], "fvar": b["var_" + L], "ws_expert": b["ws_expert"],
-                    "Afr": b.get("Afr"), "Tfr": b.get("Tfr")}
+                    "Afr": b.get("Afr_" + L, b.get("Afr")), "Tfr": b.get("Tfr"), "A32": b.get("A32_" + L)}
             layer.conditional_kn(X, LinvT[L], bufs=bufs, timing=timing, images=images.get(L))
         if kl_out is not None and not b["x6"]:
             with _Stage(timing, "gauss_kl"):
@@ -404,6 +425,89 @@ class SMGP(SGP):
         ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"],
                          out64=b["elbo64"])
         return b["elbo64"] if return64 else b["elbo"]
+
+    # ------------------------------------------------------------------ training
+    def trainable_parameters(self):
+        """[(name, tensor, transform)] of every trainable variable (Z, q_mu,
+        q_sqrt (lower triangle), kernel variance / lengthscales (softplus) of both layers,
+        and the shared Gaussian likelihood variance (softplus))."""
+        ps = []
+        for name, layer in (("pred", self.pred_layer), ("assign", self.assign_layer)):
+            ps += [(name + ".Z", layer.Z, "free"), (name + ".q_mu", layer.q_mu, "free"),
+                   (name + ".q_sqrt", layer.q_sqrt, "free"),
+                   (name + ".variance", layer.kernel.variance, "positive"),
+                   (name + ".lengthscales", layer.kernel.lengthscales, "positive")]
+        ps.append(("lik_variance", self.likelihood.likelihood.variance, "positive"))
+        if self._assign_lik_var() is not None:
+            ps.append(("assign_lik_variance", self.assign_likelihood.likelihood.variance, "positive"))
+        return ps
+
+    def elbo_and_grad(self, X, Y, noise=None, seed=None, n_offset=0, n_total=None, process_group=None,
+                      timing=None):
+        """ELBO (0-d float32) and its gradient w.r.t. every constrained parameter of
+        trainable_parameters() (dict name -> device tensor), i.e. the GradientTape pass
+        of run_adam's optimisation step (training_utils.py:10) on the HIP kernels:
+        K6 backward -> per layer conditional backward (x6) -> Cholesky backward -> RBF
+        backward (Kuf and Kuu) -> + KL.  Data-parallel: one all-reduce of the
+        data-term gradients per step (the KL part is added after it)."""
+        X = self.pred_layer.kernel._x(X)
+        N = X.shape[0]
+        Yd = _to_dev(Y, self.device).reshape(-1).contiguous()
+        b = self._buffers(N, train=True)
+        kl = b["kl"]
+        mu_f, var_f, mu_a, var_a = self.conditionals(X, timing=timing, kl_out=kl, train=True)
+        lik_var = self.likelihood.likelihood.variance.reshape(-1)
+        alv = self._assign_lik_var()
+        if seed is None and noise is None:
+            seed = self.next_seed()
+        with _Stage(timing, "elbo_terms"):
+            ops.elbo_terms(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU, noise=noise,
+                           seed=seed or 0, n_offset=n_offset, out=b["data_sum"], assign_lik_var=alv)
+        n_batch = n_total if n_total is not None else N
+        with _Stage(timing, "elbo_terms_bwd"):
+            G, glv, glva = ops.elbo_terms_backward(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU,
+                                                   noise=noise, seed=seed or 0, n_offset=n_offset,
+                                                   scale=1.0 / n_batch, assign_lik_var=alv, G=b["G"])
+        grads = {"lik_variance": glv}
+        if alv is not None:
+            grads["assign_lik_variance"] = glva
+        for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
+            M = layer.num_inducing
+            with _Stage(timing, "conditional_bwd"):
+                g = ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], b["Lfr_" + L], layer.q_sqrt,
+                                                layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
+                                                workspace=b["ws_cbwd"])
+            with _Stage(timing, "chol_bwd"):
+                gKuu = ops.chol_backward(b["L_" + L], b["LinvT_" + L], g["g_Lm"])
+            with _Stage(timing, "rbf_bwd"):
+                k = layer.kernel
+                gZ, gvar, gls = ops.rbf_backward(X, layer.Z, k.variance, k.lengthscales, g["g_Kuf"],
+                                                 accumulate=True, g_var=g["g_var"],
+                                                 gZ=torch.zeros_like(layer.Z),
+                                                 g_ls=torch.zeros(k.lengthscales.numel(), dtype=torch.float64,
+                                                                  device=self.device))
+                ops.rbf_backward(layer.Z, layer.Z, k.variance, k.lengthscales, gKuu, symmetric=True,
+                                 accumulate=True, gZ=gZ, g_var=gvar, g_ls=gls)
+            grads.update({name + ".Z": gZ, name + ".variance": gvar, name + ".lengthscales": gls,
+                          name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]})
+        if process_group is not None:
+            import torch.distributed as dist
+            with _Stage(timing, "allreduce"):
+                dist.all_reduce(b["data_sum"], op=dist.ReduceOp.SUM, group=process_group)
+                for t in grads.values():
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=process_group)
+        num_data = self.num_data if self.num_data is not None else n_batch
+        for name, layer in (("pred", self.pred_layer), ("assign", self.assign_layer)):
+            ops.kl_grad(layer.q_mu, layer.q_sqrt, num_data, grads[name + ".q_mu"], grads[name + ".q_sqrt"])
+        ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"], out64=b["elbo64"])
+        return b["elbo"], grads
+
+    def training_loss_closure(self, data_iter, compile=True):
+        """GPflow ExternalDataTrainingLossMixin.training_loss_closure: () -> -ELBO on the next batch."""
+        def closure():
+            X, Y = next(data_iter)
+            return self.training_loss((X, Y))
+        return closure
 
     def elbo(self, data, **kw):
         X, Y = data

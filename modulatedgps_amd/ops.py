@@ -381,6 +381,25 @@ def chol_backward(L, LinvT, gL, out=None, workspace=None):
     return out
 
 
+def kl_grad(q_mu, q_sqrt, num_data, g_q_mu, g_q_sqrt):
+    """Fold -KL / num_data into the ELBO gradients (in place)."""
+    M, K = q_mu.shape
+    _lib.call("mgp_kl_grad", q_mu.data_ptr(), _ld(q_mu), q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), M, K,
+              float(num_data), g_q_mu.data_ptr(), _ld(g_q_mu), g_q_sqrt.data_ptr(), _ld(g_q_sqrt),
+              g_q_sqrt.stride(0), _stream())
+
+
+def adam_step(theta, grad, m1, m2, t, lr, u=None, beta1=0.9, beta2=0.999, eps=1e-7, grad_sign=-1.0):
+    """One TF-legacy Adam step on theta (2-D view [rows, cols] with leading dimension),
+    gradient of the ELBO (grad_sign -1 minimises -ELBO); u: unconstrained softplus shadow."""
+    rows, cols = theta.shape
+    if grad.shape[-1] != cols:
+        raise ValueError("gradient / parameter shape mismatch")
+    _lib.call("mgp_adam_step", theta.data_ptr(), u.data_ptr() if u is not None else None, grad.data_ptr(),
+              int(grad.dtype == torch.float64), _ld(grad), m1.data_ptr(), m2.data_ptr(), rows, cols, _ld(theta),
+              float(lr), float(beta1), float(beta2), float(eps), int(t), float(grad_sign), _stream())
+
+
 def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):
     """out[i][j] = alpha * sum_n X[i][n] Y[j][n] (tri: lower triangle, zeros above)."""
     _check(X, "X", 2), _check(Y, "Y", 2)
@@ -395,6 +414,10 @@ def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):
     _lib.call("mgp_gram", X.data_ptr(), _ld(X), MI, Y.data_ptr(), _ld(Y), MJ, N, float(alpha), int(tri),
               out.data_ptr(), _ld(out), workspace.data_ptr(), workspace.numel(), _stream())
     return out
+
+
+def conditional_backward_workspace_bytes(M, N, K):
+    return int(_lib.load().mgp_conditional_backward_workspace_bytes(M, N, K))
 
 
 def conditional_backward_x6(Afr, A, Lfr, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None):

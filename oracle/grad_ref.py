@@ -40,7 +40,7 @@ def layer_conditional(X, L):
     """Whitened SVGP marginals (models.py:129-144): fmean, fvar [N, K] and A [M, N]."""
     Z = L["Z"]
     M = Z.shape[0]
-    Kuu = rbf(Z, Z, L["variance"], L["lengthscales"]) + JITTER * torch.eye(M, dtype=torch.float64)
+    Kuu = rbf(Z, Z, L["variance"], L["lengthscales"]) + JITTER * torch.eye(M, dtype=Z.dtype)
     Lm = torch.linalg.cholesky(Kuu)
     Kuf = rbf(Z, X, L["variance"], L["lengthscales"])
     A = torch.linalg.solve_triangular(Lm, Kuf, upper=False)

@@ -1,0 +1,146 @@
+"""GPU parity of the training step (utils/training_utils.py:4-28 run_adam):
+the full ELBO gradient assembled by SMGP.elbo_and_grad (K6 backward -> conditional
+backward -> Cholesky backward -> RBF backward -> KL) against float64 autograd of
+oracle/grad_ref.py at the same explicit noise, and the TF-legacy Adam kernel
+against cpu_ref.adam_tf_legacy_step.
+
+Tolerance of the end-to-end gradient (normwise per parameter block, float32
+kernels vs float64 autograd): max(3e-4, 1.5 x the error of float32 torch
+autograd of the same oracle graph, measured in the test).  The Z / lengthscale
+/ variance gradients are sums of large opposing Kuf and Kuu contributions
+through an ill-conditioned Cholesky (jitter 1e-6) and, for the assignment
+layer, pass the Gumbel-softmax at temperature 0.01, so no fixed float32
+tolerance fits every configuration; the criterion asks the HIP path to be as
+accurate as a float32 evaluation of the reference's own graph.  Measured: the
+HIP path is 1-30x more accurate than float32 autograd on every block."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref as R
+from oracle import grad_ref as GR
+from tests.helpers import build_model, dev_noise, normwise, to_np
+
+pytestmark = pytest.mark.gpu
+
+FLOOR = 3e-4
+
+
+def _model(p, device, a_var):
+    base = build_model(p, device)
+    if a_var is None:
+        return base
+    from modulatedgps_amd.likelihoods import GaussianModified
+    from modulatedgps_amd.models import SMGPModified
+    K = p.lik_variance.shape[1]
+    return SMGPModified(base.likelihood.likelihood, GaussianModified(variance=a_var, device=device),
+                        base.pred_layer, base.assign_layer, K=K, num_samples=p.S, num_data=p.num_data)
+
+
+def _oracle(X, Y, p, z, u, a_var, dtype=torch.float64):
+    pred, assign, lik = GR.params_from_oracle(p)
+    leaf = lambda t: t.detach().to(dtype).requires_grad_(True)
+    pred = {k: leaf(v) for k, v in pred.items()}
+    assign = {k: leaf(v) for k, v in assign.items()}
+    lik = leaf(lik)
+    f64 = lambda a: torch.tensor(np.asarray(a, np.float32)).to(dtype)
+    av = None
+    if a_var is not None:
+        av = leaf(torch.tensor(np.asarray(a_var, np.float32).reshape(-1)))
+    e = GR.elbo(f64(X), f64(Y), pred, assign, lik, f64(z), f64(u), p.num_data, assign_lik_var=av)
+    e.backward()
+    g = {"lik_variance": lik.grad.double().numpy()}
+    if av is not None:
+        g["assign_lik_variance"] = av.grad.double().numpy()
+    for name, L in (("pred", pred), ("assign", assign)):
+        for k in GR.LAYER_KEYS:
+            gk = L[k].grad.double().numpy()
+            if k == "q_sqrt":
+                gk = np.tril(gk)
+            g[name + "." + k] = gk
+    return float(e.detach()), g
+
+
+def _dense(name, t, M):
+    a = to_np(t)
+    return a.reshape(-1) if name.endswith(("variance", "lengthscales")) else a
+
+
+@pytest.mark.parametrize("N,M,K,D,ls,S,modified", [(1000, 25, 3, 1, 0.5, 25, False),
+                                                    (2049, 64, 4, 2, 0.8, 7, False),
+                                                    (1000, 25, 3, 1, 0.5, 25, True),
+                                                    (4096, 130, 3, 3, 1.0, 5, False)])
+def test_elbo_and_grad(device, N, M, K, D, ls, S, modified):
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
+    a_var = np.linspace(0.3, 0.9, K)[None, :] if modified else None
+    z, u = R.explicit_noise(S, N, K, seed=5)
+    e_ref, g_ref = _oracle(X, Y, p, z, u, a_var)
+    _, g_f32 = _oracle(X, Y, p, z, u, a_var, dtype=torch.float32)
+    model = _model(p, device, a_var)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    e, grads = model.elbo_and_grad(Xd, Y, noise=dev_noise(z, u, device))
+    assert float(e.cpu()) == pytest.approx(e_ref, rel=1e-4)
+    names = [n for n, _, _ in model.trainable_parameters()]
+    assert sorted(names) == sorted(g_ref)
+    errs, errs32 = {}, {}
+    for n in names:
+        got = _dense(n, grads[n], M)
+        ref = g_ref[n].reshape(got.shape)
+        errs[n] = normwise(got, ref)
+        errs32[n] = normwise(g_f32[n].reshape(got.shape), ref)
+    print({k: f"{v:.1e}/{errs32[k]:.1e}" for k, v in errs.items()})
+    for n, err in errs.items():
+        assert err < max(FLOOR, 1.5 * errs32[n]), (n, err, errs32[n])
+
+
+def test_adam_step(device):
+    """mgp_adam_step, free and softplus-positive parameters, three steps, against
+    cpu_ref.adam_tf_legacy_step on the unconstrained variable (minimising -ELBO)."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(3)
+    rows, cols, ld = 37, 5, 8
+    lr = 0.01
+    for positive in (False, True):
+        theta0 = rng.uniform(0.2, 2.0, (rows, cols))
+        buf = torch.zeros(rows, ld, dtype=torch.float32, device=device)
+        theta = buf[:, :cols]
+        theta.copy_(torch.as_tensor(theta0, dtype=torch.float32))
+        th32 = theta0.astype(np.float32).astype(np.float64)
+        u_ref = np.log(np.expm1(th32)) if positive else th32.copy()
+        u = torch.as_tensor(u_ref, dtype=torch.float32, device=device).contiguous() if positive else None
+        u_ref = u_ref.astype(np.float32).astype(np.float64)
+        m1 = torch.zeros(rows, cols, dtype=torch.float32, device=device)
+        m2 = torch.zeros_like(m1)
+        m_ref = np.zeros((rows, cols))
+        v_ref = np.zeros((rows, cols))
+        for t in (1, 2, 3):
+            g = rng.standard_normal((rows, cols))
+            gd = torch.as_tensor(g, dtype=torch.float64 if t == 2 else torch.float32, device=device)
+            ops.adam_step(theta, gd, m1, m2, t, lr, u=u)
+            g32 = g.astype(np.float32).astype(np.float64)
+            gu = -g32 * (1.0 / (1.0 + np.exp(-u_ref)) if positive else 1.0)
+            u_ref, m_ref, v_ref = R.adam_tf_legacy_step(u_ref, gu, m_ref, v_ref, t, lr)
+        th_ref = np.log1p(np.exp(u_ref)) if positive else u_ref
+        assert np.abs(to_np(theta) - th_ref).max() < 1e-5 * max(1.0, np.abs(th_ref).max())
+        assert np.all(to_np(buf[:, cols:]) == 0)
+
+
+def test_run_adam_improves_elbo(device):
+    """utils.training_utils.run_adam drop-in: same signature / return value; the ELBO
+    rises over a short run on the c1-shaped problem (minibatches of 250)."""
+    from utils.training_utils import run_adam
+    X, Y, p = R.synthetic_problem(1000, 25, 3, 1, 0.5, state="init", S=5)
+    model = build_model(p, device)
+    rng = np.random.default_rng(0)
+
+    def batches():
+        while True:
+            idx = rng.choice(1000, 250, replace=False)
+            yield X[idx].astype(np.float32), Y[idx].astype(np.float32)
+
+    it = batches()
+    e0 = np.mean([-float(model.training_loss(next(it)).cpu()) for _ in range(10)])
+    iters, elbos = run_adam(model, 60, it, 0.01)
+    assert iters == list(range(5, 61, 5))
+    assert np.all(np.isfinite(elbos))
+    assert np.mean(elbos[-3:]) > e0
