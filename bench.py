@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-step (ELBO + gradient + Adam) leg")
     ap.add_argument("--cpu-sample", type=int, nargs=2, default=(8192, 65536),
                     help="two N sizes of the CPU oracle sample (linear fit in N; the full N "
                          "is timed directly when it is one of them)")
@@ -174,6 +175,42 @@ def load_traffic(kernel):
     return e.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
+def train_leg(model, X, Y, kw, args, barrier, world, device):
+    """Secondary line: the run_adam optimisation step (utils/training_utils.py:10-13:
+    ELBO, its gradient w.r.t. every trainable parameter, one TF-legacy Adam update),
+    same workload and timing protocol as the forward leg."""
+    from modulatedgps_amd.training import AdamTF
+    opt = AdamTF(model.trainable_parameters(), 1e-3)
+
+    from modulatedgps_amd.models import _Stage
+
+    def step(timing=None):
+        e, g = model.elbo_and_grad(X, Y, timing=timing, **kw)
+        with _Stage(timing, "adam"):
+            opt.step(g)
+        return e
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    timing = {}
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e = step(timing)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = stage_stats(timing)
+    return {"metric": "training steps/sec (forward + full gradient + Adam)", "value": world * args.steps / elapsed,
+            "unit": "train steps/s", "ms_per_step": elapsed / args.steps * 1e3, "elbo_last": float(e.item()),
+            "stages_us_per_step": {k: round(v[0] * v[1] / args.steps * 1e3, 1) for k, v in st.items()}}
+
+
 def main():
     args = parse()
     from modulatedgps_amd.config import conditional_mode
@@ -262,6 +299,7 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.steps / elapsed
+    train = None if args.no_train else train_leg(model, X, Y, kw, args, barrier, world, device)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, tuple(args.cpu_sample))
@@ -285,6 +323,7 @@ def main():
             "step_tflops": step_flops / (ms_per_step * 1e-3) / 1e12,
             "step_frac_f32_mfma": step_flops / (ms_per_step * 1e-3) / PEAK_F32_MFMA,
             "cpu_baseline": cpu,
+            "train": train,
             "elbo": elbo_val, "cholesky_info": info,
         }
         print(json.dumps(out))

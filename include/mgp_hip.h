@@ -174,6 +174,18 @@ int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ld
              float alpha, int32_t tri, float* out, int64_t ldo, void* workspace, size_t workspace_bytes,
              mgp_stream_t stream);
 
+/* The same contraction at f32 accuracy on the bf16 MFMA (operands split into
+ * three bf16 planes on the fly, six plane products), batched and weighted:
+ *   out[b][i][j] = alpha * sum_n X_b[i][n] w_b[n] Y_b[j][n]
+ * X_b = X + b sx ([MI][ldx]), Y_b = Y + b sy, w_b = W + b sw (W may be NULL:
+ * no weight), out_b = out + b so; mode 0 full, 1 lower triangle (zeros above),
+ * 2 symmetric (upper mirrors lower).  ldx, ldy, strides multiples of 4 floats,
+ * pointers 16-B aligned.  Workspace mgp_gram_x6_workspace_bytes. */
+size_t mgp_gram_x6_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t batch, int32_t mode);
+int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy, int64_t sy,
+                int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha, int32_t mode,
+                float* out, int64_t ldo, int64_t so, void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+
 /* Backward of one layer's whitened conditional (the GradientTape pass through
  * GPflow base_conditional, models.py:141-143, and SVGP's Knn = var,
  * models.py:133), given G_mu = d/d fmean and G_v = d/d fvar ([K][ldg]):
@@ -182,13 +194,15 @@ int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ld
  *   g_Kuf [M][ldk]         = L^-T gA,  gA = q_mu G_mu - 2 A sum_k G_v,k + 2 sum_k L_k (L_k^T A) diag(G_v,k)
  *   g_Lm [M][ldgl]         = -tril(g_Kuf A^T)          (gradient w.r.t. chol(Kuu))
  *   g_var (double)         = sum G_v                   (through Knn)
- * Inputs: A's split image and f32 A (both from mgp_trsm_stats_x6), the
- * tril(q_sqrt) image (mgp_split_lower_x6) and q_sqrt itself, q_mu, LinvT.
- * The N-scaled products run on the split-bf16 x6 path (f32 accuracy) and the
- * f32 MFMA (grams).  Workspace: mgp_conditional_backward_workspace_bytes. */
+ * Inputs: A's split image and f32 A (both from mgp_trsm_stats_x6), q_sqrt
+ * (its lower triangle is used), q_mu, LinvT.  The expert terms use
+ * S_k = L_k L_k^T (sum_k L_k (L_k^T A) diag(G_v,k) = sum_k (S_k A) diag(G_v,k))
+ * and P_k = A diag(G_v,k) A^T (g_q_sqrt[k] = 2 tril(P_k L_k)).  Every product
+ * that scales with N runs on the split-bf16 x6 path (f32 accuracy), g_q_mu on
+ * the f32 MFMA.  Workspace: mgp_conditional_backward_workspace_bytes. */
 size_t mgp_conditional_backward_workspace_bytes(int64_t M, int64_t N, int32_t K);
 int mgp_conditional_backward_x6(const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
-                                const void* Lfr, size_t lfr_bytes, const float* q_sqrt, int64_t ldqs,
+                                const float* q_sqrt, int64_t ldqs,
                                 int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
                                 int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M,
                                 int64_t N, int32_t K, float* g_q_mu, int64_t ldgq, float* g_q_sqrt,

@@ -75,8 +75,11 @@ SIGNATURES = {
     "mgp_gram_workspace_bytes": (c_size, [c_i64, c_i64, c_i64, c_i32]),
     "mgp_gram": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, ctypes.c_float, c_i32, c_ptr,
                                 c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_gram_x6_workspace_bytes": (c_size, [c_i64, c_i64, c_i64, c_i32, c_i32]),
+    "mgp_gram_x6": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64,
+                                   c_i32, ctypes.c_float, c_i32, c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_conditional_backward_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
-    "mgp_conditional_backward_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_i64, c_ptr, c_size, c_ptr, c_i64,
+    "mgp_conditional_backward_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
                                                    c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                                                    c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64,
                                                    c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),

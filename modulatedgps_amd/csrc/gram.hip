@@ -142,6 +142,239 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
   out[i * ldo + j] = v;
 }
 
+
+// ------------------------------------------------------------------ x6 gram
+// out[b][i][j] = alpha * sum_n X_b[i][n] (w_b[n]) Y_b[j][n] at f32 accuracy on
+// the bf16 MFMA: each 32-wide n chunk is loaded as f32 (optionally scaled by
+// the weight w_b[n]), split into hi/mid/lo bf16 planes on the fly and staged
+// in LDS as 32x32x16 operand fragments; six plane products per fragment pair
+// (mfma_x6).  The contraction is over n, so both operands use the same lane
+// -> k assignment (lane (r, h), element j <-> n0 + 16 s + 8 h + j) and no
+// permutation is needed.  128 x 128 output tile per workgroup (4 waves of
+// 64 x 64), split-K over blockIdx.z into a workspace, batch over blockIdx.y;
+// gram_x6_reduce_kernel sums the splits in a fixed order (deterministic).
+constexpr int kXC = 32;    // n per chunk = two bf16 k-steps
+constexpr int kXG = 3200;  // LDS bytes per (32-row block, k-step) group: 3 planes x 1 KiB + 128 B pad
+
+// Split 4 consecutive n-values of one row into the three planes and store them
+// as half of a lane's 16-B fragment slot (plane stride 1 KiB).
+__device__ __forceinline__ void stash4(char* dst, floatx4 v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 h, m, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    __bf16 a, b, c;
+    split3(v[j], a, b, c);
+    h[j] = a; m[j] = b; l[j] = c;
+  }
+  *reinterpret_cast<bf16x4*>(dst) = h;
+  *reinterpret_cast<bf16x4*>(dst + 1024) = m;
+  *reinterpret_cast<bf16x4*>(dst + 2048) = l;
+}
+
+// 768 threads in two roles, three waves per SIMD: one consumer (waves 0-3)
+// multiplies one LDS buffer (64 x 64 of the tile each) while two producers
+// (waves 4-11; two waves per SIMD double the VALU issue rate of one) load the
+// next f32 chunks (two chunks ahead, in registers), split them and store the
+// fragments into the other buffer.  One barrier per chunk.
+template <bool TRI, bool WEIGHT>
+__global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict__ X, int64_t ldx, int64_t sx,
+                                                         int64_t MI, const float* __restrict__ Y, int64_t ldy,
+                                                         int64_t sy, int64_t MJ, const float* __restrict__ W,
+                                                         int64_t sw, int64_t N, int64_t nper, int nbj, int tiles,
+                                                         int batch, int nsplit, float* __restrict__ ws,
+                                                         int64_t bstride, int64_t zstride) {
+  // per buffer: [32-row block][k-step] groups of [plane][lane] 16-B fragment slots
+  __shared__ __attribute__((aligned(16))) char sX[2][8 * kXG], sY[2][8 * kXG];
+  // item: when the splits come in multiples of 8, split z runs on XCD z % 8 and
+  // every (tile, batch) item of a split is adjacent there (one n-slab per L2)
+  int q, b, z;
+  {
+    const int id = blockIdx.x, items = tiles * batch;
+    if (nsplit % 8 == 0) {
+      const int x = id & 7, j = id >> 3;
+      z = x + 8 * (j / items);
+      const int rem = j % items;
+      q = rem % tiles;
+      b = rem / tiles;
+    } else {
+      q = id % tiles;
+      b = (id / tiles) % batch;
+      z = id / items;
+    }
+  }
+  int bi, bj;
+  if (TRI) {
+    bi = (int)((sqrtf(8.f * q + 1.f) - 1.f) * 0.5f);
+    while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+    while (bi * (bi + 1) / 2 > q) --bi;
+    bj = q - bi * (bi + 1) / 2;
+  } else {
+    bi = q / nbj;
+    bj = q % nbj;
+  }
+  X += b * sx;
+  Y += b * sy;
+  if (WEIGHT) W += b * sw;
+  const int64_t i0 = (int64_t)bi * kGT, j0 = (int64_t)bj * kGT;
+  const int64_t nb = (int64_t)z * nper;
+  const int64_t ne = (nb + nper < N) ? nb + nper : N;
+  const int64_t nch = nb < ne ? (ne - nb + kXC - 1) / kXC : 0;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool producer = w >= 4;
+
+  // ---- producer state: thread loads 4 consecutive n (column group cg) of rows
+  // 32 q + rr (q = q0, q0 + 1) of both tiles.  Lane l of producer wave pw (0..7):
+  // rr = 8 (pw % 4) + (l / 2) % 8, q0 = 2 (pw / 4), cg = 2 (l / 16) + l % 2, so a
+  // wave reads 8 rows x 128 B per load and each 16-lane group of a ds_write_b64
+  // (one (k-step, lane half) pair: cg / 4, (cg / 2) % 2) stores 8 rows x 16 B =
+  // 128 contiguous bytes.
+  const int pw = w - 4;
+  const int rr = 8 * (pw & 3) + ((lane >> 1) & 7), cg = 2 * (lane >> 4) + (lane & 1);
+  const int q0 = 2 * ((pw >> 2) & 1);
+  const int soff = (cg >> 2) * kXG + (rr + 32 * ((cg >> 1) & 1)) * 16 + (cg & 1) * 8;
+  // buffer loads: rows beyond the matrix fall outside the resource and read 0;
+  // the one partial chunk at the end of n is masked when it is stashed
+  const int64_t rows_x = MI - i0 < kGT ? MI - i0 : kGT, rows_y = MJ - j0 < kGT ? MJ - j0 : kGT;
+  const __amdgpu_buffer_rsrc_t rX =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(X + i0 * ldx), (short)0, (int)(uint32_t)(rows_x * ldx * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rY =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Y + j0 * ldy), (short)0, (int)(uint32_t)(rows_y * ldy * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)(uint32_t)(WEIGHT ? N * 4 : 0), 0x00020000);
+  const uint32_t vx = (uint32_t)((32 * q0 + rr) * ldx + 4 * cg) * 4u;
+  const uint32_t vy = (uint32_t)((32 * q0 + rr) * ldy + 4 * cg) * 4u;
+  const uint32_t qx = (uint32_t)(32 * ldx * 4), qy = (uint32_t)(32 * ldy * 4);
+  struct Regs { floatx4 x[2], y[2], w; };
+  Regs ra, rb;
+  auto load = [&](Regs& r, int64_t c) {
+    const uint32_t so = (uint32_t)((nb + c * kXC) * 4);
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      r.x[qq] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rX, vx + qq * qx, so, 0));
+      r.y[qq] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rY, vy + qq * qy, so, 0));
+    }
+    if (WEIGHT) r.w = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rW, 16u * cg, so, 0));
+  };
+  auto stash = [&](Regs& r, int64_t c, int buf) {
+    const int64_t n0 = nb + c * kXC;
+    if (n0 + kXC > ne) {  // the last, partial chunk: zero the columns >= ne
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n0 + 4 * cg + e >= ne) {
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) {
+            r.x[qq][e] = 0.f;
+            r.y[qq][e] = 0.f;
+          }
+        }
+    }
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      stash4(sX[buf] + 2 * (q0 + qq) * kXG + soff, r.x[qq]);
+      stash4(sY[buf] + 2 * (q0 + qq) * kXG + soff, WEIGHT ? r.y[qq] * r.w : r.y[qq]);
+    }
+  };
+
+  // ---- consumer state: wave w multiplies X blocks wb, wb + 1 by Y blocks vb, vb + 1
+  const int wb = (w >> 1) * 2, vb = (w & 1) * 2;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][c][e] = 0.f;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 c[2][3];
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          c[t2][p] = *reinterpret_cast<const bf16x8*>(sY[buf] + (2 * (vb + t2) + ks) * kXG + p * 1024 + lane * 16);
+#pragma unroll
+      for (int ta = 0; ta < 2; ++ta) {
+        bf16x8 a[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          a[p] = *reinterpret_cast<const bf16x8*>(sX[buf] + (2 * (wb + ta) + ks) * kXG + p * 1024 + lane * 16);
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb) acc[ta][tb] = mfma_x6(a, c[tb], acc[ta][tb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the next k-step's fragment reads after these MFMAs
+    }
+  };
+
+  // chunk c lives in register set (c even: ra, odd: rb) and LDS buffer c % 2.
+  // The two roles run separate loops with the same barriers (one per chunk),
+  // so neither role's registers are live in the other's loop.
+  if (producer) {
+    if (nch > 0) {
+      load(ra, 0);
+      if (nch > 1) load(rb, 1);
+      stash(ra, 0, 0);
+      if (nch > 2) load(ra, 2);
+    }
+    __syncthreads();
+    for (int64_t i = 0; i < nch; i += 2) {
+      if (i + 1 < nch) {
+        stash(rb, i + 1, 1);
+        if (i + 3 < nch) load(rb, i + 3);
+      }
+      __syncthreads();
+      if (i + 1 >= nch) break;
+      if (i + 2 < nch) {
+        stash(ra, i + 2, 0);
+        if (i + 4 < nch) load(ra, i + 4);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  __syncthreads();
+  for (int64_t i = 0; i < nch; i += 2) {
+    compute(0);
+    __syncthreads();
+    if (i + 1 >= nch) break;
+    compute(1);
+    __syncthreads();
+  }
+  float* out = ws + (int64_t)z * zstride + (int64_t)b * bstride;
+#pragma unroll
+  for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+      const int64_t j = j0 + 32 * (vb + tb) + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t i = i0 + 32 * (wb + ta) + acc_row(e, lane);
+        if (i < MI && j < MJ) out[i * MJ + j] = acc[ta][tb][e];
+      }
+    }
+}
+
+// out[b][i][j] = alpha * sum_z ws[z][b][i][j]; mode 0 full, 1 lower triangle
+// (zero above), 2 symmetric (the upper triangle mirrors the lower).
+__global__ __launch_bounds__(256) void gram_x6_reduce_kernel(const float* __restrict__ ws, int64_t bstride,
+                                                             int64_t zstride, int nsplit, int64_t MI, int64_t MJ,
+                                                             int64_t total, float alpha, int mode,
+                                                             float* __restrict__ out, int64_t ldo, int64_t so) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int64_t b = idx / (MI * MJ), rem = idx % (MI * MJ);
+  const int64_t i = rem / MJ, j = rem % MJ;
+  float v = 0.f;
+  if (!(mode == 1 && j > i)) {
+    const int64_t src = b * bstride + ((mode == 2 && j > i) ? j * MJ + i : i * MJ + j);
+    for (int z = 0; z < nsplit; ++z) v += ws[(int64_t)z * zstride + src];
+    v *= alpha;
+  }
+  out[b * so + i * ldo + j] = v;
+}
+
 }  // namespace mgp
 
 using namespace mgp;
@@ -193,5 +426,80 @@ extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y,
   if (st) return st;
   hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((MI * MJ + 255) / 256)), dim3(256), 0, s, ws, MJ, stride,
                      nsplit, MI, MJ, alpha, tri, out, ldo);
+  return launch_status();
+}
+
+static int gram_x6_splits(int64_t N, int64_t wgs) {
+  // aim for >= 2048 workgroups, each with >= 2048 points
+  int s = 1;
+  while (wgs * s < 2048 && N / (2 * s) >= 2048) s *= 2;
+  return s;
+}
+
+static int gram_x6_tiles(int64_t MI, int64_t MJ, int tri) {
+  const int nbi = (int)((MI + kGT - 1) / kGT), nbj = (int)((MJ + kGT - 1) / kGT);
+  return tri ? nbi * (nbi + 1) / 2 : nbi * nbj;
+}
+
+extern "C" size_t mgp_gram_x6_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t batch, int32_t mode) {
+  if (MI <= 0 || MJ <= 0 || N <= 0 || batch <= 0) return 16;
+  const int tiles = gram_x6_tiles(MI, MJ, mode != 0);
+  return (size_t)gram_x6_splits(N, (int64_t)tiles * batch) * (size_t)batch * (size_t)MI * (size_t)MJ * sizeof(float);
+}
+
+extern "C" int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
+                           int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                           int32_t mode, float* out, int64_t ldo, int64_t so, void* workspace,
+                           size_t workspace_bytes, mgp_stream_t stream) {
+  if (!X) return -1;
+  if (ldx < N || ldx % 4) return -2;
+  if (batch > 1 && sx % 4) return -3;
+  if (MI < 0) return -4;
+  if (!Y) return -5;
+  if (ldy < N || ldy % 4) return -6;
+  if (batch > 1 && sy % 4) return -7;
+  if (MJ < 0) return -8;
+  if (W && batch > 1 && sw % 4) return -10;
+  if (W && N * 4 >= ((int64_t)1 << 31)) return MGP_ERR_UNSUPPORTED;
+  if (N < 0) return -11;
+  if (batch < 0) return -12;
+  if (mode < 0 || mode > 2) return -14;
+  if (mode && MI != MJ) return -14;
+  if ((int64_t)kGT * (ldx > ldy ? ldx : ldy) * 4 >= ((int64_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  if (!out) return -15;
+  if (ldo < MJ) return -16;
+  if (batch > 1 && so < ldo * MI) return -17;
+  if (MI == 0 || MJ == 0 || batch == 0) return MGP_OK;
+  if (!aligned16(X) || !aligned16(Y) || (W && !aligned16(W))) return MGP_ERR_ALIGN;
+  if (!workspace || workspace_bytes < mgp_gram_x6_workspace_bytes(MI, MJ, N, batch, mode)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles = gram_x6_tiles(MI, MJ, mode != 0);
+  const int nbj = (int)((MJ + kGT - 1) / kGT);
+  const int nsplit = N > 0 ? gram_x6_splits(N, (int64_t)tiles * batch) : 1;
+  int64_t nper = (N + nsplit - 1) / nsplit;
+  nper = (nper + kXC - 1) / kXC * kXC;
+  float* ws = (float*)workspace;
+  const int64_t bstride = MI * MJ, zstride = (int64_t)batch * MI * MJ;
+  const dim3 grid((unsigned)(tiles * batch * nsplit));
+  if (mode) {
+    if (W)
+      hipLaunchKernelGGL((gram_x6_kernel<true, true>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, N,
+                         nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
+    else
+      hipLaunchKernelGGL((gram_x6_kernel<true, false>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw,
+                         N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
+  } else {
+    if (W)
+      hipLaunchKernelGGL((gram_x6_kernel<false, true>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw,
+                         N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
+    else
+      hipLaunchKernelGGL((gram_x6_kernel<false, false>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw,
+                         N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
+  }
+  int st = launch_status();
+  if (st) return st;
+  const int64_t total = (int64_t)batch * MI * MJ;
+  hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, bstride,
+                     zstride, nsplit, MI, MJ, total, alpha, (int)mode, out, ldo, so);
   return launch_status();
 }

@@ -67,6 +67,21 @@ __device__ __forceinline__ void store_split(bf16x8* __restrict__ dst, const floa
   dst[128] = l;
 }
 
+__device__ __forceinline__ floatx16 mfma_bf16(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc += (a_hi + a_mid + a_lo)(b_hi + b_mid + b_lo) without the three
+// products of weight < 2^-16; smallest terms first.
+__device__ __forceinline__ floatx16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 acc) {
+  acc = mfma_bf16(a[2], b[0], acc);
+  acc = mfma_bf16(a[1], b[1], acc);
+  acc = mfma_bf16(a[0], b[2], acc);
+  acc = mfma_bf16(a[1], b[0], acc);
+  acc = mfma_bf16(a[0], b[1], acc);
+  return mfma_bf16(a[0], b[0], acc);
+}
+
 // ------------------------------------------------------------------ reductions
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

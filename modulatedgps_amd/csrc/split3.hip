@@ -53,7 +53,7 @@ constexpr int kFragBytes = 1024;
 // (upper: LinvT, K4's T[k][i] = L^-T[k][i]).  One wave per fragment block
 // (b, mb, mk): grid.x = batch * nmb * nmk / 4.
 // TRANS: the source is stored transposed (element (m, m') read at S[m' ld + m]).
-template <bool LOWER, bool TRANS = false>
+template <bool LOWER, bool TRANS = false, bool FULL = false>
 __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict__ src, int64_t ld,
                                                         int64_t stride, int64_t M, int nmb, int nmk,
                                                         int64_t nfrag, bf16x8* __restrict__ img) {
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int64_t m = 16 * (int64_t)mk + kperm(h, j);
-    const bool keep = LOWER ? (m >= mc) : (m <= mc);
+    const bool keep = FULL || (LOWER ? (m >= mc) : (m <= mc));
     v[j] = (m < M && mc < M && keep) ? S[TRANS ? mc * ld + m : m * ld + mc] : 0.f;
   }
   store_split(img + f * 3 * 64 + lane, v);
@@ -94,23 +94,8 @@ __global__ __launch_bounds__(256) void split_cols_kernel(const float* __restrict
   store_split(Afr + f * 3 * 64 + lane, v);
 }
 
-__device__ __forceinline__ floatx16 mfma_bf16(bf16x8 a, bf16x8 b, floatx16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
 __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-
-// acc += (a_hi + a_mid + a_lo)(b_hi + b_mid + b_lo) without the three
-// products of weight < 2^-16; smallest terms first.
-__device__ __forceinline__ floatx16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 acc) {
-  acc = mfma_bf16(a[2], b[0], acc);
-  acc = mfma_bf16(a[1], b[1], acc);
-  acc = mfma_bf16(a[0], b[2], acc);
-  acc = mfma_bf16(a[1], b[0], acc);
-  acc = mfma_bf16(a[0], b[1], acc);
-  return mfma_bf16(a[0], b[0], acc);
 }
 
 // Item b -> (row tile t heavy-first, column tile tn, expert k); the K experts of
@@ -131,6 +116,21 @@ __device__ __forceinline__ void x6_item(int b, int nTn, int K, int& t, int& tn, 
   }
 }
 
+// Item b -> (row tile t, column tile tn) for the one-matrix products (K4,
+// gA, gKuf): the nT row tiles of a column tile are adjacent block ids on one
+// XCD (b % 8), heaviest first, so the column slab of the B image they all read
+// is served from that XCD's L2.
+__device__ __forceinline__ void col_major_item(int b, int nT, int nTn, int& t, int& tn) {
+  if (nTn % 8 == 0) {
+    const int x = b & 7, j = b >> 3;
+    t = nT - 1 - j % nT;
+    tn = (j / nT) * 8 + x;
+  } else {
+    t = nT - 1 - b % nT;
+    tn = b / nT;
+  }
+}
+
 // Main loop shared by K4 and K5: acc[i][c] (row sub-tile i = 0..3 of the
 // 128-row tile, column sub-tile c = 0..1 of this wave's 64 columns) +=
 // sum over k-steps mk in [mk_begin, mk_end) (even count) of T-image blocks
@@ -146,8 +146,10 @@ using ic = std::integral_constant<int, V>;
 // are non-zero.  Otherwise (K4, T upper: zero for 16 mk > 32 mb + 31) the last
 // 8 k-steps do, with sub-tiles i >= p of pair p.  Those MFMAs are skipped
 // (8% of the work), everything else is unchanged.
-template <bool DIAG_FIRST>
-__device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[4 * 3 * 64],
+// DIAG: 1 = diagonal first (lower T), 2 = diagonal last (upper T), 0 = full T.
+// NC: column sub-tiles (32 wide) per wave (B blocks nb0 .. nb0 + NC - 1).
+template <int DIAG, int NC = 2>
+__device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)[4 * 3 * 64],
                                             __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
                                             __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
                                             int mk_end, int nmk, bool init = true) {
@@ -167,17 +169,17 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][c][e] = 0.f;
   }
 
-  auto load_b = [&](bf16x8 (&b)[2][3], int mk) {
+  auto load_b = [&](bf16x8 (&b)[NC][3], int mk) {
     const uint32_t o = (uint32_t)mk * 3u * kFragBytes;
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       b[0][p] = ld_frag(rB, vB, sB0 + o + p * kFragBytes);
-      b[1][p] = ld_frag(rB, vB, sB1 + o + p * kFragBytes);
+      if constexpr (NC > 1) b[1][p] = ld_frag(rB, vB, sB1 + o + p * kFragBytes);
     }
   };
   auto load_t = [&](u32x4v (&st)[3], int mk) {
@@ -189,7 +191,7 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[
 #pragma unroll
     for (int s = 0; s < 3; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
   };
-  auto compute = [&](int buf, const bf16x8 (&b)[2][3], auto ilo, auto ihi) {
+  auto compute = [&](int buf, const bf16x8 (&b)[NC][3], auto ilo, auto ihi) {
     constexpr int ILO = decltype(ilo)::value, IHI = decltype(ihi)::value;
 #pragma unroll
     for (int i = ILO; i < IHI; ++i) {
@@ -197,11 +199,11 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[
 #pragma unroll
       for (int p = 0; p < 3; ++p) a[p] = sL[buf][(i * 3 + p) * 64 + lane];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) acc[i][c] = mfma_x6(a, b[c], acc[i][c]);
+      for (int c = 0; c < NC; ++c) acc[i][c] = mfma_x6(a, b[c], acc[i][c]);
     }
   };
 
-  bf16x8 b0[2][3], b1[2][3];
+  bf16x8 b0[NC][3], b1[NC][3];
   u32x4v st[3];
   load_t(st, mk_begin);
   load_b(b0, mk_begin);
@@ -227,13 +229,16 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][2], bf16x8 (*sL)[
     store_t(0, st);
     __syncthreads();
   };
-  if constexpr (DIAG_FIRST) {
+  if constexpr (DIAG == 1) {
     pair(mk_begin, ic<0>{}, ic<1>{});
     pair(mk_begin + 2, ic<0>{}, ic<2>{});
     pair(mk_begin + 4, ic<0>{}, ic<3>{});
     pair(mk_begin + 6, ic<0>{}, ic<4>{});
 #pragma nounroll
     for (int mk = mk_begin + 8; mk < mk_end; mk += 2) pair(mk, ic<0>{}, ic<4>{});
+  } else if constexpr (DIAG == 0) {
+#pragma nounroll
+    for (int mk = mk_begin; mk < mk_end; mk += 2) pair(mk, ic<0>{}, ic<4>{});
   } else {
 #pragma nounroll
     for (int mk = mk_begin; mk < mk_end - 8; mk += 2) pair(mk, ic<0>{}, ic<4>{});
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   floatx16 acc[4][2];
-  x6_mainloop<true>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+  x6_mainloop<1>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
               img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
@@ -336,28 +341,6 @@ __device__ __forceinline__ void store_acc_image(const floatx16 (&acc)[4][2], bf1
   }
 }
 
-// B-a: CG_k = (L_k^T A) diag(Gv_k) for every expert, as f32 [K][M][ldc] (for
-// the q_sqrt gradient) and as split images [K][image] (for the A gradient).
-// Items and main loop as K5.
-__global__ __launch_bounds__(256, 2) void expert_bwd_c_kernel(const bf16x8* __restrict__ Afr,
-                                                             const bf16x8* __restrict__ Lfr, uint32_t afr_bytes,
-                                                             uint32_t lfr_bytes, int nmk, int nmb, int nTn, int K,
-                                                             int64_t M, int64_t N, const float* __restrict__ Gv,
-                                                             int64_t ldg, float* __restrict__ CG, int64_t ldc,
-                                                             int64_t strideC, bf16x8* __restrict__ CGfr,
-                                                             int64_t img_elems) {
-  __shared__ bf16x8 sL[2][4 * 3 * 64];
-  int t, tn, k;
-  x6_item(blockIdx.x, nTn, K, t, tn, k);
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  floatx16 acc[4][2];
-  x6_mainloop<true>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
-                    img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
-  const float* g = Gv + (int64_t)k * ldg;
-  store_acc_f32(acc, CG + (int64_t)k * strideC, ldc, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, g);
-  store_acc_image(acc, CGfr + (int64_t)k * img_elems, nmk, t, tn, N, g);
-}
-
 // gA0[m][n] = sum_k q_mu[m][k] G_mu[k][n] - 2 A[m][n] sum_k Gv[k][n]: the part
 // of the A gradient that needs no GEMM (one thread per column n, looping rows).
 template <int KMAX>
@@ -395,53 +378,65 @@ __global__ __launch_bounds__(256) void grad_a_base_kernel(const float* __restric
   }
 }
 
-// B-b: gA = 2 sum_k L_k CG_k + gA0, written as the split image of gA (the B
-// operand of B-d).  T images: L_k^T (upper in (k, i)); the contraction runs
-// over (expert, m') into one accumulator; item (t, tn) as K4, heavy first.
-__global__ __launch_bounds__(256, 2) void expert_bwd_a_kernel(
-    const bf16x8* __restrict__ LTfr, uint32_t ltfr_bytes, const bf16x8* __restrict__ CGfr, uint32_t cgfr_bytes,
-    int64_t img_elems, int nmk, int nTn, int K, int64_t M, int64_t N, const float* __restrict__ gA0,
-    int64_t ld0, bf16x8* __restrict__ gAfr) {
+// B-b: gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0 with S_k = L_k L_k^T
+// (full split images): item = (row tile t of 128 rows, column tile tn of
+// 128), wave w owns the 32 columns of B block 4 tn + w.  Each expert's
+// product runs through the K5 main loop (full T, one column sub-tile per
+// wave) and is folded into the output registers with its column weights, so
+// no per-expert intermediate is written.
+__global__ __launch_bounds__(256, 2) void grad_a_s_kernel(const bf16x8* __restrict__ Sfr, uint32_t s_bytes,
+                                                          const bf16x8* __restrict__ Afr, uint32_t afr_bytes,
+                                                          int nmk, int nTn, int K, int64_t M, int64_t N,
+                                                          const float* __restrict__ Gv, int64_t ldg,
+                                                          const float* __restrict__ gA0, int64_t ld0,
+                                                          bf16x8* __restrict__ gAfr) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   const int nT = nmk / 8, nmb = nmk / 2;
   int t, tn;
-  {
-    const int b = blockIdx.x;
-    if (nTn % 8 == 0) {
-      const int x = b & 7, j = b >> 3, per = nTn / 8;
-      t = nT - 1 - j / per;
-      tn = (j % per) * 8 + x;
-    } else {
-      t = nT - 1 - b / nTn;
-      tn = b % nTn;
-    }
-  }
+  col_major_item(blockIdx.x, nT, nTn, t, tn);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  floatx16 acc[4][2];
-  const int64_t t_elems = (int64_t)nmb * nmk * 3 * 64;  // one expert's T image (bf16x8 units)
-  for (int k = 0; k < K; ++k)
-    x6_mainloop<false>(acc, sL, img_rsrc(LTfr + k * t_elems, ltfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
-                       img_rsrc(CGfr + k * img_elems, cgfr_bytes),
-                       (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8, nmk, k == 0);
-  const int64_t i0 = 128 * (int64_t)t, n0 = (int64_t)tn * kX6BN;
-  const __amdgpu_buffer_rsrc_t r0 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)gA0, (short)0, (int)(uint32_t)(M * ld0 * 4), 0x00020000);
-  const uint32_t soff = (uint32_t)((i0 * ld0 + n0) * 4), ld32 = (uint32_t)ld0;
+  const int64_t nb = 4 * (int64_t)tn + w;
+  const int64_t n = 32 * nb + (lane & 31);
+  floatx16 acc[4][1], out[4][1];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int nl = 64 * w + 32 * c + (lane & 31);
-    const bool ok = n0 + nl < N;
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) out[i][0][e] = 0.f;
+  const int64_t s_elems = (int64_t)nmb * nmk * 3 * 64;  // one expert's S image (bf16x8 units)
+  for (int k = 0; k < K; ++k) {
+    x6_mainloop<0, 1>(acc, sL, img_rsrc(Sfr + k * s_elems, s_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
+                      img_rsrc(Afr, afr_bytes), (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, nmk, nmk);
+    const float g = n < N ? Gv[(int64_t)k * ldg + n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
-        const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
-        acc[i][c][e] = ok ? fmaf(2.f, acc[i][c][e], b0) : 0.f;   // rows >= M read 0 (outside the resource)
-      }
+      for (int e = 0; e < 16; ++e) out[i][0][e] = fmaf(g, acc[i][0][e], out[i][0][e]);
   }
-  store_acc_image(acc, gAfr, nmk, t, tn, N, nullptr);
+  const int64_t i0 = 128 * (int64_t)t;
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)gA0, (short)0, (int)(uint32_t)(M * ld0 * 4), 0x00020000);
+  const uint32_t soff = (uint32_t)((i0 * ld0 + 128 * (int64_t)tn) * 4), ld32 = (uint32_t)ld0;
+  const int nl = 32 * w + (lane & 31);
+  const bool ok = n < N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
+      const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
+      v[e] = ok ? fmaf(2.f, out[i][0][e], b0) : 0.f;   // rows >= M read 0 (outside the resource)
+    }
+    const int64_t mk = 8 * (int64_t)t + 2 * i;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = v[8 * s2 + j];
+      store_split(gAfr + ((nb * nmk + mk + s2) * 3) * 64 + lane, u);
+    }
+  }
 }
 
 // B-d: gKuf = L^-T gA = Linv^T gA as f32 [M][ld]; T image = Linv (lower in
@@ -452,11 +447,12 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restri
                                                          int64_t M, int64_t N, float* __restrict__ gKuf,
                                                          int64_t ldk) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
-  int t, tn, k;
-  x6_item(blockIdx.x, nTn, 1, t, tn, k);
+  int t, tn;
+  col_major_item(blockIdx.x, nmk / 8, nTn, t, tn);
+  t = nmk / 8 - 1 - t;  // lower T from the diagonal on: row tile 0 is the heaviest
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   floatx16 acc[4][2];
-  x6_mainloop<true>(acc, sL, img_rsrc(LIfr, lifr_bytes), (uint32_t)((4 * t) * nmk) * 3u * kFragBytes,
+  x6_mainloop<1>(acc, sL, img_rsrc(LIfr, lifr_bytes), (uint32_t)((4 * t) * nmk) * 3u * kFragBytes,
                     img_rsrc(gAfr, gafr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
   store_acc_f32(acc, gKuf, ldk, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
 }
@@ -476,22 +472,12 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   const int nT = nmk / 8;
   int t, tn;
-  {
-    const int b = blockIdx.x;
-    if (nTn % 8 == 0) {  // the row tiles of one column tile share an XCD (its Kuf slab in L2)
-      const int x = b & 7, j = b >> 3, per = nTn / 8;
-      t = nT - 1 - j / per;
-      tn = (j % per) * 8 + x;
-    } else {
-      t = nT - 1 - b / nTn;
-      tn = b % nTn;
-    }
-  }
+  col_major_item(blockIdx.x, nT, nTn, t, tn);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nmb = nmk / 2;
   floatx16 acc[4][2];
-  x6_mainloop<false>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
+  x6_mainloop<2>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
               img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8,
               nmk);
   (void)nmb;
@@ -710,41 +696,89 @@ extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* 
 
 // ------------------------------------------------------------------ conditional backward (x6)
 extern "C" size_t mgp_gram_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t tri);
+extern "C" size_t mgp_gram_x6_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t batch, int32_t mode);
+
+extern "C" int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
+                           int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                           int32_t mode, float* out, int64_t ldo, int64_t so, void* workspace,
+                           size_t workspace_bytes, mgp_stream_t stream);
 extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ldy, int64_t MJ,
                         int64_t N, float alpha, int32_t tri, float* out, int64_t ldo, void* workspace,
                         size_t workspace_bytes, mgp_stream_t stream);
 
 namespace {
 struct CondBwdWs {  // workspace carve-up (256-B aligned pieces)
-  size_t cg, cgfr, ltfr, ga0, gafr, lifr, gram, total;
+  size_t sfr, ga0, gafr, lifr, P, LT, part, gram, total;
 };
 size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
   CondBwdWs w;
   const int64_t ldn = (N + 3) / 4 * 4;
   size_t o = 0;
-  w.cg = o;   o += al256((size_t)K * M * ldn * 4);
-  w.cgfr = o; o += al256((size_t)K * mgp_x6_cols_bytes(M, N));
-  w.ltfr = o; o += al256(mgp_x6_lower_bytes(M, K));
+  const int64_t ldm = (M + 3) / 4 * 4;
+  w.sfr = o;  o += al256(mgp_x6_lower_bytes(M, K));
   w.ga0 = o;  o += al256((size_t)M * ldn * 4);
   w.gafr = o; o += al256(mgp_x6_cols_bytes(M, N));
   w.lifr = o; o += al256(mgp_x6_lower_bytes(M, 1));
+  w.P = o;    o += al256((size_t)K * M * ldm * 4);
+  w.LT = o;   o += al256((size_t)K * M * ldm * 4);
+  w.part = o; o += al256((size_t)K * 8);
   w.gram = o;
-  size_t g = mgp_gram_workspace_bytes(M, M, N, 1);
-  const size_t g2 = mgp_gram_workspace_bytes(M, K, N, 0);
-  o += al256(g > g2 ? g : g2);
+  size_t g = mgp_gram_x6_workspace_bytes(M, M, N, K, 2);
+  g = g > mgp_gram_x6_workspace_bytes(M, M, M, K, 2) ? g : mgp_gram_x6_workspace_bytes(M, M, M, K, 2);
+  const size_t sizes[3] = {mgp_gram_x6_workspace_bytes(M, M, M, K, 1), mgp_gram_x6_workspace_bytes(M, M, N, 1, 1),
+                           mgp_gram_workspace_bytes(M, K, N, 0)};
+  for (size_t v : sizes) g = v > g ? v : g;
+  o += al256(g);
   w.total = o;
   return w;
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void sum_all_kernel(const float* __restrict__ x, int64_t rows, int64_t cols,
-                                                      int64_t ld, double* __restrict__ out) {
+// part[k] = sum_n x[k][n] (one block per row), then out = sum_k part[k] (fixed order).
+__global__ __launch_bounds__(1024) void row_sums_kernel(const float* __restrict__ x, int64_t cols, int64_t ld,
+                                                        double* __restrict__ part) {
   __shared__ double scratch[16];
+  const float* row = x + (int64_t)blockIdx.x * ld;
   double v = 0.0;
-  for (int64_t i = threadIdx.x; i < rows * cols; i += 256) v += (double)x[(i / cols) * ld + i % cols];
+  for (int64_t n = threadIdx.x; n < cols; n += 1024) v += (double)row[n];
   v = mgp::block_sum<double>(v, scratch);
-  if (threadIdx.x == 0) *out = v;
+  if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+
+__global__ void sum_parts_kernel(const double* __restrict__ part, int rows, double* __restrict__ out) {
+  double v = 0.0;
+  for (int k = 0; k < rows; ++k) v += part[k];
+  *out = v;
+}
+
+// T[k][i][j] = L_k[i][j] for j <= i, else 0 (the lower triangle of q_sqrt).
+__global__ __launch_bounds__(256) void tril_copy_kernel(const float* __restrict__ q, int64_t ldq, int64_t sq,
+                                                        int64_t M, float* __restrict__ T, int64_t ldt, int64_t st) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= M * M) return;
+  const int k = blockIdx.y;
+  const int64_t i = idx / M, j = idx % M;
+  T[k * st + i * ldt + j] = j <= i ? q[k * sq + i * ldq + j] : 0.f;
+}
+
+// LT[k][j][l] = L_k[l][j] for l >= j, else 0 (the transposed lower triangle of q_sqrt).
+__global__ __launch_bounds__(256) void tril_transpose_kernel(const float* __restrict__ q, int64_t ldq, int64_t sq,
+                                                             int64_t M, float* __restrict__ LT, int64_t ldt,
+                                                             int64_t st) {
+  __shared__ float tile[32][33];
+  const int k = blockIdx.z;
+  const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;  // source rows l, columns j
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int64_t l = r0 + y, j = c0 + tx;
+    tile[y][tx] = (l < M && j < M && l >= j) ? q[k * sq + l * ldq + j] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int64_t j = c0 + y, l = r0 + tx;
+    if (j < M && l < M) LT[k * st + j * ldt + l] = tile[tx][y];
+  }
 }
 
 extern "C" size_t mgp_conditional_backward_workspace_bytes(int64_t M, int64_t N, int32_t K) {
@@ -753,7 +787,7 @@ extern "C" size_t mgp_conditional_backward_workspace_bytes(int64_t M, int64_t N,
 }
 
 extern "C" int mgp_conditional_backward_x6(
-    const void* Afr, size_t afr_bytes, const float* A, int64_t lda, const void* Lfr, size_t lfr_bytes,
+    const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
     const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
     int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
     float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
@@ -762,8 +796,6 @@ extern "C" int mgp_conditional_backward_x6(
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!A) return -3;
   if (lda < N) return -4;
-  if (!Lfr) return -5;
-  if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return -6;
   if (!q_sqrt) return -7;
   if (ldqs < M) return -8;
   if (!q_mu) return -10;
@@ -783,16 +815,18 @@ extern "C" int mgp_conditional_backward_x6(
   if (!g_Lm) return -27;
   if (!g_var) return -29;
   if (!workspace || workspace_bytes < mgp_conditional_backward_workspace_bytes(M, N, K)) return MGP_ERR_WORKSPACE;
-  if (!aligned16(workspace) || !aligned16(Afr) || !aligned16(Lfr)) return MGP_ERR_ALIGN;
+  if (!aligned16(workspace) || !aligned16(Afr)) return MGP_ERR_ALIGN;
   const size_t img = mgp_x6_cols_bytes(M, N);
   if (img >= ((size_t)1 << 32) || (size_t)M * ((N + 3) / 4 * 4) * 4 >= ((size_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const CondBwdWs L = cond_bwd_layout(M, N, K);
   char* ws = (char*)workspace;
   const int64_t ldn = (N + 3) / 4 * 4;
-  float* CG = (float*)(ws + L.cg);
-  bf16x8* CGfr = (bf16x8*)(ws + L.cgfr);
-  bf16x8* LTfr = (bf16x8*)(ws + L.ltfr);
+  float* P = (float*)(ws + L.P);
+  float* LT = (float*)(ws + L.LT);
+  double* part = (double*)(ws + L.part);
+  const int64_t ldm = (M + 3) / 4 * 4;
+  bf16x8* Sfr = (bf16x8*)(ws + L.sfr);
   float* gA0 = (float*)(ws + L.ga0);
   bf16x8* gAfr = (bf16x8*)(ws + L.gafr);
   bf16x8* LIfr = (bf16x8*)(ws + L.lifr);
@@ -801,24 +835,25 @@ extern "C" int mgp_conditional_backward_x6(
   const int64_t Mp = x6_mp(M);
   const int nmk = (int)(Mp / 16), nmb = (int)(Mp / 32), nT = (int)(Mp / kX6BM);
   const int nTn = (int)(x6_np(N) / kX6BN);
-  const int64_t img_elems = (int64_t)(img / 16);
   int st;
-  // 1. images of L_k^T (T operand of B-b) and of Linv (T operand of B-d)
+  // 1. S_k = L_k L_k^T (x6 gram over M of tril(q_sqrt), into the LT buffer) and its
+  //    full split images; the image of Linv (T operand of B-d)
+  hipLaunchKernelGGL(tril_copy_kernel, dim3((unsigned)((M * M + 255) / 256), (unsigned)K), dim3(256), 0, s, q_sqrt,
+                     ldqs, strideq, M, P, ldm, M * ldm);
+  if ((st = launch_status())) return st;
+  st = mgp_gram_x6(P, ldm, M * ldm, M, P, ldm, M * ldm, M, nullptr, 0, M, K, 1.f, 2, LT, ldm, M * ldm, gws, gwsb,
+                   stream);
+  if (st) return st;
   {
     const int64_t nfrag = (int64_t)K * nmb * nmk;
-    hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
-                       ldqs, strideq, M, nmb, nmk, nfrag, LTfr);
+    hipLaunchKernelGGL((split_tri_kernel<true, false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, LT,
+                       ldm, M * ldm, M, nmb, nmk, nfrag, Sfr);
     const int64_t nf1 = (int64_t)nmb * nmk;
     hipLaunchKernelGGL((split_tri_kernel<true, true>), dim3((unsigned)((nf1 + 3) / 4)), dim3(256), 0, s, LinvT, ldl,
                        (int64_t)0, M, nmb, nmk, nf1, LIfr);
     if ((st = launch_status())) return st;
   }
-  // 2. CG_k = (L_k^T A) diag(Gv_k)
-  hipLaunchKernelGGL(expert_bwd_c_kernel, dim3((unsigned)(K * nT * nTn)), dim3(256), 0, s, (const bf16x8*)Afr,
-                     (const bf16x8*)Lfr, (uint32_t)afr_bytes, (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K,
-                     M, N, Gv, ldg, CG, ldn, M * ldn, CGfr, img_elems);
-  if ((st = launch_status())) return st;
-  // 3. gA0 = q_mu G_mu - 2 A sum_k Gv_k
+  // 2. gA0 = q_mu G_mu - 2 A sum_k Gv_k
   {
     const int rows = 128;
     const dim3 grid((unsigned)((N + 255) / 256), (unsigned)((M + rows - 1) / rows));
@@ -833,26 +868,33 @@ extern "C" int mgp_conditional_backward_x6(
                          rows, gA0, ldn);
     if ((st = launch_status())) return st;
   }
-  // 4. gA (image) = 2 sum_k L_k CG_k + gA0
-  hipLaunchKernelGGL(expert_bwd_a_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)LTfr,
-                     (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)CGfr, (uint32_t)img, img_elems, nmk, nTn, K, M,
-                     N, gA0, ldn, gAfr);
+  // 3. gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0
+  hipLaunchKernelGGL(grad_a_s_kernel, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
+                     (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes, nmk, 2 * nTn, K, M,
+                     N, Gv, ldg, gA0, ldn, gAfr);
   if ((st = launch_status())) return st;
-  // 5. gKuf = Linv^T gA
+  // 4. gKuf = Linv^T gA
   hipLaunchKernelGGL(trsm_bwd_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)gAfr,
                      (const bf16x8*)LIfr, (uint32_t)img, (uint32_t)mgp_x6_lower_bytes(M, 1), nmk, nmb, nTn, M, N, g_Kuf,
                      ldk);
   if ((st = launch_status())) return st;
-  // 6. grams over N
-  for (int k = 0; k < K; ++k) {
-    st = mgp_gram(A, lda, M, CG + (int64_t)k * M * ldn, ldn, M, N, 2.f, 1, g_q_sqrt + (int64_t)k * strideg, ldgs,
-                  gws, gwsb, stream);
-    if (st) return st;
-  }
-  st = mgp_gram(g_Kuf, ldk, M, A, lda, M, N, -1.f, 1, g_Lm, ldgl, gws, gwsb, stream);
+  // 5. g_q_sqrt[k] = 2 tril(A diag(Gv_k) (L_k^T A)^T) = 2 tril(P_k L_k), P_k = A diag(Gv_k) A^T
+  //    (x6 grams over N, then over M with the transposed triangle of L_k)
+  st = mgp_gram_x6(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, gws, gwsb, stream);
+  if (st) return st;
+  hipLaunchKernelGGL(tril_transpose_kernel, dim3((unsigned)((M + 31) / 32), (unsigned)((M + 31) / 32), (unsigned)K),
+                     dim3(256), 0, s, q_sqrt, ldqs, strideq, M, LT, ldm, M * ldm);
+  if ((st = launch_status())) return st;
+  st = mgp_gram_x6(P, ldm, M * ldm, M, LT, ldm, M * ldm, M, nullptr, 0, M, K, 2.f, 1, g_q_sqrt, ldgs, strideg, gws,
+                   gwsb, stream);
+  if (st) return st;
+  // 6. g_Lm = -tril(g_Kuf A^T), g_q_mu = A G_mu^T, g_var = sum G_v
+  st = mgp_gram_x6(g_Kuf, ldk, 0, M, A, lda, 0, M, nullptr, 0, N, 1, -1.f, 1, g_Lm, ldgl, M * ldgl, gws, gwsb,
+                   stream);
   if (st) return st;
   st = mgp_gram(A, lda, M, Gmu, ldg, K, N, 1.f, 0, g_q_mu, ldgq, gws, gwsb, stream);
   if (st) return st;
-  hipLaunchKernelGGL(sum_all_kernel, dim3(1), dim3(256), 0, s, Gv, (int64_t)K, N, ldg, g_var);
+  hipLaunchKernelGGL(row_sums_kernel, dim3((unsigned)K), dim3(1024), 0, s, Gv, N, ldg, part);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1), 0, s, part, (int)K, g_var);
   return launch_status();
 }

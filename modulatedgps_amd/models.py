@@ -474,7 +474,7 @@ class SMGP(SGP):
         for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
             M = layer.num_inducing
             with _Stage(timing, "conditional_bwd"):
-                g = ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], b["Lfr_" + L], layer.q_sqrt,
+                g = ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], layer.q_sqrt,
                                                 layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
                                                 workspace=b["ws_cbwd"])
             with _Stage(timing, "chol_bwd"):

@@ -416,11 +416,36 @@ def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):
     return out
 
 
+def gram_x6(X, Y, W=None, alpha=1.0, mode=0, N=None, out=None, workspace=None):
+    """out[b][i][j] = alpha * sum_n X[b][i][n] W[b][n] Y[b][j][n] at f32 accuracy on the bf16 MFMA.
+    X [B, MI, >=N] / [MI, >=N] (Y likewise; a 2-D operand is shared by the batch); W [B, >=N] or None;
+    mode 0 full, 1 lower triangle, 2 symmetric."""
+    X3 = X if X.dim() == 3 else X.unsqueeze(0)
+    Y3 = Y if Y.dim() == 3 else Y.unsqueeze(0)
+    B = max(X3.shape[0], Y3.shape[0], W.shape[0] if W is not None and W.dim() == 2 else 1)
+    MI, MJ = X3.shape[1], Y3.shape[1]
+    N = X3.shape[2] if N is None else N
+    dev = X.device
+    if out is None:
+        out = padded(MI, MJ, dev, batch=B)
+    sx = X3.stride(0) if X3.shape[0] > 1 else 0
+    sy = Y3.stride(0) if Y3.shape[0] > 1 else 0
+    sw = (W.stride(0) if W.dim() == 2 and W.shape[0] > 1 else 0) if W is not None else 0
+    nbytes = _lib.load().mgp_gram_x6_workspace_bytes(MI, MJ, N, B, int(mode))
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, dev)
+    so = out.stride(0) if out.dim() == 3 else MI * _ld(out)
+    _lib.call("mgp_gram_x6", X3.data_ptr(), X3.stride(1), sx, MI, Y3.data_ptr(), Y3.stride(1), sy, MJ,
+              W.data_ptr() if W is not None else None, sw, N, B, float(alpha), int(mode), out.data_ptr(),
+              out.stride(-2), so, workspace.data_ptr(), workspace.numel(), _stream())
+    return out
+
+
 def conditional_backward_workspace_bytes(M, N, K):
     return int(_lib.load().mgp_conditional_backward_workspace_bytes(M, N, K))
 
 
-def conditional_backward_x6(Afr, A, Lfr, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None):
+def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None):
     """Backward of one layer's conditional (see include/mgp_hip.h): returns dict of
     g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1])."""
     K = q_mu.shape[1]
@@ -435,8 +460,8 @@ def conditional_backward_x6(Afr, A, Lfr, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out
     if _ld(Gmu) != _ld(Gv):
         raise ValueError("Gmu and Gv must share a leading dimension")
     o = out
-    _lib.call("mgp_conditional_backward_x6", Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A), Lfr.data_ptr(),
-              Lfr.numel(), q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), q_mu.data_ptr(), _ld(q_mu),
+    _lib.call("mgp_conditional_backward_x6", Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A),
+              q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), q_mu.data_ptr(), _ld(q_mu),
               LinvT.data_ptr(), _ld(LinvT), Gmu.data_ptr(), Gv.data_ptr(), _ld(Gmu), M, N, K,
               o["g_q_mu"].data_ptr(), _ld(o["g_q_mu"]), o["g_q_sqrt"].data_ptr(), _ld(o["g_q_sqrt"]),
               o["g_q_sqrt"].stride(0), o["g_Kuf"].data_ptr(), _ld(o["g_Kuf"]), o["g_Lm"].data_ptr(),

@@ -92,8 +92,7 @@ def test_conditional_backward(device, N, M, K, D, ls):
     Tfr = ops.split_upper_x6(LinvT[0])
     A = ops.padded(M, N, device)
     Afr, _ = ops.trsm_stats_x6(Tfr, Kfr, qmu, M, N, A=A)
-    Lfr = ops.split_lower_x6(qs)
-    g = ops.conditional_backward_x6(Afr, A, Lfr, qs, qmu, LinvT[0], Gmu, Gv, M, N)
+    g = ops.conditional_backward_x6(Afr, A, qs, qmu, LinvT[0], Gmu, Gv, M, N)
     # float64 autograd at the device's own A and L^-1 (the kernels under test see
     # exactly these inputs; A's own f32 error is a forward property, tested there)
     A64 = torch.tensor(to_np(A)[:, :N], requires_grad=True)
@@ -161,3 +160,30 @@ def test_rbf_backward(device, N, M, D, ard, sym):
     assert normwise(to_np(gZ), z64.grad.numpy()) < 1e-4
     assert float(gv.cpu()) == pytest.approx(float(v64.grad), rel=1e-4)
     assert normwise(gl.cpu().numpy(), l64.grad.numpy()) < 1e-4
+
+
+@pytest.mark.parametrize("MI,MJ,N,B,mode,weighted", [(1024, 1024, 16384, 4, 2, True), (300, 300, 5000, 3, 1, False),
+                                                     (130, 70, 777, 1, 0, True), (256, 256, 256, 2, 1, False)])
+def test_gram_x6(device, MI, MJ, N, B, mode, weighted):
+    """x6 gram (on-the-fly split-bf16, six plane products): against float64, errors
+    at float32 level (normwise <= 2e-6 incl. the f32 rounding of the weighted operand)."""
+    from modulatedgps_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(MI + N)
+    X = torch.randn(B, MI, N, generator=g)
+    Y = X[:, :MJ] + 0.3 * torch.randn(B, MJ, N, generator=g) if mode else torch.randn(B, MJ, N, generator=g)
+    W = torch.rand(B, N, generator=g) if weighted else None
+    def pad3(t):
+        d = ops.padded(t.shape[1], t.shape[2], device, batch=t.shape[0])
+        d.copy_(t.to(device))
+        return d if t.shape[0] > 1 else d[0]
+    Xd, Yd = pad3(X), pad3(Y)
+    Wd = pad3(W[:, None, :])[..., 0, :] if weighted else None
+    out = ops.gram_x6(Xd, Yd, Wd, alpha=-0.5, mode=mode, N=N)
+    Yw = Y.double() * (W.double()[:, None, :] if weighted else 1.0)
+    ref = -0.5 * torch.einsum("bin,bjn->bij", X.double(), Yw)
+    if mode == 1:
+        ref = torch.tril(ref)
+    elif mode == 2:
+        ref = torch.tril(ref) + torch.tril(ref, -1).transpose(1, 2)
+    got = to_np(out).reshape(B, MI, -1)[:, :, :MJ]
+    assert normwise(got, ref.numpy()) < 2e-6

@@ -57,6 +57,20 @@ def main():
     Afr, st6 = ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N)
     Lfr = ops.split_lower_x6(q_sqrt)
     fm6, fv6 = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K)
+    # backward operands
+    A32 = ops.padded(M, N, dev)
+    ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Afr, stats=st6, A=A32)
+    G = ops.padded(2 * K, N, dev)
+    G.copy_(1e-3 * torch.randn(2 * K, N, device=dev, generator=g))
+    Gmu, Gv = G[:K], G[K:]
+    P = ops.padded(M, M, dev, batch=K)
+    gK = ops.padded(M, N, dev)
+    gK.copy_(torch.randn(M, N, device=dev, generator=g))
+    gLm = ops.padded(M, M, dev)
+    wsg = torch.empty(max(ops._lib.load().mgp_gram_x6_workspace_bytes(M, M, N, K, 2),
+                          ops._lib.load().mgp_gram_x6_workspace_bytes(M, M, N, 1, 1)), dtype=torch.uint8, device=dev)
+    cb = ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N)
+    wsc = torch.empty(ops.conditional_backward_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     runs = {
         "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
@@ -68,6 +82,10 @@ def main():
         "trsm_stats_x6": lambda: ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Afr, stats=st6),
         "split_lower_x6": lambda: ops.split_lower_x6(q_sqrt, out=Lfr),
         "expert_cond_x6": lambda: ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmean=fm6, fvar=fv6),
+        "gram_x6_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg),
+        "gram_x6_Lm": lambda: ops.gram_x6(gK, A32, None, mode=1, N=N, out=gLm, workspace=wsg),
+        "cond_bwd_x6": lambda: ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
+                                                           out=cb, workspace=wsc),
     }
     if a.only:
         runs = {k: v for k, v in runs.items() if k in a.only.split(",")}
@@ -84,6 +102,10 @@ def main():
         out["expert_cond_x6"]["tflops"] = K * M * M * N / (out["expert_cond_x6"]["median_ms"] * 1e-3) / 1e12
     if "trsm_stats_x6" in out:
         out["trsm_stats_x6"]["tflops"] = M * M * N / (out["trsm_stats_x6"]["median_ms"] * 1e-3) / 1e12
+    for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N),
+                     ("cond_bwd_x6", (2 * K + 1) * M * M * N)):
+        if name in out:
+            out[name]["tflops"] = fl / (out[name]["median_ms"] * 1e-3) / 1e12
     if "rbf_kuf_x6" in out:
         out["rbf_kuf_x6"]["GBps"] = (4 * (N * D + M * D) + 6 * M * N) / (out["rbf_kuf_x6"]["median_ms"] * 1e-3) / 1e9
     if "trsm_stats" in out:
