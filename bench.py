@@ -169,7 +169,7 @@ def load_traffic(kernel):
     if not os.path.exists(path):
         return None, None
     d = json.load(open(path))
-    e = d.get(kernel)
+    e = d.get("kernels", d).get(kernel)
     if not e:
         return None, None
     return e.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)

@@ -526,43 +526,74 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
 // models.py:141), as in PyTorch / Murray (2016):
 //   P = Phi(Lm^T gL)  (lower triangle, diagonal halved),  S = Lm^-T P Lm^-1,
 //   gKuu = (S + S^T) / 2,
-// all in float64 (M^3 work; Kuu is badly conditioned).  dgemm: C = op(A) op(B),
-// 64 x 64 tiles, 256 threads x 4 x 4 outputs, 16-deep LDS chunks.
+// all in float64 (M^3 work; Kuu is badly conditioned).  dgemm: C = op(A) op(B)
+// on v_mfma_f64_16x16x4_f64: 64 x 64 tile per workgroup (4 waves x 32 x 32 =
+// 2 x 2 MFMA blocks each), 16-deep LDS chunks.
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A, int64_t lda,
                                                     const double* __restrict__ B, int64_t ldb,
                                                     double* __restrict__ C, int64_t ldc, int64_t M) {
-  __shared__ double sa[16][64 + 1], sb[16][64 + 1];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  __shared__ double sa[64][17], sb[16][65];  // sa[i][k] = op(A), sb[k][j] = op(B)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wi = (w >> 1) * 32, wj = (w & 1) * 32;
   const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
-  double acc[4][4] = {};
-  for (int64_t k0 = 0; k0 < M; k0 += 16) {
-    for (int idx = threadIdx.x; idx < 16 * 64; idx += 256) {
-      const int kk = idx / 64, r = idx % 64;
-      const int64_t k = k0 + kk, i = i0 + r, j = j0 + r;
-      sa[kk][r] = (k < M && i < M) ? (TA ? A[k * lda + i] : A[i * lda + k]) : 0.0;
-      sb[kk][r] = (k < M && j < M) ? (TB ? B[j * ldb + k] : B[k * ldb + j]) : 0.0;
+  doublex4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = doublex4{0.0, 0.0, 0.0, 0.0};
+  // chunk k0 .. k0 + 15: thread loads 4 elements of each operand (coalesced along
+  // the contiguous index), one chunk ahead in registers
+  double ra[4], rb[4];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + 256 * q;
+      const int r_a = TA ? idx % 64 : idx / 16, k_a = TA ? idx / 64 : idx % 16;
+      const int64_t ia = i0 + r_a, kA = k0 + k_a;
+      ra[q] = (ia < M && kA < M) ? (TA ? A[kA * lda + ia] : A[ia * lda + kA]) : 0.0;
+      const int c_b = TB ? idx / 16 : idx % 64, k_b = TB ? idx % 16 : idx / 64;
+      const int64_t jb = j0 + c_b, kB = k0 + k_b;
+      rb[q] = (jb < M && kB < M) ? (TB ? B[jb * ldb + kB] : B[kB * ldb + jb]) : 0.0;
     }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + 256 * q;
+      sa[TA ? idx % 64 : idx / 16][TA ? idx / 64 : idx % 16] = ra[q];
+      sb[TB ? idx % 16 : idx / 64][TB ? idx / 16 : idx % 64] = rb[q];
+    }
+  };
+  load(0);
+  for (int64_t k0 = 0; k0 < M; k0 += 16) {
+    store();
     __syncthreads();
+    if (k0 + 16 < M) load(k0 + 16);
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      double a[4], b[4];
+    for (int ks = 0; ks < 4; ++ks) {
+      double av[2], bv[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) { a[q] = sa[kk][ty + 16 * q]; b[q] = sb[kk][tx + 16 * q]; }
+      for (int t = 0; t < 2; ++t) {
+        av[t] = sa[wi + 16 * t + (lane & 15)][4 * ks + (lane >> 4)];
+        bv[t] = sb[4 * ks + (lane >> 4)][wj + 16 * t + (lane & 15)];
+      }
 #pragma unroll
-      for (int qi = 0; qi < 4; ++qi)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int qj = 0; qj < 4; ++qj) acc[qi][qj] = fma(a[qi], b[qj], acc[qi][qj]);
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int qi = 0; qi < 4; ++qi)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int qj = 0; qj < 4; ++qj) {
-      const int64_t i = i0 + ty + 16 * qi, j = j0 + tx + 16 * qj;
-      if (i < M && j < M) C[i * ldc + j] = acc[qi][qj];
-    }
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = i0 + wi + 16 * a + (lane >> 4) + 4 * r, j = j0 + wj + 16 * b + (lane & 15);
+        if (i < M && j < M) C[i * ldc + j] = acc[a][b][r];
+      }
 }
 
 // mode 0: dst = f64(src) (src f32);  1: dst = f64(src^T);  2: Phi (tril, diag / 2) in place on f64;

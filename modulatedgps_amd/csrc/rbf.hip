@@ -176,13 +176,16 @@ static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, 
 
 // ------------------------------------------------------------------ RBF backward
 // Reverse mode of K(Z, X) = var exp(-1/2 sum_d c_d^2 (z_d - x_d)^2), c = 1 / l
-// (models.py:135,139) for a cotangent gK [M][N]: with w_mn = gK_mn k_mn
-//   g_var = sum w / var,   g_z_md = -c_d^2 (z_md S0_m - S1_md),
-//   g_l_d = c_d^3 sum_m (z_md^2 S0_m - 2 z_md S1_md + S2_md),
-//   S0_m = sum_n w_mn, S1_md = sum_n w_mn x_nd, S2_md = sum_n w_mn x_nd^2  (float64).
+// (models.py:135,139) for a cotangent gK [M][N]: with w_mn = gK_mn k_mn and the
+// centred sums (no cancellation between large terms)
+//   S0_m = sum_n w_mn,  T1_md = sum_n w_mn (x_nd - z_md),  T2_md = sum_n w_mn (x_nd - z_md)^2
+//   g_var = sum w / var,  g_z_md = c_d^2 T1_md,  g_l_d = c_d^3 sum_m T2_md.
 // For Kuu (X = Z, symmetric gK) z enters both arguments: g_z doubles.
-// Kernel 1: 4 waves x 4 rows of Z per block, lanes stride over an n-chunk;
-// per-(chunk, row) partials.  Kernel 2 folds the chunks and writes the grads.
+// Kernel 1: 4 waves x 2 rows of Z per block, lanes stride over an n-chunk four
+// points at a time; each lane accumulates its <= 64 points in float32 (sums of
+// centred terms), the lane / chunk reduction is float64.  Kernel 2 folds the
+// chunks and writes the grads.
+constexpr int kRbfRows = 2;  // rows of Z per wave
 template <int DMAX>
 __global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restrict__ X, int64_t ldx,
                                                            const float* __restrict__ Z, int64_t ldz, int64_t N,
@@ -190,55 +193,64 @@ __global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restri
                                                            const float* __restrict__ ls, int n_ls,
                                                            const float* __restrict__ gK, int64_t ldg,
                                                            int64_t nchunk, double* __restrict__ part) {
-  constexpr int NS = 1 + 2 * DMAX;
+  constexpr int NS = 1 + 2 * DMAX, R = kRbfRows;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * 16 + 4 * w;
+  const int64_t m0 = (int64_t)blockIdx.x * 4 * R + R * w;
   const int64_t nb = (int64_t)blockIdx.y * nchunk;
   const int64_t ne = (nb + nchunk < N) ? nb + nchunk : N;
-  float c2[DMAX], z[4][DMAX];
+  float hc2[DMAX], z[R][DMAX];
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
     const float c = (d < D) ? 1.f / ls[n_ls == 1 ? 0 : d] : 0.f;
-    c2[d] = c * c;
+    hc2[d] = -0.5f * c * c;
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) z[r][d] = (m0 + r < M && d < D) ? Z[(m0 + r) * ldz + d] : 0.f;
   const float var = variance[0];
-  double acc[4][NS];
+  float acc[R][NS];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int j = 0; j < NS; ++j) acc[r][j] = 0.0;
-  for (int64_t n = nb + lane; n < ne; n += 64) {
-    float x[DMAX];
+    for (int j = 0; j < NS; ++j) acc[r][j] = 0.f;
+  auto point = [&](int64_t n) {
+    float x[DMAX], g[R];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[n * ldx + d] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (m0 + r >= M) break;
-      float q = 0.f;
+    for (int r = 0; r < R; ++r) g[r] = (m0 + r < M) ? gK[(m0 + r) * ldg + n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float dx[DMAX], q = 0.f;
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        const float df = z[r][d] - x[d];
-        q = fmaf(c2[d] * df, df, q);
+        dx[d] = x[d] - z[r][d];
+        q = fmaf(hc2[d] * dx[d], dx[d], q);
       }
-      const double wv = (double)gK[(m0 + r) * ldg + n] * (double)(var * __expf(-0.5f * q));
+      const float wv = g[r] * (var * __expf(q));
       acc[r][0] += wv;
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        const double xd = (double)x[d];
-        acc[r][1 + d] = fma(wv, xd, acc[r][1 + d]);
-        acc[r][1 + DMAX + d] = fma(wv * xd, xd, acc[r][1 + DMAX + d]);
+        const float t = wv * dx[d];
+        acc[r][1 + d] += t;
+        acc[r][1 + DMAX + d] = fmaf(t, dx[d], acc[r][1 + DMAX + d]);
       }
     }
+  };
+  int64_t n = nb + lane;
+  for (; n + 192 < ne; n += 256) {
+    point(n);
+    point(n + 64);
+    point(n + 128);
+    point(n + 192);
   }
+  for (; n < ne; n += 64) point(n);
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      double v = acc[r][j];
+      double v = (double)acc[r][j];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
       if (lane == 0 && m0 + r < M) part[((int64_t)blockIdx.y * M + m0 + r) * NS + j] = v;
@@ -271,10 +283,9 @@ __global__ __launch_bounds__(256) void rbf_bwd_finish_kernel(const double* __res
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
       if (d >= D) break;
-      const double zd = (double)Z[m * ldz + d];
-      const double gz = -zfactor * c[d] * c[d] * (zd * S[0] - S[1 + d]);
+      const double gz = zfactor * c[d] * c[d] * S[1 + d];
       gZ[m * ldgz + d] = (float)(accumulate ? (double)gZ[m * ldgz + d] + gz : gz);
-      gl[d] += c[d] * c[d] * c[d] * (zd * zd * S[0] - 2.0 * zd * S[1 + d] + S[1 + DMAX + d]);
+      gl[d] += c[d] * c[d] * c[d] * S[1 + DMAX + d];
     }
   }
   const double var = (double)variance[0];
@@ -414,7 +425,7 @@ extern "C" int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int
   const int nch = (int)((N + chunk - 1) / chunk);
   double* part = (double*)workspace;
   const float zf = symmetric ? 2.f : 1.f;
-  const dim3 grid((unsigned)((M + 15) / 16), (unsigned)(nch > 0 ? nch : 1));
+  const dim3 grid((unsigned)((M + 4 * kRbfRows - 1) / (4 * kRbfRows)), (unsigned)(nch > 0 ? nch : 1));
 #define MGP_RBF_BWD_CASE(DM)                                                                                  \
   if (D <= DM) {                                                                                              \
     if (nch > 0)                                                                                              \

@@ -50,6 +50,27 @@ def allreduce_data_term(t, group=None):
     return t
 
 
+def allreduce_gradients(tensors, group=None):
+    """Sum a list of gradient tensors over the group with one collective per dtype:
+    the tensors are packed into a flat bucket (float32 / float64), all-reduced and
+    unpacked in place.  The training step's only data-path exchange (the gradients
+    of the per-shard data terms; the KL part is added after it on every rank)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return tensors
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for ts in by_dtype.values():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        o = 0
+        for t in ts:
+            n = t.numel()
+            t.copy_(flat[o:o + n].view_as(t))
+            o += n
+    return tensors
+
+
 def sharded_elbo(model, X_local, Y_local, n_offset, n_total, group=None, **kw):
     """ELBO of the global batch from this rank's shard (SMGP._build_likelihood with
     the shard's global row offset and one all-reduce of the data term)."""

@@ -491,11 +491,9 @@ class SMGP(SGP):
             grads.update({name + ".Z": gZ, name + ".variance": gvar, name + ".lengthscales": gls,
                           name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]})
         if process_group is not None:
-            import torch.distributed as dist
+            from .distributed import allreduce_gradients
             with _Stage(timing, "allreduce"):
-                dist.all_reduce(b["data_sum"], op=dist.ReduceOp.SUM, group=process_group)
-                for t in grads.values():
-                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=process_group)
+                allreduce_gradients([b["data_sum"]] + list(grads.values()), group=process_group)
         num_data = self.num_data if self.num_data is not None else n_batch
         for name, layer in (("pred", self.pred_layer), ("assign", self.assign_layer)):
             ops.kl_grad(layer.q_mu, layer.q_sqrt, num_data, grads[name + ".q_mu"], grads[name + ".q_sqrt"])

@@ -87,3 +87,69 @@ def test_two_rank_allreduce_reproduces_full_elbo():
     reduced, full, elbo_dp, elbo_ref = res
     assert reduced == pytest.approx(full, rel=1e-12)
     assert elbo_dp == pytest.approx(elbo_ref, rel=1e-12)
+
+
+def _grad_worker(rank, world, port, q):
+    """Data-parallel training-step gradient: each rank differentiates its shard's
+    data term (scaled by 1 / N_total) with the float64 autograd oracle, the
+    gradients go through modulatedgps_amd.distributed.allreduce_gradients (one
+    bucket per dtype), then every rank adds the KL gradient - the order
+    SMGP.elbo_and_grad uses.  Rank 0 compares with the single-process gradient."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from modulatedgps_amd.distributed import allreduce_gradients
+    from oracle import cpu_ref as R
+    from oracle import grad_ref as GR
+    N = 240
+    X, Y, p = R.synthetic_problem(N, 10, 3, 2, 0.7, state="perturbed", S=3)
+    z, u = R.explicit_noise(p.S, N, 3, seed=11)
+    t64 = lambda a: torch.tensor(np.asarray(a, np.float64))
+
+    def leaves():
+        pred, assign, lik = GR.params_from_oracle(p)
+        return pred, assign, lik
+
+    def grads_of(pred, assign, lik):
+        out = [lik.grad]
+        for L in (pred, assign):
+            out += [L[k].grad for k in GR.LAYER_KEYS]
+        return out
+
+    # this rank's shard
+    lo, hi = shard_rows(N, rank, world)
+    pred, assign, lik = leaves()
+    mu_f, var_f, _ = GR.layer_conditional(t64(X[lo:hi]), pred)
+    mu_a, var_a, _ = GR.layer_conditional(t64(X[lo:hi]), assign)
+    dt = GR.data_term(mu_f, var_f, mu_a, var_a, t64(Y[lo:hi]), lik, t64(z[:, lo:hi]), t64(u[:, lo:hi]))
+    (dt / N).backward()
+    g = [t.clone() for t in grads_of(pred, assign, lik)]
+    allreduce_gradients(g)
+    # KL part, added locally after the reduction
+    pred2, assign2, lik2 = leaves()
+    kl = GR.gauss_kl_white(pred2["q_mu"], pred2["q_sqrt"]) + GR.gauss_kl_white(assign2["q_mu"], assign2["q_sqrt"])
+    (-kl / p.num_data).backward()
+    for i, L in enumerate((pred2, assign2)):
+        for j, k in enumerate(GR.LAYER_KEYS):
+            if L[k].grad is not None:
+                g[1 + 5 * i + j] = g[1 + 5 * i + j] + L[k].grad
+    if rank == 0:
+        pr, asg, lk = leaves()
+        GR.elbo(t64(X), t64(Y), pr, asg, lk, t64(z), t64(u), p.num_data).backward()
+        ref = grads_of(pr, asg, lk)
+        q.put([float((a - b).abs().max() / (b.abs().max() + 1e-300)) for a, b in zip(g, ref)])
+    dist.destroy_process_group()
+
+
+def test_two_rank_gradient_allreduce_reproduces_full_gradient():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    errs = q.get(timeout=180)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert max(errs) < 1e-10, errs

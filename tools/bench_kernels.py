@@ -84,6 +84,7 @@ def main():
         "expert_cond_x6": lambda: ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmean=fm6, fvar=fv6),
         "gram_x6_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg),
         "gram_x6_Lm": lambda: ops.gram_x6(gK, A32, None, mode=1, N=N, out=gLm, workspace=wsg),
+        "rbf_bwd": lambda: ops.rbf_backward(X, Z, var, lsc, gK),
         "cond_bwd_x6": lambda: ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
                                                            out=cb, workspace=wsc),
     }
@@ -106,6 +107,8 @@ def main():
                      ("cond_bwd_x6", (2 * K + 1) * M * M * N)):
         if name in out:
             out[name]["tflops"] = fl / (out[name]["median_ms"] * 1e-3) / 1e12
+    if "rbf_bwd" in out:
+        out["rbf_bwd"]["GBps"] = 4 * M * N / (out["rbf_bwd"]["median_ms"] * 1e-3) / 1e9
     if "rbf_kuf_x6" in out:
         out["rbf_kuf_x6"]["GBps"] = (4 * (N * D + M * D) + 6 * M * N) / (out["rbf_kuf_x6"]["median_ms"] * 1e-3) / 1e9
     if "trsm_stats" in out:
