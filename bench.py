@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (ELBO + gradient + Adam) leg")
+    ap.add_argument("--layout", default="data", choices=("data", "expert"),
+                    help="multi-GPU layout: 'data' shards N (weak scaling, the default); 'expert' shards the "
+                         "K experts over the ranks on a fixed N (the north_star layout, strong scaling)")
     ap.add_argument("--cpu-sample", type=int, nargs=2, default=(8192, 65536),
                     help="two N sizes of the CPU oracle sample (linear fit in N; the full N "
                          "is timed directly when it is one of them)")
@@ -221,15 +224,24 @@ def main():
     device = torch.device("cuda", local if world > 1 else 0)
     cfg = CONFIGS[args.config]
     N, M, K, D, ls, S = cfg
-    X_np, Y_np, layers = synthetic(cfg, rank, device)
-    n_total = N * world
+    expert = args.layout == "expert" and world > 1
+    X_np, Y_np, layers = synthetic(cfg, 0 if expert else rank, device)
+    n_total = N if expert else N * world
     model = build_model(cfg, layers, device, num_data=n_total)
     X = torch.from_numpy(X_np).to(device)
     Y = torch.from_numpy(Y_np).to(device)
     kw = dict(n_offset=rank * N, n_total=n_total, process_group=group)
+    if expert:
+        from modulatedgps_amd.distributed import expert_parallel_elbo
+
+        def elbo_step(timing=None):
+            return expert_parallel_elbo(model, X, Y, group=group)
+    else:
+        def elbo_step(timing=None):
+            return model._build_likelihood(X, Y, timing=timing, **kw)
 
     for _ in range(args.warmup):
-        model._build_likelihood(X, Y, **kw)
+        elbo_step()
     torch.cuda.synchronize()
     timing = {}
 
@@ -241,7 +253,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        elbo = model._build_likelihood(X, Y, timing=timing, **kw)
+        elbo = elbo_step(timing)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -250,7 +262,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     elbo_val = float(elbo.item())
-    info = model.last_info.cpu().tolist()
+    info = model.last_info.cpu().tolist() if model.last_info is not None else None
     st = stage_stats(timing)
 
     # algorithmic work per launch
@@ -298,8 +310,8 @@ def main():
                               "2.5 PF bf16 dense / 6" if x6 else "f32 MFMA dense peak")}
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * args.steps / elapsed
-    train = None if args.no_train else train_leg(model, X, Y, kw, args, barrier, world, device)
+    value = (1 if expert else world) * args.steps / elapsed
+    train = None if (args.no_train or expert) else train_leg(model, X, Y, kw, args, barrier, world, device)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, tuple(args.cpu_sample))
@@ -309,14 +321,16 @@ def main():
             "metric": "ELBO steps/sec (N=65536, M=1024, K=8); Kuf HBM GB/s vs roofline",
             "value": value, "unit": "ELBO steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "strong" if expert else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "dtype_note": ("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
                            "3-plane split (6 products, f32-accurate); K3 in f64" if x6 else
                            "f32 MFMA (exact f32); K3 in f64"),
             "config": {"workload": f"{args.config}: SMGP ELBO forward, N={N}/GPU, M={M}, K={K}, "
                                    f"D={D}, S={S}, lengthscale={ls}",
                        "global_batch": n_total, "N_per_gpu": N, "M": M, "K": K, "D": D, "S": S,
-                       "parallelism": f"dp{world} (N-sharded, scalar RCCL all-reduce)"},
+                       "parallelism": (f"ep{world} (K experts sharded over ranks on N={N}, one RCCL all_to_all of "
+                                       f"the conditionals + one scalar all-reduce)" if expert else
+                                       f"dp{world} (N-sharded, scalar RCCL all-reduce)")},
             "roofline": roofline,
             "kernels": kernels,
             "kuf_hbm": kernels.get("rbf_kuf"),

@@ -198,6 +198,25 @@ class SVGPModified:
                                              fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
                                              workspace=bufs.get("ws_expert"))
 
+    def conditional_experts(self, X, k0, k1, LinvT=None):
+        """fmean, fvar [k1 - k0, N] of experts k0 .. k1 - 1 only (the expert-parallel
+        layout: each rank owns a range of the K experts).  Kuf, the
+        Cholesky and A are shared by all experts and computed in full; K4's
+        statistics and K5 run on the expert range (q_mu columns, q_sqrt batch)."""
+        X = self.kernel._x(X)
+        M, N = self.num_inducing, X.shape[0]
+        if not (0 <= k0 <= k1 <= self.num_latent_gps):
+            raise ValueError("invalid expert range")
+        if LinvT is None:
+            _, LinvT, info = self.factorise()
+            self._last_info = info
+            LinvT = LinvT[0]
+        Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales)
+        Tfr = ops.split_upper_x6(LinvT)
+        Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu[:, k0:k1], M, N)
+        Lfr = ops.split_lower_x6(self.q_sqrt[k0:k1])
+        return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, k1 - k0)
+
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
         """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior
         (models.py:129-144).  Xnew [..., N, D] -> mean, var [..., N, K]."""

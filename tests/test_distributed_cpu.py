@@ -153,3 +153,41 @@ def test_two_rank_gradient_allreduce_reproduces_full_gradient():
         pr.join(timeout=60)
         assert pr.exitcode == 0
     assert max(errs) < 1e-10, errs
+
+
+def _a2a_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from modulatedgps_amd.distributed import redistribute_experts
+    K, C, N = 5, 4, 37
+    counts = [b - a for a, b in (shard_rows(K, r, world) for r in range(world))]
+    k0, k1 = shard_rows(K, rank, world)
+    k = torch.arange(k0, k1, dtype=torch.float32)[:, None, None]
+    c = torch.arange(C, dtype=torch.float32)[None, :, None]
+    n = torch.arange(N, dtype=torch.float32)[None, None, :]
+    local = 1000 * k + 100 * c + n
+    mine = redistribute_experts(local, counts, N)
+    lo, hi = shard_rows(N, rank, world)
+    kk = torch.arange(K, dtype=torch.float32)[:, None, None]
+    ref = 1000 * kk + 100 * c + torch.arange(lo, hi, dtype=torch.float32)[None, None, :]
+    q.put((rank, bool(torch.equal(mine, ref)), tuple(mine.shape)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_expert_layout_redistribution(world):
+    """Expert-parallel layout (north_star: experts sharded over GPUs): the exchange
+    that moves every expert's conditionals to the rank owning each point slice
+    (all_to_all on RCCL, point-to-point on gloo), including a rank with fewer
+    experts than another (K = 5)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert all(ok for _, ok, _ in res), res

@@ -145,3 +145,60 @@ def test_smgp_modified_elbo(device, N, M, K, D, ls, S):
     assert e == pytest.approx(ref, rel=1e-4)
     # the plain SMGP term on the same model state is different (the extra term is live)
     assert abs(float(base._build_likelihood(Xd, Y, noise=dev_noise(z, u, device)).cpu()) - e) > 1e-3 * abs(e)
+
+
+def test_conditional_experts_partition(device):
+    """Expert-parallel layout: the conditionals of an expert range (K4 stats and K5
+    on q_mu[:, k0:k1], q_sqrt[k0:k1]) equal those rows of the full conditional."""
+    X, Y, p = R.synthetic_problem(3000, 130, 5, 3, 0.9, state="perturbed", S=4)
+    model = build_model(p, device)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    for layer in (model.pred_layer, model.assign_layer):
+        fm, fv = (t.clone() for t in layer.conditional_kn(Xd))
+        for k0, k1 in ((0, 2), (2, 3), (3, 5)):
+            em, ev = layer.conditional_experts(Xd, k0, k1)
+            assert torch.equal(em[:, :3000], fm[k0:k1, :3000])
+            assert torch.equal(ev[:, :3000], fv[k0:k1, :3000])
+
+
+def _expert_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    from modulatedgps_amd.distributed import expert_parallel_elbo
+    X, Y, p = R.synthetic_problem(2000, 64, 5, 2, 0.8, state="perturbed", S=6)
+    z, u = R.explicit_noise(6, 2000, 5, seed=5)
+    model = build_model(p, dev)
+    e = expert_parallel_elbo(model, torch.as_tensor(X, dtype=torch.float32, device=dev), Y,
+                             noise=dev_noise(z, u, dev))
+    if rank == 0:
+        ref = float(model._build_likelihood(torch.as_tensor(X, dtype=torch.float32, device=dev), Y,
+                                            noise=dev_noise(z, u, dev)).cpu())
+        q.put((float(e.cpu()), ref, R.smgp_elbo(X, Y, p, z, u)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_expert_parallel_elbo(device, world):
+    """The north_star expert layout (experts sharded over ranks, all_to_all of the
+    conditionals, one scalar all-reduce) reproduces the single-process ELBO and
+    the oracle.  Rehearsed with gloo, every rank on cuda:0 (the 8-GPU run uses RCCL)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_expert_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    e, ref, oracle = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert e == pytest.approx(ref, rel=1e-6)
+    assert e == pytest.approx(oracle, rel=1e-4)
