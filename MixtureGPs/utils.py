@@ -1,2 +1,2 @@
 """Drop-in for MixtureGPs/utils.py (reparameterize)."""
-from modulatedgps_amd.utils import reparameterize  # noqa: F401
+from modulatedgps_amd.utils import print_summary, reparameterize  # noqa: F401

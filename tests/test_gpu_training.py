@@ -128,17 +128,16 @@ def test_adam_step(device):
 def test_run_adam_improves_elbo(device):
     """utils.training_utils.run_adam drop-in: same signature / return value; the ELBO
     rises over a short run on the c1-shaped problem (minibatches of 250)."""
+    from MixtureGPs.utils import print_summary
+    from utils.data import Dataset
     from utils.training_utils import run_adam
     X, Y, p = R.synthetic_problem(1000, 25, 3, 1, 0.5, state="init", S=5)
     model = build_model(p, device)
-    rng = np.random.default_rng(0)
-
-    def batches():
-        while True:
-            idx = rng.choice(1000, 250, replace=False)
-            yield X[idx].astype(np.float32), Y[idx].astype(np.float32)
-
-    it = batches()
+    # the demos' tf.data pipeline, on HBM-resident arrays
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    Yd = torch.as_tensor(Y, dtype=torch.float32, device=device)
+    it = iter(Dataset.from_tensor_slices((Xd, Yd)).shuffle(buffer_size=1000, seed=0).batch(250).repeat())
+    assert "pred.q_sqrt" in print_summary(model)
     e0 = np.mean([-float(model.training_loss(next(it)).cpu()) for _ in range(10)])
     iters, elbos = run_adam(model, 60, it, 0.01)
     assert iters == list(range(5, 61, 5))

@@ -5,3 +5,31 @@ def test_run_adam_signature():
     import inspect
     from utils.training_utils import run_adam
     assert list(inspect.signature(run_adam).parameters) == ["model", "num_iter", "train_iter", "lr", "compile"]
+
+
+def test_dataset_pipeline_semantics():
+    """tf.data replacement: shuffle(buffer = all).batch(b).repeat():
+    each pass is a fresh permutation, the short remainder batch is emitted, the
+    stream is seeded, components stay aligned, device/host arrays both work."""
+    import itertools
+    import numpy as np
+    import torch
+    from utils.data import Dataset
+    X = np.arange(600, dtype=np.float32)[:, None]
+    Y = 10 * np.arange(600, dtype=np.float32)[:, None]
+    ds = Dataset.from_tensor_slices((X, Y)).shuffle(buffer_size=600, seed=0).batch(500).repeat()
+    it = iter(ds)
+    batches = list(itertools.islice(it, 6))
+    assert [len(b[0]) for b in batches] == [500, 100] * 3
+    for bx, by in batches:
+        assert np.array_equal(by, 10 * bx)
+    e1 = np.concatenate([b[0][:, 0] for b in batches[:2]])
+    e2 = np.concatenate([b[0][:, 0] for b in batches[2:4]])
+    assert sorted(e1) == list(range(600)) and sorted(e2) == list(range(600))
+    assert not np.array_equal(e1, e2)                      # reshuffled each pass
+    again = list(itertools.islice(iter(ds), 2))
+    assert np.array_equal(again[0][0], batches[0][0])      # seeded
+    assert [len(b[0]) for b in Dataset.from_tensor_slices((X, Y)).batch(500, drop_remainder=True).repeat(2)] == [500, 500]
+    # a small shuffle buffer still yields a permutation per pass
+    small = list(Dataset.from_tensor_slices(torch.arange(50)).shuffle(8, seed=1).batch(50))
+    assert sorted(small[0].tolist()) == list(range(50))
