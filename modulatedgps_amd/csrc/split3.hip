@@ -498,6 +498,7 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
       }
     }
   if (Af32) store_acc_f32(acc, Af32, lda, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
+  if (!stats) return;
   // ---- stats (rows beyond M are zero in A; tiles starting at or beyond M are not stored)
   const int64_t i0 = 128 * (int64_t)t;
   float* sQ = reinterpret_cast<float*>(&sL[0][0]);  // [128][KMAX]; the main loop ended on a barrier
@@ -680,8 +681,7 @@ extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* 
   if (K > 16) return MGP_ERR_UNSUPPORTED;
   if (!Afr) return -10;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -11;
-  if (!stats) return -12;
-  if (lds < N) return -13;
+  if (stats && lds < N) return -13;
   if (A && lda < N) return -15;
   if (!aligned16(Tfr) || !aligned16(Kfr) || !aligned16(Afr)) return MGP_ERR_ALIGN;
   if (mgp_x6_cols_bytes(M, N) >= ((size_t)1 << 32) || mgp_x6_lower_bytes(M, 1) >= ((size_t)1 << 32))

@@ -187,16 +187,23 @@ class SVGPModified:
                 return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
                                               fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
                                               workspace=bufs.get("ws_expert"))
-        M, N, K = self.num_inducing, X.shape[0], self.num_latent_gps
+        Afr, stats = self.x6_trsm(X.shape[0], LinvT, Kfr, bufs, timing)
+        return self.x6_expert(X.shape[0], Afr, Lfr, stats, bufs, timing)
+
+    def x6_trsm(self, N, LinvT, Kfr, bufs, timing=None):
+        """K4 on images: A's image and the column statistics (x6 mode)."""
         with _Stage(timing, "split_tri"):
             Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"))
         with _Stage(timing, "trsm_stats"):
-            Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, M, N, Afr=bufs.get("Afr"),
-                                           stats=bufs.get("stats"), A=bufs.get("A32"))
+            return ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, self.num_inducing, N, Afr=bufs.get("Afr"),
+                                     stats=bufs.get("stats"), A=bufs.get("A32"))
+
+    def x6_expert(self, N, Afr, Lfr, stats, bufs, timing=None):
+        """K5 on images: fmean, fvar [K, N] (x6 mode)."""
         with _Stage(timing, "expert_cond"):
-            return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, K,
-                                             fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
-                                             workspace=bufs.get("ws_expert"))
+            return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, self.num_inducing, N,
+                                             self.num_latent_gps, fmean=bufs.get("fmean"),
+                                             fvar=bufs.get("fvar"), workspace=bufs.get("ws_expert"))
 
     def conditional_experts(self, X, k0, k1, LinvT=None):
         """fmean, fvar [k1 - k0, N] of experts k0 .. k1 - 1 only (the expert-parallel
@@ -287,13 +294,13 @@ class SMGP(SGP):
         x6 = conditional_mode() == "x6"
         kuf = None if x6 else ops.padded(Mx, N, dev)
         a = None if x6 else ops.padded(Mx, N, dev)
-        st = ops.padded(T * (K + 1), N, dev)
+        st = ops.padded(2 * T * (K + 1), N, dev)  # per layer (the layers' K4 may run concurrently)
         cond = ops.padded(4 * K, N, dev)          # mu_f, var_f, mu_a, var_a
         b = {
             "Kuf_f": None if x6 else kuf[:Mf], "Kuf_a": None if x6 else kuf[:Ma],
             "A_f": None if x6 else a[:Mf], "A_a": None if x6 else a[:Ma],
             "stats_f": st[:ops.stats_tiles(Mf) * (K + 1)].unflatten(0, (-1, K + 1)),
-            "stats_a": st[:ops.stats_tiles(Ma) * (K + 1)].unflatten(0, (-1, K + 1)),
+            "stats_a": st[T * (K + 1):(T + ops.stats_tiles(Ma)) * (K + 1)].unflatten(0, (-1, K + 1)),
             "mu_f": cond[0:K], "var_f": cond[K:2 * K], "mu_a": cond[2 * K:3 * K],
             "var_a": cond[3 * K:4 * K],
             "kl": torch.empty(2, dtype=torch.float64, device=dev),
@@ -309,8 +316,9 @@ class SMGP(SGP):
             for L in ("f", "a"):
                 b["Kfr_" + L] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
                 b["Lfr_" + L] = torch.empty(ops.x6_lower_bytes(Mx, K), dtype=torch.uint8, device=dev)
-            b["Afr"] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
-            b["Tfr"] = torch.empty(ops.x6_lower_bytes(Mx, 1), dtype=torch.uint8, device=dev)
+            for L in ("f", "a"):  # per layer: the two layers' K4 run concurrently
+                b["Afr_" + L] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
+                b["Tfr_" + L] = torch.empty(ops.x6_lower_bytes(Mx, 1), dtype=torch.uint8, device=dev)
         b["x6"] = x6
         if Mf == Ma and self.pred_layer.Z.shape[1] == self.assign_layer.Z.shape[1]:
             b["LinvT2"] = ops.padded(Mf, Mf, dev, batch=2)
@@ -321,7 +329,6 @@ class SMGP(SGP):
             if "LinvT2" in b:
                 b["L2"] = ops.padded(Mf, Mf, dev, batch=2)
             for L, M in (("f", Mf), ("a", Ma)):  # kept for the backward pass
-                b["Afr_" + L] = torch.empty(ops.x6_cols_bytes(Mx, N), dtype=torch.uint8, device=dev)
                 b["A32_" + L] = ops.padded(M, N, dev)
             b["G"] = ops.padded(4 * K, N, dev).unflatten(0, (4, K))
             b["ws_cbwd"] = torch.empty(ops.conditional_backward_workspace_bytes(Mx, N, K), dtype=torch.uint8,
@@ -392,11 +399,24 @@ class SMGP(SGP):
         if b["x6"]:
             main.wait_stream(side)
         LinvT = {"f": LinvT_f, "a": LinvT_a}
-        for L, layer in layers:
-            bufs = {"Kuf": b["Kuf_" + L], "A": b["A_" + L], "stats": b["stats_" + L],
+        bufs = {L: {"Kuf": b["Kuf_" + L], "A": b["A_" + L], "stats": b["stats_" + L],
                     "fmean": b["mu_" + L], "fvar": b["var_" + L], "ws_expert": b["ws_expert"],
-                    "Afr": b.get("Afr_" + L, b.get("Afr")), "Tfr": b.get("Tfr"), "A32": b.get("A32_" + L)}
-            layer.conditional_kn(X, LinvT[L], bufs=bufs, timing=timing, images=images.get(L))
+                    "Afr": b.get("Afr_" + L, b.get("Afr")), "Tfr": b.get("Tfr_" + L, b.get("Tfr")),
+                    "A32": b.get("A32_" + L)} for L, _ in layers}
+        if b["x6"] and "Tfr_a" in b:
+            # K4 of the assign layer on the side stream, beside the pred layer's K4 and
+            # K5 (K4 leaves MFMA and memory slack that the other kernels fill)
+            pf, pa = self.pred_layer, self.assign_layer
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing)
+            Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing)
+            pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing)
+            main.wait_stream(side)
+            pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing)
+        else:
+            for L, layer in layers:
+                layer.conditional_kn(X, LinvT[L], bufs=bufs[L], timing=timing, images=images.get(L))
         if kl_out is not None and not b["x6"]:
             with _Stage(timing, "gauss_kl"):
                 self.pred_layer.prior_kl(out=kl_out[0:1])

@@ -80,6 +80,9 @@ def main():
         "rbf_kuf_x6": lambda: ops.rbf_kuf_x6(X, Z, var, lsc, out=Kfr),
         "split_upper_x6": lambda: ops.split_upper_x6(LinvT[0], out=Tfr),
         "trsm_stats_x6": lambda: ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Afr, stats=st6),
+        "trsm_x6_nostats": lambda: ops._lib.call("mgp_trsm_stats_x6", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(),
+                                                 Kfr.numel(), M, N, q_mu.data_ptr(), K, K, Afr.data_ptr(),
+                                                 Afr.numel(), None, N, None, N, ops._stream()),
         "split_lower_x6": lambda: ops.split_lower_x6(q_sqrt, out=Lfr),
         "expert_cond_x6": lambda: ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmean=fm6, fvar=fv6),
         "gram_x6_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg),
