@@ -64,6 +64,7 @@ def test_golden_c2_shapes(device):
 
 @pytest.mark.parametrize("N,M,K,D,ls,S", [(8192, 256, 4, 2, 0.15, 25),      # BASELINE config 2
                                            (8192, 1024, 8, 8, 1.0, 25),      # config-3 shapes, N reduced
+                                           (4096, 2048, 16, 16, 2.0, 25),    # config-5 shapes, N reduced
                                            (1001, 33, 2, 3, 0.8, 7)])        # ragged sizes
 def test_elbo_configs(device, N, M, K, D, ls, S):
     X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)

@@ -69,7 +69,8 @@ def _dense(name, t, M):
 @pytest.mark.parametrize("N,M,K,D,ls,S,modified", [(1000, 25, 3, 1, 0.5, 25, False),
                                                     (2049, 64, 4, 2, 0.8, 7, False),
                                                     (1000, 25, 3, 1, 0.5, 25, True),
-                                                    (4096, 130, 3, 3, 1.0, 5, False)])
+                                                    (4096, 130, 3, 3, 1.0, 5, False),
+                                                    (2048, 2048, 16, 16, 2.0, 3, False)])   # config-5 shapes
 def test_elbo_and_grad(device, N, M, K, D, ls, S, modified):
     X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
     a_var = np.linspace(0.3, 0.9, K)[None, :] if modified else None

@@ -1,0 +1,37 @@
+"""K3 critical-path breakdown from in-kernel s_memtime stamps (GPU box only).
+Rebuilds libmgp_hip.so with -DMGP_DBG_STAMPS in this (scratch) tree, runs one
+batched Kuu Cholesky + inverse at M = 1024, batch 2, and prints per-step
+deltas (s_memtime ticks, 100 MHz) of the look-ahead workgroup:
+  0 start, 1 tiles loaded, 2 P_i stored, 3 update done, 4 staged, 5 panels
+  factored, 6 inverse done, 7 diag written."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from modulatedgps_amd import build as B  # noqa: E402
+
+B.build(extra_flags=["-DMGP_DBG_STAMPS"])
+import torch  # noqa: E402
+from modulatedgps_amd import _lib, ops  # noqa: E402
+
+dev = torch.device("cuda", 0)
+M = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+g = torch.Generator(device=dev).manual_seed(0)
+Z = torch.randn(M, 8, device=dev, generator=g)
+var = torch.tensor([0.5], device=dev)
+ls = torch.tensor([1.0], device=dev)
+for _ in range(3):
+    ops.kuu_potrf_trtri([Z, Z], [var, var], [ls, ls], 1e-6)
+torch.cuda.synchronize()
+lib = _lib.load()
+buf = (ctypes.c_ulonglong * (64 * 16))()
+lib.mgp_dbg_chol_stamps(buf)
+st = [[buf[j * 16 + k] for k in range(16)] for j in range(64)]
+steps = M // 64 - 1
+print("step  load  P_i  update  stage  panels  inverse  write  | next-step gap")
+for j in range(steps):
+    s = st[j]
+    d = [s[k + 1] - s[k] if s[k + 1] and s[k] else 0 for k in range(7)]
+    gap = (st[j + 1][0] - s[7]) if j + 1 < steps and st[j + 1][0] else 0
+    print(j, d[0], d[1], d[2], d[3], s[5] - s[4], s[6] - s[5], s[7] - s[6], "|", gap)
