@@ -86,14 +86,31 @@ __device__ __forceinline__ double input_elem(const CholArgs& a, int b, int64_t g
   return v;
 }
 
-// 64x64 tile (row-major f64, ld) -> LDS (ld LDT).
-__device__ __forceinline__ void tile_load(double* __restrict__ s, const double* __restrict__ g, int64_t ld) {
-  for (int idx = threadIdx.x; idx < CB * CB / 2; idx += kCholThreads) {
-    const int r = idx >> 5, c = (idx & 31) * 2;
-    const double2 v = *reinterpret_cast<const double2*>(g + (int64_t)r * ld + c);
-    s[r * LDT + c] = v.x;
-    s[r * LDT + c + 1] = v.y;
+// 64x64 f64 tile (row-major, ld) staged through registers: fetch issues all
+// eight 16-B loads per thread before any LDS store, so several tiles' loads
+// can be in flight together (fetch, fetch, ..., put, put).
+struct TileRegs {
+  double2 v[8];
+};
+__device__ __forceinline__ void tile_fetch(TileRegs& t, const double* __restrict__ g, int64_t ld) {
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
+    t.v[it] = *reinterpret_cast<const double2*>(g + (int64_t)r * ld + c);
   }
+}
+__device__ __forceinline__ void tile_put(double* __restrict__ s, const TileRegs& t) {
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
+    s[r * LDT + c] = t.v[it].x;
+    s[r * LDT + c + 1] = t.v[it].y;
+  }
+}
+__device__ __forceinline__ void tile_load(double* __restrict__ s, const double* __restrict__ g, int64_t ld) {
+  TileRegs t;
+  tile_fetch(t, g, ld);
+  tile_put(s, t);
 }
 
 // LDS tile -> float32 global, optionally transposed (dst[c][r] = s[r][c]),
@@ -243,7 +260,8 @@ __device__ __forceinline__ void blk_store(double* __restrict__ s, const doublex4
 // 16 panel entries of row r; square-root-free right-looking sweep whose column
 // broadcasts are readlanes from the owning lane (no LDS round trip on the
 // critical path).  Writes L's panel (zeros above the diagonal) and
-// col[16P + c] = 1 / L[16P + c][16P + c].
+// col[16P + c] = 1 / L[16P + c][16P + c].  (A division-free Bareiss-scaled
+// sweep was measured 18 % slower: the wave is issue-bound, not latency-bound.)
 template <int P>
 __device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __restrict__ col, int r, int& bad) {
   constexpr int C0 = 16 * P;
@@ -270,11 +288,11 @@ __device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __
 
 // Trailing update after panel P (all waves): W[I][J] -= L[I][panel] L[J][panel]^T
 // for the 16x16 blocks I >= J > P (lower triangle of blocks incl. the diagonal).
+// Block q of the NBLK goes to wave q % nw (waves w >= nw skip).
 template <int P>
-__device__ __forceinline__ void panel_update(double* __restrict__ sF) {
+__device__ __forceinline__ void panel_update(double* __restrict__ sF, int w, int nw = 4) {
   constexpr int NB = 3 - P, NBLK = NB * (NB + 1) / 2;
-  const int w = threadIdx.x >> 6;
-  for (int q = w; q < NBLK; q += 4) {
+  for (int q = w; q < NBLK; q += nw) {
     int bi = 0;
     while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
     const int bj = q - bi * (bi + 1) / 2;
@@ -285,90 +303,111 @@ __device__ __forceinline__ void panel_update(double* __restrict__ sF) {
   }
 }
 
+// X_pp = L_pp^-1 of diagonal block p (one wave; quad layout: lane = column
+// cc x row group g, DPP broadcast of the pivot row); needs col[16p ..].
+__device__ __forceinline__ void inv_diag_block(const double* __restrict__ sF, double* __restrict__ sX,
+                                               const double* __restrict__ col, int p, int lane) {
+  const int cc = lane >> 2, g = lane & 3;
+  const double* L = sF + 16 * p * LDT + 16 * p;
+  double x[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = (4 * g + k == cc) ? 1.0 : 0.0;
+#pragma unroll
+  for (int I = 0; I < 16; ++I) {
+    const int GI = I >> 2, KI = I & 3;
+    double xi = x[KI] * col[16 * p + I];
+    switch (GI) {  // compile-time after unrolling
+      case 0: xi = quad_bcast_f64<0>(xi); break;
+      case 1: xi = quad_bcast_f64<1>(xi); break;
+      case 2: xi = quad_bcast_f64<2>(xi); break;
+      default: xi = quad_bcast_f64<3>(xi); break;
+    }
+    if (g == GI) x[KI] = xi;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = 4 * g + k;
+      const double l = L[row * LDT + I];
+      x[k] = (row > I) ? fma(-l, xi, x[k]) : x[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sX[(16 * p + 4 * g + k) * LDT + 16 * p + cc] = x[k];
+}
+
+// X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj (one wave, f64 MFMA; the product's
+// accumulator registers are directly the B operand of the second product).
+__device__ __forceinline__ void inv_offdiag_block(const double* __restrict__ sF, double* __restrict__ sX, int i,
+                                                  int j, int lane) {
+  doublex4 y = {0.0, 0.0, 0.0, 0.0};
+  for (int k = j; k < i; ++k) blk_mma<false>(y, sF + 16 * i * LDT + 16 * k, sX + 16 * k * LDT + 16 * j, 1.0);
+  doublex4 xv = {0.0, 0.0, 0.0, 0.0};
+  const double* Xii = sX + 16 * i * LDT + 16 * i;
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const double av = -Xii[(lane & 15) * LDT + 4 * s4 + (lane >> 4)];
+    xv = __builtin_amdgcn_mfma_f64_16x16x4f64(av, y[s4], xv, 0, 0, 0);
+  }
+  blk_store(sX + 16 * i * LDT + 16 * j, xv);
+}
+
 // Factor the symmetric 64x64 tile in sF (lower part used) in place: sF <- L
 // (zeros above), sX <- L^-1 (zeros above).  Called by all 256 threads.
 //
 // Blocked in four 16-column panels: wave 0 factors a panel (register rows,
-// readlane broadcasts, no sqrt/division on the per-column chain), then the four
-// waves apply its rank-16 update to the trailing blocks on the f64 MFMA.
-// Inverse, by 16x16 blocks: wave p inverts L_pp (quad layout: lane = column x
-// row group, DPP broadcast of the pivot row), then the block diagonals
-// d = 1..3: X_{j+d,j} = -X_{j+d,j+d} sum_{k=j}^{j+d-1} L_{j+d,k} X_{k,j} on the
-// f64 MFMA (the product's accumulator registers are directly the B operand of
-// the second product).  Records the first non-positive pivot (LAPACK info,
-// 1-based, + gcol0).
+// readlane broadcasts, division-free chain), then the waves apply its rank-16
+// update to the trailing blocks on the f64 MFMA.  The inverse is built by the
+// idle waves while wave 0 runs the next panel: X_pp = L_pp^-1 as soon as panel
+// p is final, X_ij (i > j) = -X_ii sum_k L_ik X_kj as soon as its operands are:
+//   S0  w0 panel 0
+//   U0  update 0 (6 blocks, 4 waves)
+//   S1  w0 panel 1          | w1 X_00
+//   U1  update 1 (w0..w2)   | w3 zero the upper blocks of X
+//   S2  w0 panel 2          | w1 X_11
+//   U2  update 2 (w0)       | w1 X_10
+//   S3  w0 panel 3          | w1 X_22
+//   I1  w0 X_33             | w1 X_21 | w2 X_20
+//   I2  w0 X_32             | w1 X_31 | w2 X_30
+// Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int bad = 0;
   if (w == 0) panel_factor<0>(sF, col, lane, bad);
   __syncthreads();
-  panel_update<0>(sF);
+  panel_update<0>(sF, w);
   __syncthreads();
   if (w == 0) panel_factor<1>(sF, col, lane, bad);
+  else if (w == 1) inv_diag_block(sF, sX, col, 0, lane);
   __syncthreads();
-  panel_update<1>(sF);
+  if (w < 3) {
+    panel_update<1>(sF, w, 3);
+  } else {
+    for (int q = 0; q < 6; ++q) {  // upper blocks (i < j) of X are zero
+      const int i = q < 3 ? 0 : (q < 5 ? 1 : 2), j = q < 3 ? q + 1 : (q < 5 ? q - 1 : 3);
+      blk_store(sX + 16 * i * LDT + 16 * j, doublex4{0.0, 0.0, 0.0, 0.0});
+    }
+  }
   __syncthreads();
   if (w == 0) panel_factor<2>(sF, col, lane, bad);
+  else if (w == 1) inv_diag_block(sF, sX, col, 1, lane);
   __syncthreads();
-  panel_update<2>(sF);
+  if (w == 0) panel_update<2>(sF, 0, 1);
+  else if (w == 1) inv_offdiag_block(sF, sX, 1, 0, lane);
   __syncthreads();
   if (w == 0) {
     panel_factor<3>(sF, col, lane, bad);
     if (bad && lane == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
+  } else if (w == 1) {
+    inv_diag_block(sF, sX, col, 2, lane);
   }
   __syncthreads();
   STAMP((int)(gcol0 / CB) - 1, 5);
-  // ---- inverse: diagonal blocks (wave p -> X_pp), upper blocks zero
-  {
-    const int p = w, cc = lane >> 2, g = lane & 3;
-    const double* L = sF + 16 * p * LDT + 16 * p;
-    double x[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = (4 * g + k == cc) ? 1.0 : 0.0;
-#pragma unroll
-    for (int I = 0; I < 16; ++I) {
-      const int GI = I >> 2, KI = I & 3;
-      double xi = x[KI] * col[16 * p + I];
-      switch (GI) {  // compile-time after unrolling
-        case 0: xi = quad_bcast_f64<0>(xi); break;
-        case 1: xi = quad_bcast_f64<1>(xi); break;
-        case 2: xi = quad_bcast_f64<2>(xi); break;
-        default: xi = quad_bcast_f64<3>(xi); break;
-      }
-      if (g == GI) x[KI] = xi;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int row = 4 * g + k;
-        const double l = L[row * LDT + I];
-        x[k] = (row > I) ? fma(-l, xi, x[k]) : x[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sX[(16 * p + 4 * g + k) * LDT + 16 * p + cc] = x[k];
-    // upper blocks (i < j) of X are zero: wave p clears row block p to its right
-    for (int j = p + 1; j < 4; ++j) blk_store(sX + 16 * p * LDT + 16 * j, doublex4{0.0, 0.0, 0.0, 0.0});
-  }
+  if (w == 0) inv_diag_block(sF, sX, col, 3, lane);
+  else if (w == 1) inv_offdiag_block(sF, sX, 2, 1, lane);
+  else if (w == 2) inv_offdiag_block(sF, sX, 2, 0, lane);
   __syncthreads();
-  // ---- block diagonals d = 1..3
-#pragma unroll
-  for (int d = 1; d < 4; ++d) {
-    if (w < 4 - d) {
-      const int j = w, i = j + d;
-      doublex4 y = {0.0, 0.0, 0.0, 0.0};
-      for (int k = j; k < i; ++k) blk_mma<false>(y, sF + 16 * i * LDT + 16 * k, sX + 16 * k * LDT + 16 * j, 1.0);
-      // X_ij = -X_ii Y: register s of y is the B operand of k-step s
-      doublex4 xv = {0.0, 0.0, 0.0, 0.0};
-      const double* Xii = sX + 16 * i * LDT + 16 * i;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const double av = -Xii[(lane & 15) * LDT + 4 * s4 + (lane >> 4)];
-        xv = __builtin_amdgcn_mfma_f64_16x16x4f64(av, y[s4], xv, 0, 0, 0);
-      }
-      blk_store(sX + 16 * i * LDT + 16 * j, xv);
-    }
-    __syncthreads();
-  }
+  if (w < 3) inv_offdiag_block(sF, sX, 3, 2 - w, lane);
+  __syncthreads();
 }
 
 // Write the factored diagonal tile j: L block (f32, guarded to M; optional) and D_j (f64).
@@ -383,8 +422,7 @@ __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, cons
 __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   __shared__ double s1[CB * LDT], s2[CB * LDT], col[CB];
   const int b = blockIdx.y;
-  const int ntiles = a.nb * a.nb;
-  if ((int)blockIdx.x == ntiles) {  // factor tile (0, 0) straight from the input
+  if (blockIdx.x == 0) {  // factor tile (0, 0) straight from the input (dispatched first)
     if (threadIdx.x == 0) a.info[b] = 0;
     for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
       const int r = idx >> 6, c = idx & 63;
@@ -396,7 +434,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     write_diag(a, b, 0, s1, s2);
     return;
   }
-  const int bi = blockIdx.x / a.nb, bl = blockIdx.x % a.nb;
+  const int bi = (blockIdx.x - 1) / a.nb, bl = (blockIdx.x - 1) % a.nb;
   const int64_t r0 = (int64_t)bi * CB, c0 = (int64_t)bl * CB;
   if (bl <= bi) {
     double* W = ws_W(a, b) + r0 * a.Mp + c0;
@@ -460,9 +498,15 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     const int i = j + 1 + ai, l = j + 1 + bl_;
     const bool la = (ai == 0 && bl_ == 0);
     if (la) STAMP(j, 0);
-    tile_load(s1, Wt(i, j), Mp);
-    tile_load(sD, ws_D(a, b, j), CB);
-    if (l != i) tile_load(s2, Wt(l, j), Mp);
+    TileRegs r1, rD, r2;
+    Quad u;
+    tile_fetch(r1, Wt(i, j), Mp);
+    tile_fetch(rD, ws_D(a, b, j), CB);
+    if (l != i) tile_fetch(r2, Wt(l, j), Mp);
+    quad_from_global(u, Wt(i, l), Mp);  // the updated tile, in flight with the operands
+    tile_put(s1, r1);
+    tile_put(sD, rD);
+    if (l != i) tile_put(s2, r2);
     __syncthreads();
     if (la) STAMP(j, 1);
     Quad pi = quad_zero(), pl = quad_zero();
@@ -478,8 +522,6 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
       tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
                      (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
     }
-    Quad u;
-    quad_from_global(u, Wt(i, l), Mp);
     tile_mma<false, true>(u, s1, (l == i) ? s1 : s2, -1.0);  // W_il -= P_i P_l^T
     if (ai == 0 && bl_ == 0) {  // look-ahead: factor the next diagonal tile
       __syncthreads();
@@ -502,9 +544,17 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   // ------------------ forward-substitution tile (i, c), i > j, c <= j
   const int x = idx - nU;
   const int i = j + 1 + x / (j + 1), c = x % (j + 1);
-  tile_load(s1, Wt(i, j), Mp);
-  tile_load(sD, ws_D(a, b, j), CB);
-  if (c < j) tile_load(s2, Bt(j, c), Mp);
+  TileRegs r1, rD, r2;
+  Quad u = quad_zero();
+  tile_fetch(r1, Wt(i, j), Mp);
+  tile_fetch(rD, ws_D(a, b, j), CB);
+  if (c < j) {
+    tile_fetch(r2, Bt(j, c), Mp);
+    quad_from_global(u, Bt(i, c), Mp);
+  }
+  tile_put(s1, r1);
+  tile_put(sD, rD);
+  if (c < j) tile_put(s2, r2);
   __syncthreads();
   Quad pi = quad_zero(), xq = quad_zero();
   tile_mma<false, true>(pi, s1, sD, 1.0);                   // P_i
@@ -515,8 +565,6 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   __syncthreads();
   const double* sx = (c < j) ? s2 : sD;                     // X_jj = D_j
   if (i == j + 1) store_linvT(c, sx);
-  Quad u = quad_zero();
-  if (c < j) quad_from_global(u, Bt(i, c), Mp);
   tile_mma<false, false>(u, s1, sx, -1.0);                  // B_ic -= P_i X_jc
   quad_to_global(Bt(i, c), Mp, u);
 }

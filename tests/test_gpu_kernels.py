@@ -116,6 +116,31 @@ def test_kuu_factorisation_matches_float64(device):
         assert normwise(to_np(LinvT[b]).T, Li) < 1e-6
 
 
+@pytest.mark.parametrize("M,dup", [(1024, 0.0), (1024, 1e-3), (700, 1e-2)])
+def test_kuu_factorisation_ill_conditioned(device, M, dup):
+    """K3 on badly conditioned Kuu (inducing points with near-duplicates, cond up
+    to ~1e9): L and L^-1 against float64 LAPACK, to float32 output rounding
+    amplified by at most cond(L) eps64."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(M)
+    Z = rng.standard_normal((M, 4))
+    if dup:
+        Z[1::7] = Z[0::7][:len(Z[1::7])] + dup * rng.standard_normal(Z[1::7].shape)
+    Z = Z.astype(np.float32)
+    L, LinvT, info = ops.kuu_potrf_trtri([_t(Z, device), _t(Z, device)], [_t([0.5], device)] * 2,
+                                         [_t([1.0], device)] * 2, 1e-6, want_L=True)
+    assert (info.cpu() == 0).all()
+    Kuu = R.rbf_Kuu(Z.astype(np.float64), 0.5, np.array([1.0]))
+    Lr = np.linalg.cholesky(Kuu)
+    Li = sla.solve_triangular(Lr, np.eye(M), lower=True)
+    condK = np.linalg.cond(Kuu)
+    for b in range(2):
+        eL, eI = normwise(to_np(L[b]), Lr), normwise(to_np(LinvT[b]).T, Li)
+        print(f"cond(Kuu)={condK:.2e} L {eL:.2e} Linv {eI:.2e}")
+        assert eL < 1e-6 + condK * 1e-15
+        assert eI < 1e-6 + condK * 1e-15
+
+
 def test_conditional_ignores_upper_triangle(device):
     """band_part(q_sqrt, -1, 0): garbage above the diagonal must not matter."""
     from modulatedgps_amd import ops
