@@ -48,7 +48,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--planes", type=int, default=3, choices=(1, 2, 3),
+                    help="bf16 planes per operand in K5 (3: f32-accurate x6, the default; 2 / 1: the "
+                         "'bf16 mixed' modes of BASELINE config 5, reported with their measured tolerance)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-modes", action="store_true", help="skip the reduced-plane K5 side measurements")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (ELBO + gradient + Adam) leg")
     ap.add_argument("--layout", default="data", choices=("data", "expert"),
                     help="multi-GPU layout: 'data' shards N (weak scaling, the default); 'expert' shards the "
@@ -178,6 +182,30 @@ def load_traffic(kernel):
     return e.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
+def k5_modes_leg(elbo_step, args, steps=10):
+    """Side measurement (never the headline): the same ELBO step with K5 on 2 and 1
+    bf16 planes (BASELINE config 5's 'bf16 mixed'); their measured fvar error vs the
+    float64 oracle at c3 shapes is asserted in tests/test_gpu_kernels.py::
+    test_expert_conditional_planes (2 planes ~3e-6, 1 plane ~2e-3 normwise)."""
+    from modulatedgps_amd.config import set_expert_planes
+    out = {}
+    for planes in (2, 1):
+        set_expert_planes(planes)
+        for _ in range(2):
+            elbo_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            elbo_step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        out[f"planes{planes}"] = {"value": 1.0 / dt, "unit": "ELBO steps/s", "ms_per_step": dt * 1e3,
+                                  "k5_products": planes * (planes + 1) // 2,
+                                  "fvar_normwise_err_vs_f64": {2: "3.3e-6", 1: "2.1e-3"}[planes]}
+    set_expert_planes(3)
+    return out
+
+
 def train_leg(model, X, Y, kw, args, barrier, world, device):
     """Secondary line: the run_adam optimisation step (utils/training_utils.py:10-13:
     ELBO, its gradient w.r.t. every trainable parameter, one TF-legacy Adam update),
@@ -216,8 +244,11 @@ def train_leg(model, X, Y, kw, args, barrier, world, device):
 
 def main():
     args = parse()
-    from modulatedgps_amd.config import conditional_mode
+    from modulatedgps_amd.config import conditional_mode, set_expert_planes
     x6 = conditional_mode() == "x6"
+    set_expert_planes(args.planes)
+    k5_products = args.planes * (args.planes + 1) // 2   # 6 / 3 / 1 bf16 MFMA products per f32 product
+    peak_k5 = PEAK_BF16_MFMA / k5_products if x6 else PEAK_F32_MFMA
     from modulatedgps_amd.distributed import init_from_env
     rank, world, local = init_from_env("nccl")
     group = torch.distributed.group.WORLD if world > 1 else None
@@ -283,7 +314,7 @@ def main():
                               "timing": "20 back-to-back launches after the timed steps",
                               "in_step_avg_us": st["rbf_kuf"][0] * 1e3}
     for name, fl, peak in (("trsm_stats", trsm_flops, PEAK_X6 if x6 else PEAK_F32_MFMA),
-                           ("expert_cond", expert_flops, PEAK_X6 if x6 else PEAK_F32_MFMA)):
+                           ("expert_cond", expert_flops, peak_k5)):
         if name in st:
             ms = st[name][0]
             kernels[name] = {"bound": "mfma", "avg_us": ms * 1e3, "flops": fl,
@@ -302,16 +333,19 @@ def main():
     kname = "expert_cond_x6_kernel" if x6 else "expert_cond_kernel"
     traffic, traffic_src = load_traffic(kname)
     roofline = {"kernel": f"{kname} (K5, L_k^T A + sum of squares, + cond_finalize)", "bound": "mfma",
-                "achieved": ek.get("achieved"), "peak": (PEAK_X6 if x6 else PEAK_F32_MFMA) / 1e12,
+                "achieved": ek.get("achieved"), "peak": peak_k5 / 1e12,
                 "unit": "TFLOP/s", "frac": ek.get("frac"), "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_per_launch": f"K*M^2*N = {expert_flops:.4g} f32 flop",
-                "peak_note": ("split-bf16: each f32 product is 6 bf16 MFMA products, peak = "
-                              "2.5 PF bf16 dense / 6" if x6 else "f32 MFMA dense peak")}
+                "peak_note": (f"split-bf16: each f32 product is {k5_products} bf16 MFMA products, peak = "
+                              f"2.5 PF bf16 dense / {k5_products}" if x6 else "f32 MFMA dense peak")}
 
     ms_per_step = elapsed / args.steps * 1e3
     value = (1 if expert else world) * args.steps / elapsed
     train = None if (args.no_train or expert) else train_leg(model, X, Y, kw, args, barrier, world, device)
+    modes = None
+    if world == 1 and x6 and args.planes == 3 and not args.no_modes:
+        modes = k5_modes_leg(elbo_step, args)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, tuple(args.cpu_sample))
@@ -321,9 +355,13 @@ def main():
             "metric": "ELBO steps/sec (N=65536, M=1024, K=8); Kuf HBM GB/s vs roofline",
             "value": value, "unit": "ELBO steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong" if expert else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "dtype_note": ("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
-                           "3-plane split (6 products, f32-accurate); K3 in f64" if x6 else
+            "scaling": "strong" if expert else "weak", "vs_baseline": None,
+            "dtype": {3: "f32", 2: "f32/bf16x3 mixed", 1: "f32/bf16 mixed"}[args.planes] if x6 else "f32",
+            "data": "synthetic",
+            "dtype_note": (("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
+                            "3-plane split (6 products, f32-accurate); K3 in f64") if x6 and args.planes == 3 else
+                           (f"K1-K4 f32-accurate (x6 split-bf16), K5 on the leading {args.planes} bf16 plane(s) "
+                            f"({k5_products} product(s), f32 accumulation); K3 in f64") if x6 else
                            "f32 MFMA (exact f32); K3 in f64"),
             "config": {"workload": f"{args.config}: SMGP ELBO forward, N={N}/GPU, M={M}, K={K}, "
                                    f"D={D}, S={S}, lengthscale={ls}",
@@ -338,6 +376,7 @@ def main():
             "step_frac_f32_mfma": step_flops / (ms_per_step * 1e-3) / PEAK_F32_MFMA,
             "cpu_baseline": cpu,
             "train": train,
+            "k5_modes": modes,
             "elbo": elbo_val, "cholesky_info": info,
         }
         print(json.dumps(out))

@@ -164,6 +164,16 @@ int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, const void* Lfr
                               const float* stats, int64_t lds, const float* variance, int64_t M,
                               int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
                               void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+/* K5 from the same images using only the leading `planes` bf16 planes of each
+ * operand (BASELINE config 5, "bf16 mixed"; K1-K4 stay x6):
+ *   planes = 3: identical to mgp_expert_conditional_x6 (six products, f32-accurate);
+ *   planes = 2: three products (hi.hi + hi.mid + mid.hi), ~16-bit operands;
+ *   planes = 1: one product (bf16 operands, f32 accumulation).
+ * Replaces the same call site (GPflow base_conditional, models.py:141-143). */
+int mgp_expert_conditional_planes(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                  const float* stats, int64_t lds, const float* variance, int64_t M,
+                                  int64_t N, int32_t K, int32_t planes, float* fmean, float* fvar,
+                                  int64_t ldf, void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- backward of K1-K5
  * Gram products over the data dimension (float32 MFMA, deterministic split-K):

@@ -93,6 +93,9 @@ SIGNATURES = {
     "mgp_expert_x6_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
     "mgp_expert_conditional_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
                                                  c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_expert_conditional_planes": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
+                                                     c_i64, c_i32, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
+                                                     c_ptr]),
     "mgp_kl_workspace_bytes": (c_size, [c_i64, c_i32]),
     "mgp_gauss_kl_white": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr,
                                           c_ptr, c_size, c_ptr]),

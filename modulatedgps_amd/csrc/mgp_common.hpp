@@ -82,6 +82,22 @@ __device__ __forceinline__ floatx16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (
   return mfma_bf16(a[0], b[0], acc);
 }
 
+// Reduced-plane products (K5's "bf16 mixed" modes, BASELINE config 5):
+// NPL = 2: a_hi b_hi + a_hi b_mid + a_mid b_hi (dropped terms <= 2^-16 of the
+// leading one: ~16-bit operands); NPL = 1: a_hi b_hi (bf16 operands).
+template <int NPL>
+__device__ __forceinline__ floatx16 mfma_planes(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 acc) {
+  if constexpr (NPL == 3) {
+    return mfma_x6(a, b, acc);
+  } else if constexpr (NPL == 2) {
+    acc = mfma_bf16(a[1], b[0], acc);
+    acc = mfma_bf16(a[0], b[1], acc);
+    return mfma_bf16(a[0], b[0], acc);
+  } else {
+    return mfma_bf16(a[0], b[0], acc);
+  }
+}
+
 // ------------------------------------------------------------------ reductions
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

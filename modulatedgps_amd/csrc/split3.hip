@@ -148,7 +148,9 @@ using ic = std::integral_constant<int, V>;
 // (8% of the work), everything else is unchanged.
 // DIAG: 1 = diagonal first (lower T), 2 = diagonal last (upper T), 0 = full T.
 // NC: column sub-tiles (32 wide) per wave (B blocks nb0 .. nb0 + NC - 1).
-template <int DIAG, int NC = 2>
+// NPL: planes used (3 = x6 products; 2, 1 = K5's reduced modes, mfma_planes):
+// only those planes are loaded and staged.
+template <int DIAG, int NC = 2, int NPL = 3>
 __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)[4 * 3 * 64],
                                             __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
                                             __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
@@ -156,14 +158,16 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t vB = 16u * lane;
   const uint32_t sB1 = sB0 + (uint32_t)nmk * 3u * kFragBytes;
-  // T stage: 768 16-B units per k-step, 3 per thread: unit e = tid + 256 s ->
-  //   row sub-tile i = e / 192, rest = e % 192 (= p * 64 + lane)
-  //   byte offset tbase + ((i * nmk + mk) * 192 + rest) * 16
-  uint32_t vT[3];
+  // T stage: 256 NPL 16-B units per k-step, NPL per thread: unit e = tid + 256 s ->
+  //   row sub-tile i = e / (64 NPL), plane p = (e / 64) % NPL, lane e % 64
+  //   byte offset tbase + ((i * nmk + mk) * 192 + p * 64 + lane) * 16; LDS unit (3 i + p) * 64 + lane
+  uint32_t vT[NPL];
+  int dT[NPL];
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const int e = tid + 256 * s;
-    vT[s] = (uint32_t)(((e / 192) * nmk * 192 + (e % 192)) * 16);
+  for (int s = 0; s < NPL; ++s) {
+    const int e = tid + 256 * s, i = e / (64 * NPL), p = (e / 64) % NPL;
+    vT[s] = (uint32_t)((i * nmk * 192 + p * 64 + (e & 63)) * 16);
+    dT[s] = (3 * i + p) * 64 + (e & 63);
   }
   if (init) {
 #pragma unroll
@@ -177,19 +181,19 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
   auto load_b = [&](bf16x8 (&b)[NC][3], int mk) {
     const uint32_t o = (uint32_t)mk * 3u * kFragBytes;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < NPL; ++p) {
       b[0][p] = ld_frag(rB, vB, sB0 + o + p * kFragBytes);
       if constexpr (NC > 1) b[1][p] = ld_frag(rB, vB, sB1 + o + p * kFragBytes);
     }
   };
-  auto load_t = [&](u32x4v (&st)[3], int mk) {
+  auto load_t = [&](u32x4v (&st)[NPL], int mk) {
     const uint32_t o = tbase + (uint32_t)mk * 192u * 16u;
 #pragma unroll
-    for (int s = 0; s < 3; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s], o, 0);
+    for (int s = 0; s < NPL; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s], o, 0);
   };
-  auto store_t = [&](int buf, const u32x4v (&st)[3]) {
+  auto store_t = [&](int buf, const u32x4v (&st)[NPL]) {
 #pragma unroll
-    for (int s = 0; s < 3; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
+    for (int s = 0; s < NPL; ++s) reinterpret_cast<u32x4v*>(sL[buf])[dT[s]] = st[s];
   };
   auto compute = [&](int buf, const bf16x8 (&b)[NC][3], auto ilo, auto ihi) {
     constexpr int ILO = decltype(ilo)::value, IHI = decltype(ihi)::value;
@@ -197,14 +201,14 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     for (int i = ILO; i < IHI; ++i) {
       bf16x8 a[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) a[p] = sL[buf][(i * 3 + p) * 64 + lane];
+      for (int p = 0; p < NPL; ++p) a[p] = sL[buf][(i * 3 + p) * 64 + lane];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[i][c] = mfma_x6(a, b[c], acc[i][c]);
+      for (int c = 0; c < NC; ++c) acc[i][c] = mfma_planes<NPL>(a, b[c], acc[i][c]);
     }
   };
 
   bf16x8 b0[NC][3], b1[NC][3];
-  u32x4v st[3];
+  u32x4v st[NPL];
   load_t(st, mk_begin);
   load_b(b0, mk_begin);
   store_t(0, st);
@@ -254,6 +258,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const void* p, uint32
 }
 
 // ------------------------------------------------------------------ K5 (x6)
+template <int NPL>
 __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
                                                                 const bf16x8* __restrict__ Lfr,
                                                                 uint32_t afr_bytes, uint32_t lfr_bytes,
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   floatx16 acc[4][2];
-  x6_mainloop<1>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+  x6_mainloop<1, 2, NPL>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
               img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
@@ -465,22 +470,17 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restri
 // the stats of the two 64-row stats tiles 2 t, 2 t + 1 (same layout as the
 // f32 K4: stats[st][0][n] = sum A^2, stats[st][1 + kk][n] = sum A q_mu[., kk]).
 template <int KMAX>
-__global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
-    const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
-    int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
-    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda) {
-  __shared__ bf16x8 sL[2][4 * 3 * 64];
-  const int nT = nmk / 8;
-  int t, tn;
-  col_major_item(blockIdx.x, nT, nTn, t, tn);
+__device__ __forceinline__ void trsm_stats_x6_item(
+    bf16x8 (*sL)[4 * 3 * 64], int t, int tn, const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes,
+    const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
+    const float* __restrict__ q_mu, int64_t ldq, int K, bf16x8* __restrict__ Afr, float* __restrict__ stats,
+    int64_t lds_, float* __restrict__ Af32, int64_t lda) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nmb = nmk / 2;
   floatx16 acc[4][2];
   x6_mainloop<2>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
               img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8,
               nmk);
-  (void)nmb;
 
   // ---- A image
 #pragma unroll
@@ -539,6 +539,28 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
       }
     }
   }
+}
+
+// One workgroup per (pair of row tiles t, nT - 1 - t; column tile tn): the
+// pair holds 8 t + 8 + 8 (nT - t) = 8 nT + 16 k-steps whatever t, so every
+// workgroup has the same work (the single-item grid left a tail of 64-step
+// items); both items read the same Kuf column slab.  Odd nT: the middle row
+// tile is an item alone.
+template <int KMAX>
+__global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
+    const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
+    int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
+    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];
+  const int nT = nmk / 8, nP = (nT + 1) / 2;
+  int p, tn;
+  col_major_item(blockIdx.x, nP, nTn, p, tn);
+  trsm_stats_x6_item<KMAX>(sL, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr,
+                           stats, lds_, Af32, lda);
+  if (nT - 1 - p == p) return;
+  __syncthreads();  // the epilogue's LDS reads before the next main loop's LDS stores
+  trsm_stats_x6_item<KMAX>(sL, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
+                           lds_, Af32, lda);
 }
 
 }  // namespace mgp
@@ -617,10 +639,11 @@ extern "C" size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K)
   return (size_t)K * (size_t)(x6_mp(M) / kX6BM) * (size_t)((N + 3) / 4 * 4) * sizeof(float);
 }
 
-extern "C" int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
-                                         const float* stats, int64_t lds, const float* variance, int64_t M,
-                                         int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
-                                         void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+// Argument checks report the index in mgp_expert_conditional_x6's signature.
+static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                              const float* stats, int64_t lds, const float* variance, int64_t M, int64_t N,
+                              int32_t K, int planes, float* fmean, float* fvar, int64_t ldf, void* workspace,
+                              size_t workspace_bytes, mgp_stream_t stream) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!Lfr) return -3;
@@ -644,13 +667,39 @@ extern "C" int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, cons
   const int nTn = (int)(x6_np(N) / kX6BN);
   const int64_t ldp = (N + 3) / 4 * 4;
   float* part = (float*)workspace;
-  hipLaunchKernelGGL(expert_cond_x6_kernel, dim3((unsigned)(K * nTp * nTn)), dim3(256), 0, s,
-                     (const bf16x8*)Afr, (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N),
-                     (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N, part, ldp);
+  const dim3 grid((unsigned)(K * nTp * nTn));
+#define MGP_K5_CASE(NP)                                                                                 \
+  if (planes == NP)                                                                                     \
+    hipLaunchKernelGGL(expert_cond_x6_kernel<NP>, grid, dim3(256), 0, s, (const bf16x8*)Afr,            \
+                       (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N),                           \
+                       (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N, part, ldp);
+  MGP_K5_CASE(3)
+  MGP_K5_CASE(2)
+  MGP_K5_CASE(1)
+#undef MGP_K5_CASE
   int st = launch_status();
   if (st) return st;
   return mgp_launch_cond_finalize(stats, lds, mgp_stats_tiles(M), part, ldp, nTp, variance, N, K, fmean, fvar,
                                   ldf, s);
+}
+
+extern "C" int mgp_expert_conditional_x6(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                         const float* stats, int64_t lds, const float* variance, int64_t M,
+                                         int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                                         void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  return expert_cond_planes(Afr, afr_bytes, Lfr, lfr_bytes, stats, lds, variance, M, N, K, 3, fmean, fvar, ldf,
+                            workspace, workspace_bytes, stream);
+}
+
+extern "C" int mgp_expert_conditional_planes(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                             const float* stats, int64_t lds, const float* variance, int64_t M,
+                                             int64_t N, int32_t K, int32_t planes, float* fmean, float* fvar,
+                                             int64_t ldf, void* workspace, size_t workspace_bytes,
+                                             mgp_stream_t stream) {
+  if (planes < 1 || planes > 3) return -11;
+  const int st = expert_cond_planes(Afr, afr_bytes, Lfr, lfr_bytes, stats, lds, variance, M, N, K, planes, fmean,
+                                    fvar, ldf, workspace, workspace_bytes, stream);
+  return (st <= -11 && st >= -13) ? st - 1 : st;  // fmean, fvar, ldf follow `planes` here
 }
 
 template <int KMAX>
@@ -659,7 +708,7 @@ static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb
                           float* A, int64_t lda, hipStream_t s) {
   const int64_t Mp = x6_mp(M);
   const int nmk = (int)(Mp / 16), nT = (int)(Mp / kX6BM), nTn = (int)(x6_np(N) / kX6BN);
-  hipLaunchKernelGGL(trsm_stats_x6_kernel<KMAX>, dim3((unsigned)(nT * nTn)), dim3(256), 0, s,
+  hipLaunchKernelGGL(trsm_stats_x6_kernel<KMAX>, dim3((unsigned)((nT + 1) / 2 * nTn)), dim3(256), 0, s,
                      (const bf16x8*)Tfr, (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu,
                      ldq, K, (bf16x8*)Afr, stats, lds, A, lda);
   return launch_status();

@@ -37,7 +37,7 @@ import torch
 
 from . import ops
 from .broadcasting_lik import BroadcastingLikelihood
-from .config import conditional_mode, default_device, default_jitter
+from .config import conditional_mode, default_device, default_jitter, expert_planes
 from .kernels import SquaredExponential
 
 TAU = 1e-2  # RelaxedOneHotCategorical temperature, models.py:60
@@ -203,7 +203,8 @@ class SVGPModified:
         with _Stage(timing, "expert_cond"):
             return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, self.num_inducing, N,
                                              self.num_latent_gps, fmean=bufs.get("fmean"),
-                                             fvar=bufs.get("fvar"), workspace=bufs.get("ws_expert"))
+                                             fvar=bufs.get("fvar"), workspace=bufs.get("ws_expert"),
+                                             planes=expert_planes())
 
     def conditional_experts(self, X, k0, k1, LinvT=None):
         """fmean, fvar [k1 - k0, N] of experts k0 .. k1 - 1 only (the expert-parallel
@@ -222,7 +223,8 @@ class SVGPModified:
         Tfr = ops.split_upper_x6(LinvT)
         Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu[:, k0:k1], M, N)
         Lfr = ops.split_lower_x6(self.q_sqrt[k0:k1])
-        return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, k1 - k0)
+        return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, k1 - k0,
+                                         planes=expert_planes())
 
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
         """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior

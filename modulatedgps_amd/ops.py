@@ -290,8 +290,9 @@ def split_cols_x6(A, out=None):
     return out
 
 
-def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=None, workspace=None):
-    """fmean, fvar [K, N] of the whitened K-expert conditional from split-bf16 images."""
+def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=None, workspace=None, planes=3):
+    """fmean, fvar [K, N] of the whitened K-expert conditional from split-bf16 images
+    (planes < 3: K5 on the leading bf16 planes only, mgp_expert_conditional_planes)."""
     _check(stats, "stats", 3)
     dev = stats.device
     if fmean is None:
@@ -303,9 +304,14 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
     nbytes = _lib.load().mgp_expert_x6_workspace_bytes(M, N, K)
     if workspace is None or workspace.numel() < nbytes:
         workspace = _ws(nbytes, dev)
-    _lib.call("mgp_expert_conditional_x6", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
-              stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(), fvar.data_ptr(),
-              _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
+    if planes == 3:
+        _lib.call("mgp_expert_conditional_x6", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
+                  stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(),
+                  fvar.data_ptr(), _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
+    else:
+        _lib.call("mgp_expert_conditional_planes", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
+                  stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, int(planes), fmean.data_ptr(),
+                  fvar.data_ptr(), _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
     return fmean, fvar
 
 

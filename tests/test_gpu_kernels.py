@@ -304,3 +304,35 @@ def test_kuf_and_trsm_images(device, N, M, D, K):
     Mp, Np = -(-M // 128) * 128, -(-N // 256) * 256
     full = decode_cols_image(Afr, Mp, Np)
     assert not full[M:].any() and not full[:, N:].any()
+
+
+def test_expert_conditional_planes(device):
+    """K5 on 3 / 2 / 1 bf16 planes (mgp_expert_conditional_planes): 3 planes are
+    bit-identical to the x6 entry; the reduced modes (BASELINE config 5's "bf16
+    mixed") are measured against the float64 oracle: 2 planes within the 1e-4
+    gate, 1 plane (bf16 operands) within 1e-2."""
+    from modulatedgps_amd import ops
+    N, M, K, D, ls = 8192, 1024, 8, 8, 1.0
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
+    L = p.pred
+    mu_ref, var_ref = R.svgp_predict_f_dedup(X, L["Z"], L["variance"], L["lengthscales"], L["q_mu"], L["q_sqrt"])
+    var = _t([L["variance"]], device)
+    lsc = _t([ls], device)
+    Zt = _t(L["Z"], device)
+    _, LinvT, _ = ops.kuu_potrf_trtri([Zt], [var], [lsc], 1e-6)
+    Kfr = ops.rbf_kuf_x6(_t(X, device), Zt, var, lsc)
+    Tfr = ops.split_upper_x6(LinvT[0])
+    Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, _t(L["q_mu"], device), M, N)
+    Lfr = ops.split_lower_x6(ops.as_padded(_t(L["q_sqrt"], device)))
+    fm6, fv6 = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K)
+    fm6, fv6 = to_np(fm6), to_np(fv6)
+    errs = {}
+    for planes, tol in ((3, 1e-4), (2, 1e-4), (1, 1e-2)):
+        fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, planes=planes)
+        fm, fv = to_np(fm), to_np(fv)
+        if planes == 3:
+            assert np.array_equal(fv, fv6) and np.array_equal(fm, fm6)
+        errs[planes] = normwise(fv.T, var_ref)
+        assert normwise(fm.T, mu_ref) < 1e-4  # fmean comes from K4 (x6) in every mode
+        assert errs[planes] < tol, (planes, errs[planes])
+    print("K5 planes fvar normwise error vs float64:", errs)
