@@ -10,4 +10,4 @@ tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 tail -c 300 gpurun_out/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
-ONLY=${ONLY:-expert_cond_x6,trsm_stats_x6,rbf_kuf_x6} bash tools/pmc_pass.sh
+ONLY=${ONLY:-} bash tools/pmc_pass.sh
