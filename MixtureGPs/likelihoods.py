@@ -1,2 +1,3 @@
-"""Drop-in for MixtureGPs/likelihoods.py (GaussianModified)."""
-from modulatedgps_amd.likelihoods import GaussianModified  # noqa: F401
+"""Drop-in for MixtureGPs/likelihoods.py (GaussianModified), plus the GPflow
+MultiClass / RobustMax likelihood the multiclass demos build from gpflow.likelihoods."""
+from modulatedgps_amd.likelihoods import GaussianModified, MultiClass, RobustMax  # noqa: F401

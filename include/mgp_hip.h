@@ -331,7 +331,42 @@ int mgp_predict_samples(const float* mu_f, const float* var_f, const float* mu_a
  * mgp_elbo_terms draws them in Philox mode.  Either pointer may be NULL. */
 int mgp_philox_noise(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S, float* z,
                      float* u, mgp_stream_t stream);
-/* Same, stream-2 normals (the z of mgp_predict_samples). */
+/* ---------------------------------------------------------------- MultiClass likelihood
+ * GPflow 2.7.0 likelihoods.MultiClass(num_classes = K, invlink = RobustMax(K, epsilon))
+ * as the pred likelihood (demos/demo_tf2_modified_multiclass.py:43-45, reached
+ * through BroadcastingLikelihood, broadcasting_lik.py:19-37,39-46):
+ *   p_i(n) = RobustMax.prob_is_largest(i, mu_n, var_n)  (20-point Gauss-Hermite)
+ *   ve_n   = p_y log(1 - eps) + (1 - p_y) log(eps / (K - 1)),  y = (int) Y[n]
+ * The var-exp is one value per point, multiplied by W and summed over K as the
+ * reference does (models.py:65-67).  Arguments as the Gaussian entries with
+ * lik_var replaced by epsilon (0 < eps < 1, K >= 2); assign_lik_var != NULL
+ * selects SMGPModified (its assign layer keeps the Gaussian likelihood).  The
+ * backward has no likelihood-variance gradient (MultiClass has no trainable
+ * parameter; RobustMax.epsilon is trainable=False). */
+int mgp_elbo_terms_multiclass(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
+                              int64_t ldf, const float* Y, float epsilon, const float* assign_lik_var,
+                              int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
+                              const float* noise_u, uint64_t seed, int64_t n_offset, double* data_sum,
+                              void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+int mgp_elbo_terms_multiclass_backward(const float* mu_f, const float* var_f, const float* mu_a,
+                                       const float* var_a, int64_t ldf, const float* Y, float epsilon,
+                                       const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                                       const float* noise_z, const float* noise_u, uint64_t seed,
+                                       int64_t n_offset, float scale, float* G, int64_t ldg,
+                                       double* g_assign_lik_var, void* workspace, size_t workspace_bytes,
+                                       mgp_stream_t stream);
+/* MultiClass._predict_mean_and_var: y_mean = ps, y_var = ps - ps^2 ([N][K] row-major),
+ * ps[n][i] = p_i(n) (1 - eps) + (1 - p_i(n)) eps / (K - 1). */
+int mgp_multiclass_predict(const float* fmean, const float* fvar, int64_t ldf, int64_t N, int32_t K,
+                           float epsilon, float* y_mean, float* y_var, mgp_stream_t stream);
+/* SMGP.predict_samples with the MultiClass predictive mean / variance for samples_y. */
+int mgp_predict_samples_multiclass(const float* mu_f, const float* var_f, const float* mu_a,
+                                   const float* var_a, int64_t ldf, float epsilon, int64_t N, int32_t K,
+                                   int32_t S, float tau, const float* noise_zw, const float* noise_uw,
+                                   const float* noise_zy, uint64_t seed, int64_t n_offset, float* samples_y,
+                                   float* samples_f, mgp_stream_t stream);
+
+/* Philox stream-2 normals [S][N][K] (the z of mgp_predict_samples), as mgp_philox_noise. */
 int mgp_philox_normal2(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S, float* z,
                        mgp_stream_t stream);
 

@@ -120,6 +120,19 @@ SIGNATURES = {
     "mgp_predict_samples": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i32,
                                            c_i32, ctypes.c_float, c_ptr, c_ptr, c_ptr, c_u64, c_i64,
                                            c_ptr, c_ptr, c_ptr]),
+    "mgp_elbo_terms_multiclass": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, ctypes.c_float,
+                                                 c_ptr, c_i64, c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_u64,
+                                                 c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_elbo_terms_multiclass_backward": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr,
+                                                          ctypes.c_float, c_ptr, c_i64, c_i32, c_i32,
+                                                          ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64,
+                                                          ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size,
+                                                          c_ptr]),
+    "mgp_multiclass_predict": (ctypes.c_int, [c_ptr, c_ptr, c_i64, c_i64, c_i32, ctypes.c_float, c_ptr, c_ptr,
+                                              c_ptr]),
+    "mgp_predict_samples_multiclass": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, ctypes.c_float, c_i64,
+                                                      c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_ptr, c_u64,
+                                                      c_i64, c_ptr, c_ptr, c_ptr]),
 }
 
 _lib = None

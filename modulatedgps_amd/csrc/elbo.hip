@@ -58,17 +58,110 @@ __device__ __forceinline__ void draw_noise(float (&z)[KMAX], float (&u)[KMAX], c
   }
 }
 
+// ------------------------------------------------------------------ MultiClass / RobustMax
+// GPflow 2.7.0 likelihoods.MultiClass(num_classes = K, invlink = RobustMax(K))
+// (gpflow pinned at environment.yml:95, not vendored), the pred likelihood of the
+// multiclass demos (demos/demo_tf2_modified_multiclass.py:43-45), reached through
+// BroadcastingLikelihood's flatten path (broadcasting_lik.py:19-37,39-42) from
+// E_log_p_Y (models.py:63-67,113-120):
+//   p    = RobustMax.prob_is_largest(y, mu, var): 20-point Gauss-Hermite over the
+//          selected latent, X_g = mu_y + x_g sqrt(2 var_y),
+//          p = sum_g w_g / sqrt(pi) prod_{k != y} [(1 - 2e-6) Phi((X_g - mu_k) / sqrt(var_k)) + 1e-6]
+//          (safe_sqrt: square roots of max(., 1e-10); a label outside [0, K) selects nothing)
+//   ve   = p log(1 - eps) + (1 - p) log(eps / (K - 1))
+// ve is one value per point; the reference multiplies it by W [S, N, K] and sums
+// over K, so the sample mixture is l_s = ve sum_k W_sk.
+__constant__ float kGHx[20] = {
+    -5.387480890e+00f, -4.603682450e+00f, -3.944764040e+00f, -3.347854567e+00f, -2.788806058e+00f,
+    -2.254974002e+00f, -1.738537712e+00f, -1.234076215e+00f, -7.374737285e-01f, -2.453407083e-01f,
+    2.453407083e-01f,  7.374737285e-01f,  1.234076215e+00f,  1.738537712e+00f,  2.254974002e+00f,
+    2.788806058e+00f,  3.347854567e+00f,  3.944764040e+00f,  4.603682450e+00f,  5.387480890e+00f};
+__constant__ float kGHc[20] = {  // w_g / sqrt(pi)
+    1.257800672e-13f, 2.482062362e-10f, 6.127490260e-08f, 4.402121090e-06f, 1.288262800e-04f,
+    1.830103131e-03f, 1.399783745e-02f, 6.150637206e-02f, 1.617393340e-01f, 2.607930634e-01f,
+    2.607930634e-01f, 1.617393340e-01f, 6.150637206e-02f, 1.399783745e-02f, 1.830103131e-03f,
+    1.288262800e-04f, 4.402121090e-06f, 6.127490260e-08f, 2.482062362e-10f, 1.257800672e-13f};
+
+// p and (GRAD) dp/dmu[k], dp/dvar[k] for label y over the first K latents.
+template <int KMAX, bool GRAD>
+__device__ __forceinline__ float robustmax_p(int y, const float (&mu)[KMAX], const float (&var)[KMAX], int K,
+                                             float (&dmu)[KMAX], float (&dvar)[KMAX]) {
+  constexpr float kSq = 1e-6f, kKeep = 1.f - 2e-6f, kRsqrt2 = 0.70710678118654752f;
+  constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+  float mus = 0.f, vs = 0.f, rs[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (k == y) { mus = mu[k]; vs = var[k]; }
+    rs[k] = (k < K) ? 1.f / sqrtf(fmaxf(var[k], 1e-10f)) : 0.f;
+    if constexpr (GRAD) { dmu[k] = 0.f; dvar[k] = 0.f; }
+  }
+  const float sx = sqrtf(fmaxf(2.f * vs, 1e-10f));
+  float p = 0.f, gsel = 0.f, gselx = 0.f;
+  for (int g = 0; g < 20; ++g) {
+    const float X = fmaf(kGHx[g], sx, mus);
+    float d[KMAX], C[KMAX], prod = 1.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K && k != y) {
+        d[k] = (X - mu[k]) * rs[k];
+        C[k] = fmaf(kKeep, 0.5f * erfcf(-d[k] * kRsqrt2), kSq);
+        prod *= C[k];
+      }
+    }
+    p = fmaf(kGHc[g], prod, p);
+    if constexpr (GRAD) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K && k != y) {
+          // c_g prod_{j != k} C_j (1 - 2e-6) phi(d_k) / sqrt(var_k)
+          const float t = kGHc[g] * (prod / C[k]) * kKeep * kInvSqrt2Pi * __expf(-0.5f * d[k] * d[k]) * rs[k];
+          dmu[k] -= t;
+          if (var[k] > 1e-10f) dvar[k] -= 0.5f * t * d[k] * rs[k];
+          acc += t;
+        }
+      }
+      gsel += acc;
+      gselx = fmaf(acc, kGHx[g], gselx);
+    }
+  }
+  if constexpr (GRAD) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k == y) {
+        dmu[k] = gsel;
+        dvar[k] = (2.f * vs > 1e-10f) ? gselx / sx : 0.f;
+      }
+    }
+  }
+  return p;
+}
+
+// Load the K latents of point n (expert-major [K][ldf]).
+template <int KMAX>
+__device__ __forceinline__ void load_latents(const float* __restrict__ mu_f, const float* __restrict__ var_f,
+                                             int64_t ldf, int64_t n, int K, float (&mu)[KMAX],
+                                             float (&var)[KMAX]) {
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    mu[k] = (k < K) ? mu_f[(int64_t)k * ldf + n] : 0.f;
+    var[k] = (k < K) ? var_f[(int64_t)k * ldf + n] : 1.f;
+  }
+}
+
 // MOD: SMGPModified.E_log_p_Y (models.py:112-123) -- a second Gaussian
 // var-exp of the assignment layer (likelihood variances lik_var_a) weighted by
 // the same W, with its own logsumexp over S: lse_S(sum_k W ve_a) + lse_S(sum_k W ve_f) - 2 log S.
-template <int KMAX, bool MOD>
+// MC: the pred likelihood is MultiClass/RobustMax (mc_a = log(1 - eps),
+// mc_b = log(eps / (K - 1)); lik_var unused): ve_k = the point's RobustMax var-exp.
+template <int KMAX, bool MOD, bool MC>
 __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
     const float* __restrict__ lik_var, const float* __restrict__ lik_var_a, int64_t N, int K, int S,
     float inv_tau,
     const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
-    uint32_t key1, int64_t n_offset, double* __restrict__ partials) {
+    uint32_t key1, int64_t n_offset, double* __restrict__ partials, float mc_a, float mc_b) {
   __shared__ double scratch[16];
   const int64_t n = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
   float val = 0.f;
@@ -76,12 +169,23 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
     const float kHalfLog2Pi = 0.91893853320467274f;
     float ve[KMAX], ma[KMAX], sa[KMAX], vea[MOD ? KMAX : 1];
     const float y = Y[n];
+    float vemc = 0.f;
+    if constexpr (MC) {
+      float mu[KMAX], var[KMAX], dm[KMAX], dv[KMAX];
+      load_latents<KMAX>(mu_f, var_f, ldf, n, K, mu, var);
+      const float p = robustmax_p<KMAX, false>((int)y, mu, var, K, dm, dv);
+      vemc = fmaf(p, mc_a - mc_b, mc_b);
+    }
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       if (k < K) {
-        const float s2 = lik_var[k];
-        const float d = y - mu_f[(int64_t)k * ldf + n];
-        ve[k] = -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + n]) / s2;
+        if constexpr (MC) {
+          ve[k] = vemc;
+        } else {
+          const float s2 = lik_var[k];
+          const float d = y - mu_f[(int64_t)k * ldf + n];
+          ve[k] = -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + n]) / s2;
+        }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
         sa[k] = sqrtf(va + 1e-6f);
@@ -156,14 +260,16 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
 // gradients).  Two passes over the samples with the noise redrawn (Philox is
 // counter-based): the first finds lse, the second accumulates.  Outputs are
 // multiplied by `scale` (1 / N_total for the ELBO's batch mean).
-template <int KMAX, bool MOD>
+// MC: dDT/dve_mc = sum_k om_k, chained through robustmax_p's gradient; no
+// likelihood-variance gradient (MultiClass has no trainable parameter).
+template <int KMAX, bool MOD, bool MC>
 __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
     const float* __restrict__ lik_var, const float* __restrict__ lik_var_a, int64_t N, int K, int S,
     float inv_tau, const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
     uint32_t key1, int64_t n_offset, float scale, float* __restrict__ G, int64_t ldg,
-    double* __restrict__ partials) {
+    double* __restrict__ partials, float mc_a, float mc_b) {
   __shared__ double scratch[16];
   const int64_t n = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
   float glv[KMAX], glva[MOD ? KMAX : 1];
@@ -177,12 +283,22 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     const float kHalfLog2Pi = 0.91893853320467274f;
     const float y = Y[n];
     float ve[KMAX], ma[KMAX], sa[KMAX], vea[MOD ? KMAX : 1];
+    float mcm[MC ? KMAX : 1], mcv[MC ? KMAX : 1], dpm[MC ? KMAX : 1], dpv[MC ? KMAX : 1], vemc = 0.f;
+    if constexpr (MC) {
+      load_latents<KMAX>(mu_f, var_f, ldf, n, K, mcm, mcv);
+      const float p = robustmax_p<KMAX, true>((int)y, mcm, mcv, K, dpm, dpv);
+      vemc = fmaf(p, mc_a - mc_b, mc_b);
+    }
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       if (k < K) {
-        const float s2 = lik_var[k];
-        const float d = y - mu_f[(int64_t)k * ldf + n];
-        ve[k] = -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + n]) / s2;
+        if constexpr (MC) {
+          ve[k] = vemc;
+        } else {
+          const float s2 = lik_var[k];
+          const float d = y - mu_f[(int64_t)k * ldf + n];
+          ve[k] = -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + n]) / s2;
+        }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
         sa[k] = sqrtf(va + 1e-6f);
@@ -267,15 +383,29 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
         gxz[k] = fmaf(t, z[k], gxz[k]);
       }
     }
+    float gve_mc = 0.f;
+    if constexpr (MC) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) gve_mc += (k < K) ? om[k] : 0.f;
+      gve_mc *= scale * (mc_a - mc_b);
+    }
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       if (k < K) {
-        const float s2 = lik_var[k];
-        const float mf = mu_f[(int64_t)k * ldf + n], vf = var_f[(int64_t)k * ldf + n];
-        const float d = y - mf;
         float gma = gx[k] * inv_tau;
         float gva = gxz[k] * inv_tau * 0.5f / sa[k];
-        glv[k] = scale * om[k] * (-0.5f / s2 + 0.5f * (d * d + vf) / (s2 * s2));
+        float gmf, gvf;
+        if constexpr (MC) {
+          gmf = gve_mc * dpm[k];
+          gvf = gve_mc * dpv[k];
+        } else {
+          const float s2 = lik_var[k];
+          const float mf = mu_f[(int64_t)k * ldf + n], vf = var_f[(int64_t)k * ldf + n];
+          const float d = y - mf;
+          glv[k] = scale * om[k] * (-0.5f / s2 + 0.5f * (d * d + vf) / (s2 * s2));
+          gmf = scale * om[k] * d / s2;
+          gvf = -0.5f * scale * om[k] / s2;
+        }
         if constexpr (MOD) {
           const float s2a = lik_var_a[k];
           const float da = y - ma[k];
@@ -284,8 +414,8 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
           gva -= 0.5f * oma[k] / s2a;
           glva[k] = scale * oma[k] * (-0.5f / s2a + 0.5f * (da * da + va) / (s2a * s2a));
         }
-        G[(int64_t)(0 * K + k) * ldg + n] = scale * om[k] * d / s2;
-        G[(int64_t)(1 * K + k) * ldg + n] = -0.5f * scale * om[k] / s2;
+        G[(int64_t)(0 * K + k) * ldg + n] = gmf;
+        G[(int64_t)(1 * K + k) * ldg + n] = gvf;
         G[(int64_t)(2 * K + k) * ldg + n] = scale * gma;
         G[(int64_t)(3 * K + k) * ldg + n] = scale * gva;
       }
@@ -427,14 +557,52 @@ __global__ __launch_bounds__(256) void philox_noise_kernel(uint32_t key0, uint32
   }
 }
 
-// SMGP.predict_samples (models.py:91-103).  One thread per (s, n).
+// MultiClass._predict_mean_and_var (GPflow 2.7.0, via broadcasting_lik.py:44-46):
+// ps[i] = p_i (1 - eps) + (1 - p_i) eps / (K - 1) with p_i = prob_is_largest(i, mu, var)
+// for every class i; mean = ps, var = ps - ps^2.
 template <int KMAX>
+__device__ __forceinline__ void multiclass_ps(const float (&mu)[KMAX], const float (&var)[KMAX], int K,
+                                              float keep, float other, float (&ps)[KMAX]) {
+  float dm[KMAX], dv[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    ps[i] = 0.f;
+    if (i < K) {
+      const float p = robustmax_p<KMAX, false>(i, mu, var, K, dm, dv);
+      ps[i] = fmaf(p, keep - other, other);
+    }
+  }
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void multiclass_predict_kernel(const float* __restrict__ fmean,
+                                                                 const float* __restrict__ fvar, int64_t ldf,
+                                                                 int64_t N, int K, float keep, float other,
+                                                                 float* __restrict__ y_mean,
+                                                                 float* __restrict__ y_var) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float mu[KMAX], var[KMAX], ps[KMAX];
+  load_latents<KMAX>(fmean, fvar, ldf, n, K, mu, var);
+  multiclass_ps<KMAX>(mu, var, K, keep, other, ps);
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    if (i < K) {
+      if (y_mean) y_mean[n * K + i] = ps[i];
+      if (y_var) y_var[n * K + i] = ps[i] - ps[i] * ps[i];
+    }
+  }
+}
+
+// SMGP.predict_samples (models.py:91-103).  One thread per (s, n).
+// MC: the likelihood's predictive mean / variance are MultiClass's (ps, ps - ps^2).
+template <int KMAX, bool MC = false>
 __global__ __launch_bounds__(256) void predict_samples_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ lik_var, int64_t N, int K,
     int S, float inv_tau, const float* __restrict__ zw_in, const float* __restrict__ uw_in,
     const float* __restrict__ zy_in, uint32_t key0, uint32_t key1, int64_t n_offset,
-    float* __restrict__ sy, float* __restrict__ sf) {
+    float* __restrict__ sy, float* __restrict__ sf, float mc_keep = 0.f, float mc_other = 0.f) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= N * (int64_t)S) return;
   const int s = (int)(idx / N);
@@ -477,6 +645,12 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
       x[k] = (-logf(-logf(uw[k])) + logit) * inv_tau;
       xm = fmaxf(xm, x[k]);
     }
+  float ps[MC ? KMAX : 1];
+  if constexpr (MC) {
+    float mu[KMAX], var[KMAX];
+    load_latents<KMAX>(mu_f, var_f, ldf, n, K, mu, var);
+    multiclass_ps<KMAX>(mu, var, K, mc_keep, mc_other, ps);
+  }
   float den = 0.f, ay = 0.f, af = 0.f;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
@@ -484,7 +658,10 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
       const float e = __expf(x[k] - xm);
       const float m = mu_f[(int64_t)k * ldf + n], v = var_f[(int64_t)k * ldf + n];
       den += e;
-      ay = fmaf(e, fmaf(zy[k], sqrtf(v + lik_var[k] + 1e-6f), m), ay);
+      if constexpr (MC)
+        ay = fmaf(e, fmaf(zy[k], sqrtf(ps[k] - ps[k] * ps[k] + 1e-6f), ps[k]), ay);
+      else
+        ay = fmaf(e, fmaf(zy[k], sqrtf(v + lik_var[k] + 1e-6f), m), ay);
       af = fmaf(e, fmaf(zy[k], sqrtf(v + 1e-6f), m), af);
     }
   if (sy) sy[(int64_t)s * N + n] = ay / den;
@@ -510,6 +687,31 @@ __global__ __launch_bounds__(256) void philox_normal2_kernel(uint32_t key0, uint
 
 using namespace mgp;
 
+static int predict_samples_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
+                               int64_t ldf, const float* lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                               const float* noise_zw, const float* noise_uw, const float* noise_zy, uint64_t seed,
+                               int64_t n_offset, float* samples_y, float* samples_f, hipStream_t s, bool mc,
+                               float keep, float other) {
+  if (N == 0) return MGP_OK;
+  const int64_t total = N * (int64_t)S;
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+#define MGP_PS_CASE(KM)                                                                                      \
+  if (K <= KM) {                                                                                              \
+    if (mc)                                                                                                   \
+      hipLaunchKernelGGL((predict_samples_kernel<KM, true>), grid, block, 0, s, mu_f, var_f, mu_a, var_a, ldf, \
+                         lik_var, N, K, S, 1.f / tau, noise_zw, noise_uw, noise_zy, k0, k1, n_offset, samples_y, \
+                         samples_f, keep, other);                                                              \
+    else                                                                                                      \
+      hipLaunchKernelGGL((predict_samples_kernel<KM, false>), grid, block, 0, s, mu_f, var_f, mu_a, var_a,     \
+                         ldf, lik_var, N, K, S, 1.f / tau, noise_zw, noise_uw, noise_zy, k0, k1, n_offset,     \
+                         samples_y, samples_f, 0.f, 0.f);                                                      \
+  } else
+  MGP_PS_CASE(4) MGP_PS_CASE(8) MGP_PS_CASE(16) MGP_PS_CASE(32) {}
+#undef MGP_PS_CASE
+  return launch_status();
+}
+
 extern "C" int mgp_predict_samples(const float* mu_f, const float* var_f, const float* mu_a,
                                    const float* var_a, int64_t ldf, const float* lik_var, int64_t N,
                                    int32_t K, int32_t S, float tau, const float* noise_zw,
@@ -530,19 +732,56 @@ extern "C" int mgp_predict_samples(const float* mu_f, const float* var_f, const 
   const bool any = noise_zw || noise_uw || noise_zy, all = noise_zw && noise_uw && noise_zy;
   if (any && !all) return -11;
   if (n_offset < 0) return -15;
+  return predict_samples_run(mu_f, var_f, mu_a, var_a, ldf, lik_var, N, K, S, tau, noise_zw, noise_uw, noise_zy,
+                             seed, n_offset, samples_y, samples_f, (hipStream_t)stream, false, 0.f, 0.f);
+}
+
+extern "C" int mgp_predict_samples_multiclass(const float* mu_f, const float* var_f, const float* mu_a,
+                                              const float* var_a, int64_t ldf, float epsilon, int64_t N,
+                                              int32_t K, int32_t S, float tau, const float* noise_zw,
+                                              const float* noise_uw, const float* noise_zy, uint64_t seed,
+                                              int64_t n_offset, float* samples_y, float* samples_f,
+                                              mgp_stream_t stream) {
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (!mu_a) return -3;
+  if (!var_a) return -4;
+  if (ldf < N) return -5;
+  if (!(epsilon > 0.f && epsilon < 1.f)) return -6;
+  if (N < 0) return -7;
+  if (K < 2) return -8;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -9;
+  if (!(tau > 0.f)) return -10;
+  const bool any = noise_zw || noise_uw || noise_zy, all = noise_zw && noise_uw && noise_zy;
+  if (any && !all) return -11;
+  if (n_offset < 0) return -15;
+  const float keep = 1.f - epsilon, other = (float)((double)epsilon / (double)(K - 1));
+  return predict_samples_run(mu_f, var_f, mu_a, var_a, ldf, nullptr, N, K, S, tau, noise_zw, noise_uw, noise_zy,
+                             seed, n_offset, samples_y, samples_f, (hipStream_t)stream, true, keep, other);
+}
+
+extern "C" int mgp_multiclass_predict(const float* fmean, const float* fvar, int64_t ldf, int64_t N, int32_t K,
+                                      float epsilon, float* y_mean, float* y_var, mgp_stream_t stream) {
+  if (!fmean) return -1;
+  if (!fvar) return -2;
+  if (ldf < N) return -3;
+  if (N < 0) return -4;
+  if (K < 2) return -5;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (!(epsilon > 0.f && epsilon < 1.f)) return -6;
+  if (!y_mean && !y_var) return -7;
   if (N == 0) return MGP_OK;
-  const int64_t total = N * (int64_t)S;
-  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  const float keep = 1.f - epsilon, other = (float)((double)epsilon / (double)(K - 1));
+  const dim3 grid((unsigned)((N + 255) / 256)), block(256);
   hipStream_t s = (hipStream_t)stream;
-  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
-#define MGP_PS_CASE(KM)                                                                              \
-  if (K <= KM) {                                                                                      \
-    hipLaunchKernelGGL(predict_samples_kernel<KM>, grid, block, 0, s, mu_f, var_f, mu_a, var_a, ldf,  \
-                       lik_var, N, K, S, 1.f / tau, noise_zw, noise_uw, noise_zy, k0, k1, n_offset,   \
-                       samples_y, samples_f);                                                         \
+#define MGP_MCP_CASE(KM)                                                                                  \
+  if (K <= KM) {                                                                                           \
+    hipLaunchKernelGGL(multiclass_predict_kernel<KM>, grid, block, 0, s, fmean, fvar, ldf, N, K, keep, other, \
+                       y_mean, y_var);                                                                     \
   } else
-  MGP_PS_CASE(4) MGP_PS_CASE(8) MGP_PS_CASE(16) MGP_PS_CASE(32) {}
-#undef MGP_PS_CASE
+  MGP_MCP_CASE(2) MGP_MCP_CASE(4) MGP_MCP_CASE(8) MGP_MCP_CASE(16) MGP_MCP_CASE(32) {}
+#undef MGP_MCP_CASE
   return launch_status();
 }
 
@@ -567,11 +806,25 @@ extern "C" size_t mgp_elbo_workspace_bytes(int64_t N) {
   return (size_t)(elbo_blocks(N) > 0 ? elbo_blocks(N) : 1) * sizeof(double);
 }
 
+template <int KM, bool MOD, bool MC>
+static void launch_elbo_terms(int nb, hipStream_t s, const float* mu_f, const float* var_f, const float* mu_a,
+                              const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
+                              const float* lik_var_a, int64_t N, int K, int S, float inv_tau,
+                              const float* noise_z, const float* noise_u, uint32_t k0, uint32_t k1,
+                              int64_t n_offset, double* partials, float mc_a, float mc_b) {
+  hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a, var_a,
+                     ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, noise_z, noise_u, k0, k1, n_offset, partials,
+                     mc_a, mc_b);
+}
+
+// mc: the pred likelihood is MultiClass(K)/RobustMax(eps) with mc_a = log(1 - eps),
+// mc_b = log(eps / (K - 1)) (lik_var unused); lik_var_a != NULL: SMGPModified.
 static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
                           int64_t ldf, const float* Y, const float* lik_var, const float* lik_var_a,
                           int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
                           const float* noise_u, uint64_t seed, int64_t n_offset, double* data_sum,
-                          void* workspace, size_t workspace_bytes, hipStream_t s) {
+                          void* workspace, size_t workspace_bytes, hipStream_t s, bool mc = false,
+                          float mc_a = 0.f, float mc_b = 0.f) {
   if (!workspace || workspace_bytes < mgp_elbo_workspace_bytes(N)) return MGP_ERR_WORKSPACE;
   double* partials = (double*)workspace;
   const int nb = (int)elbo_blocks(N);
@@ -579,14 +832,10 @@ static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu
   if (nb > 0) {
 #define MGP_ELBO_CASE(KM)                                                                               \
   if (K <= KM) {                                                                                         \
-    if (lik_var_a)                                                                                       \
-      hipLaunchKernelGGL((elbo_terms_kernel<KM, true>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, \
-                         mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, noise_z, noise_u,   \
-                         k0, k1, n_offset, partials);                                                    \
-    else                                                                                                 \
-      hipLaunchKernelGGL((elbo_terms_kernel<KM, false>), dim3(nb), dim3(kElboThreads), 0, s, mu_f,       \
-                         var_f, mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, noise_z,     \
-                         noise_u, k0, k1, n_offset, partials);                                           \
+    auto f = lik_var_a ? (mc ? launch_elbo_terms<KM, true, true> : launch_elbo_terms<KM, true, false>)   \
+                       : (mc ? launch_elbo_terms<KM, false, true> : launch_elbo_terms<KM, false, false>); \
+    f(nb, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, noise_z, noise_u, \
+      k0, k1, n_offset, partials, mc_a, mc_b);                                                           \
   } else
     MGP_ELBO_CASE(1) MGP_ELBO_CASE(2) MGP_ELBO_CASE(4) MGP_ELBO_CASE(8) MGP_ELBO_CASE(16)
     MGP_ELBO_CASE(32) {}
@@ -744,6 +993,54 @@ extern "C" size_t mgp_elbo_backward_workspace_bytes(int64_t N, int32_t K) {
   return (size_t)nb * 2 * (size_t)elbo_kmax(K) * sizeof(double);
 }
 
+template <int KM, bool MOD, bool MC>
+static void launch_elbo_bwd(int nb, hipStream_t s, const float* mu_f, const float* var_f, const float* mu_a,
+                            const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
+                            const float* lik_var_a, int64_t N, int K, int S, float inv_tau, const float* noise_z,
+                            const float* noise_u, uint32_t k0, uint32_t k1, int64_t n_offset, float scale,
+                            float* G, int64_t ldg, double* partials, float mc_a, float mc_b) {
+  hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, MOD, MC>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
+                     var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, noise_z, noise_u, k0, k1, n_offset,
+                     scale, G, ldg, partials, mc_a, mc_b);
+}
+
+static int elbo_bwd_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a, int64_t ldf,
+                        const float* Y, const float* lik_var, const float* assign_lik_var, int64_t N, int32_t K,
+                        int32_t S, float tau, const float* noise_z, const float* noise_u, uint64_t seed,
+                        int64_t n_offset, float scale, float* G, int64_t ldg, double* g_lik_var,
+                        double* g_assign_lik_var, void* workspace, size_t workspace_bytes, hipStream_t s, bool mc,
+                        float mc_a, float mc_b) {
+  if (!workspace || workspace_bytes < mgp_elbo_backward_workspace_bytes(N, K)) return MGP_ERR_WORKSPACE;
+  double* partials = (double*)workspace;
+  const int nb = (int)elbo_blocks(N);
+  const int km = elbo_kmax(K);
+  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+  if (nb == 0) {
+    if (g_lik_var) hipMemsetAsync(g_lik_var, 0, (size_t)K * sizeof(double), s);
+    if (assign_lik_var) hipMemsetAsync(g_assign_lik_var, 0, (size_t)K * sizeof(double), s);
+    return launch_status();
+  }
+#define MGP_ELBO_BWD_CASE(KM)                                                                             \
+  if (km == KM) {                                                                                         \
+    auto f = assign_lik_var ? (mc ? launch_elbo_bwd<KM, true, true> : launch_elbo_bwd<KM, true, false>)  \
+                            : (mc ? launch_elbo_bwd<KM, false, true> : launch_elbo_bwd<KM, false, false>); \
+    f(nb, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, 1.f / tau, noise_z,       \
+      noise_u, k0, k1, n_offset, scale, G, ldg, partials, mc_a, mc_b);                                    \
+  } else
+  MGP_ELBO_BWD_CASE(1) MGP_ELBO_BWD_CASE(2) MGP_ELBO_BWD_CASE(4) MGP_ELBO_BWD_CASE(8) MGP_ELBO_BWD_CASE(16)
+  MGP_ELBO_BWD_CASE(32) {}
+#undef MGP_ELBO_BWD_CASE
+  int st = launch_status();
+  if (st) return st;
+  if (g_lik_var)
+    hipLaunchKernelGGL(column_sums_kernel, dim3(K), dim3(256), 0, s, partials, nb, (int64_t)2 * km, g_lik_var,
+                       (int64_t)1);
+  if (assign_lik_var)
+    hipLaunchKernelGGL(column_sums_kernel, dim3(K), dim3(256), 0, s, partials + km, nb, (int64_t)2 * km,
+                       g_assign_lik_var, (int64_t)1);
+  return launch_status();
+}
+
 extern "C" int mgp_elbo_terms_backward(const float* mu_f, const float* var_f, const float* mu_a,
                                        const float* var_a, int64_t ldf, const float* Y,
                                        const float* lik_var, const float* assign_lik_var, int64_t N,
@@ -770,37 +1067,73 @@ extern "C" int mgp_elbo_terms_backward(const float* mu_f, const float* var_f, co
   if (ldg < N) return -19;
   if (!g_lik_var) return -20;
   if (assign_lik_var && !g_assign_lik_var) return -21;
-  if (!workspace || workspace_bytes < mgp_elbo_backward_workspace_bytes(N, K)) return MGP_ERR_WORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
-  double* partials = (double*)workspace;
-  const int nb = (int)elbo_blocks(N);
-  const int km = elbo_kmax(K);
-  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
-  if (nb == 0) {
-    hipMemsetAsync(g_lik_var, 0, (size_t)K * sizeof(double), s);
-    if (assign_lik_var) hipMemsetAsync(g_assign_lik_var, 0, (size_t)K * sizeof(double), s);
-    return launch_status();
-  }
-#define MGP_ELBO_BWD_CASE(KM)                                                                             \
-  if (km == KM) {                                                                                         \
-    if (assign_lik_var)                                                                                   \
-      hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, true>), dim3(nb), dim3(kElboThreads), 0, s, mu_f,     \
-                         var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, 1.f / tau, noise_z, \
-                         noise_u, k0, k1, n_offset, scale, G, ldg, partials);                             \
-    else                                                                                                  \
-      hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, false>), dim3(nb), dim3(kElboThreads), 0, s, mu_f,    \
-                         var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, 1.f / tau, noise_z, \
-                         noise_u, k0, k1, n_offset, scale, G, ldg, partials);                             \
-  } else
-  MGP_ELBO_BWD_CASE(1) MGP_ELBO_BWD_CASE(2) MGP_ELBO_BWD_CASE(4) MGP_ELBO_BWD_CASE(8) MGP_ELBO_BWD_CASE(16)
-  MGP_ELBO_BWD_CASE(32) {}
-#undef MGP_ELBO_BWD_CASE
-  int st = launch_status();
-  if (st) return st;
-  hipLaunchKernelGGL(column_sums_kernel, dim3(K), dim3(256), 0, s, partials, nb, (int64_t)2 * km, g_lik_var,
-                     (int64_t)1);
-  if (assign_lik_var)
-    hipLaunchKernelGGL(column_sums_kernel, dim3(K), dim3(256), 0, s, partials + km, nb, (int64_t)2 * km,
-                       g_assign_lik_var, (int64_t)1);
-  return launch_status();
+  return elbo_bwd_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, tau, noise_z, noise_u,
+                      seed, n_offset, scale, G, ldg, g_lik_var, g_assign_lik_var, workspace, workspace_bytes,
+                      (hipStream_t)stream, false, 0.f, 0.f);
+}
+
+// ------------------------------------------------------------------ MultiClass entries
+static bool mc_consts(int K, float epsilon, float& a, float& b) {
+  if (K < 2 || !(epsilon > 0.f) || !(epsilon < 1.f)) return false;
+  a = (float)log1p(-(double)epsilon);
+  b = (float)log((double)epsilon / (double)(K - 1));
+  return true;
+}
+
+extern "C" int mgp_elbo_terms_multiclass(const float* mu_f, const float* var_f, const float* mu_a,
+                                         const float* var_a, int64_t ldf, const float* Y, float epsilon,
+                                         const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                                         const float* noise_z, const float* noise_u, uint64_t seed,
+                                         int64_t n_offset, double* data_sum, void* workspace,
+                                         size_t workspace_bytes, mgp_stream_t stream) {
+  float a, b;
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (!mu_a) return -3;
+  if (!var_a) return -4;
+  if (ldf < N) return -5;
+  if (!Y) return -6;
+  if (!(epsilon > 0.f && epsilon < 1.f)) return -7;
+  if (N < 0) return -9;
+  if (K < 2) return -10;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -11;
+  if (!(tau > 0.f)) return -12;
+  if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
+  if (n_offset < 0) return -16;
+  if (!data_sum) return -17;
+  mc_consts(K, epsilon, a, b);
+  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, nullptr, assign_lik_var, N, K, S, tau, noise_z, noise_u,
+                        seed, n_offset, data_sum, workspace, workspace_bytes, (hipStream_t)stream, true, a, b);
+}
+
+extern "C" int mgp_elbo_terms_multiclass_backward(const float* mu_f, const float* var_f, const float* mu_a,
+                                                  const float* var_a, int64_t ldf, const float* Y, float epsilon,
+                                                  const float* assign_lik_var, int64_t N, int32_t K, int32_t S,
+                                                  float tau, const float* noise_z, const float* noise_u,
+                                                  uint64_t seed, int64_t n_offset, float scale, float* G,
+                                                  int64_t ldg, double* g_assign_lik_var, void* workspace,
+                                                  size_t workspace_bytes, mgp_stream_t stream) {
+  float a, b;
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (!mu_a) return -3;
+  if (!var_a) return -4;
+  if (ldf < N) return -5;
+  if (!Y) return -6;
+  if (!(epsilon > 0.f && epsilon < 1.f)) return -7;
+  if (N < 0) return -9;
+  if (K < 2) return -10;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -11;
+  if (!(tau > 0.f)) return -12;
+  if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
+  if (n_offset < 0) return -16;
+  if (!G) return -18;
+  if (ldg < N) return -19;
+  if (assign_lik_var && !g_assign_lik_var) return -20;
+  mc_consts(K, epsilon, a, b);
+  return elbo_bwd_run(mu_f, var_f, mu_a, var_a, ldf, Y, nullptr, assign_lik_var, N, K, S, tau, noise_z, noise_u,
+                      seed, n_offset, scale, G, ldg, nullptr, g_assign_lik_var, workspace, workspace_bytes,
+                      (hipStream_t)stream, true, a, b);
 }

@@ -141,10 +141,11 @@ def expert_parallel_elbo(model, X, Y, group=None, seed=None, noise=None):
     nz = None
     if noise is not None:
         nz = (noise[0][:, lo:hi].contiguous(), noise[1][:, lo:hi].contiguous())
-    lik_var = model.likelihood.likelihood.variance.reshape(-1)
+    mc = model._mc_eps()
+    lik_var = None if mc is not None else model.likelihood.likelihood.variance.reshape(-1)
     data = ops.elbo_terms(cond[0:K], cond[K:2 * K], cond[2 * K:3 * K], cond[3 * K:4 * K], Yd, lik_var,
                           model.num_samples, 1e-2, noise=nz, seed=seed or 0, n_offset=lo,
-                          assign_lik_var=model._assign_lik_var())
+                          assign_lik_var=model._assign_lik_var(), multiclass_eps=mc)
     allreduce_data_term(data, pg)
     kl = torch.cat([model.pred_layer.prior_kl(), model.assign_layer.prior_kl()])
     num_data = model.num_data if model.num_data is not None else N

@@ -39,6 +39,7 @@ from . import ops
 from .broadcasting_lik import BroadcastingLikelihood
 from .config import conditional_mode, default_device, default_jitter, expert_planes
 from .kernels import SquaredExponential
+from .likelihoods import MultiClass
 
 TAU = 1e-2  # RelaxedOneHotCategorical temperature, models.py:60
 
@@ -258,12 +259,22 @@ class SGP:
         X = torch.as_tensor(X)
         return X[None].expand(S, *X.shape), None
 
+    def _mc_eps(self):
+        """RobustMax epsilon when the pred likelihood is MultiClass, else None."""
+        lik = self.likelihood.likelihood
+        return lik.invlink.epsilon if isinstance(lik, MultiClass) else None
+
     def predict_y(self, Xnew, S=1):
-        """models.py:38-41 -> (mean, var) [S, N, K] (S broadcast copies)."""
+        """models.py:38-41 -> (mean, var) [S, N, K] (S broadcast copies); the
+        likelihood's _predict_mean_and_var through BroadcastingLikelihood
+        (broadcasting_lik.py:44-46): Gaussian (mu, var + sigma^2) or MultiClass (ps, ps - ps^2)."""
         lik = self.likelihood.likelihood
         X = self.pred_layer.kernel._x(Xnew)
         fm, fv = self.pred_layer.conditional_kn(X)
-        ym, yv, _ = ops.predict_epilogue(fm, fv, None, lik.variance.reshape(-1), want_y=True)
+        if self._mc_eps() is not None:
+            ym, yv = ops.multiclass_predict(fm, fv, self._mc_eps())
+        else:
+            ym, yv, _ = ops.predict_epilogue(fm, fv, None, lik.variance.reshape(-1), want_y=True)
         return ym[None].expand(S, *ym.shape), yv[None].expand(S, *yv.shape)
 
 
@@ -277,6 +288,8 @@ class SMGP(SGP):
         self.K = int(K)
         if pred_layer.num_latent_gps != self.K or assign_layer.num_latent_gps != self.K:
             raise ValueError("both layers must have num_latent_gps == K")
+        if isinstance(likelihood, MultiClass) and likelihood.num_classes != self.K:
+            raise ValueError("a MultiClass pred likelihood needs num_classes == K (one latent GP per class)")
         self.device = pred_layer.device
         self.seed = int(seed)
         self._draws = 0
@@ -450,13 +463,14 @@ class SMGP(SGP):
         b = self._buffers(N)
         kl = b["kl"]
         mu_f, var_f, mu_a, var_a = self.conditionals(X, timing=timing, kl_out=kl)
-        lik_var = self.likelihood.likelihood.variance.reshape(-1)
+        mc = self._mc_eps()
+        lik_var = None if mc is not None else self.likelihood.likelihood.variance.reshape(-1)
         if seed is None and noise is None:
             seed = self.next_seed()
         with _Stage(timing, "elbo_terms"):
             ops.elbo_terms(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU,
                            noise=noise, seed=seed or 0, n_offset=n_offset, out=b["data_sum"],
-                           assign_lik_var=self._assign_lik_var())
+                           assign_lik_var=self._assign_lik_var(), multiclass_eps=mc)
         if process_group is not None:
             import torch.distributed as dist
             with _Stage(timing, "allreduce"):
@@ -478,7 +492,8 @@ class SMGP(SGP):
                    (name + ".q_sqrt", layer.q_sqrt, "free"),
                    (name + ".variance", layer.kernel.variance, "positive"),
                    (name + ".lengthscales", layer.kernel.lengthscales, "positive")]
-        ps.append(("lik_variance", self.likelihood.likelihood.variance, "positive"))
+        if self._mc_eps() is None:  # MultiClass / RobustMax: no trainable likelihood parameter
+            ps.append(("lik_variance", self.likelihood.likelihood.variance, "positive"))
         if self._assign_lik_var() is not None:
             ps.append(("assign_lik_variance", self.assign_likelihood.likelihood.variance, "positive"))
         return ps
@@ -497,19 +512,22 @@ class SMGP(SGP):
         b = self._buffers(N, train=True)
         kl = b["kl"]
         mu_f, var_f, mu_a, var_a = self.conditionals(X, timing=timing, kl_out=kl, train=True)
-        lik_var = self.likelihood.likelihood.variance.reshape(-1)
+        mc = self._mc_eps()
+        lik_var = None if mc is not None else self.likelihood.likelihood.variance.reshape(-1)
         alv = self._assign_lik_var()
         if seed is None and noise is None:
             seed = self.next_seed()
         with _Stage(timing, "elbo_terms"):
             ops.elbo_terms(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU, noise=noise,
-                           seed=seed or 0, n_offset=n_offset, out=b["data_sum"], assign_lik_var=alv)
+                           seed=seed or 0, n_offset=n_offset, out=b["data_sum"], assign_lik_var=alv,
+                           multiclass_eps=mc)
         n_batch = n_total if n_total is not None else N
         with _Stage(timing, "elbo_terms_bwd"):
             G, glv, glva = ops.elbo_terms_backward(mu_f, var_f, mu_a, var_a, Yd, lik_var, self.num_samples, TAU,
                                                    noise=noise, seed=seed or 0, n_offset=n_offset,
-                                                   scale=1.0 / n_batch, assign_lik_var=alv, G=b["G"])
-        grads = {"lik_variance": glv}
+                                                   scale=1.0 / n_batch, assign_lik_var=alv, G=b["G"],
+                                                   multiclass_eps=mc)
+        grads = {"lik_variance": glv} if mc is None else {}
         if alv is not None:
             grads["assign_lik_variance"] = glva
         for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
@@ -574,9 +592,10 @@ class SMGP(SGP):
         mu_f, var_f, mu_a, var_a = self.conditionals(X)
         if seed is None and noise is None:
             seed = self.next_seed()
+        mc = self._mc_eps()
         sy, sf = ops.predict_samples(mu_f, var_f, mu_a, var_a,
-                                     self.likelihood.likelihood.variance.reshape(-1), S, TAU,
-                                     noise=noise, seed=seed or 0)
+                                     None if mc is not None else self.likelihood.likelihood.variance.reshape(-1),
+                                     S, TAU, noise=noise, seed=seed or 0, multiclass_eps=mc)
         return sy[..., None], sf[..., None]
 
 

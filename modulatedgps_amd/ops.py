@@ -316,9 +316,10 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
 
 
 def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0,
-                        n_offset=0, scale=1.0, assign_lik_var=None, G=None, workspace=None):
+                        n_offset=0, scale=1.0, assign_lik_var=None, G=None, workspace=None, multiclass_eps=None):
     """Gradient of the data term: G [4, K, N] = scale * d/d(mu_f, var_f, mu_a, var_a) and the
-    likelihood-variance gradients (float64 [K]; second one for SMGPModified, else None)."""
+    likelihood-variance gradients (float64 [K]; second one for SMGPModified, else None).
+    multiclass_eps: MultiClass / RobustMax pred likelihood (no likelihood-variance gradient: None)."""
     for t, n in ((mu_f, "mu_f"), (var_f, "var_f"), (mu_a, "mu_a"), (var_a, "var_a")):
         _check(t, n, 2)
     ldf = _ld(mu_f)
@@ -327,10 +328,12 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
     K, N = mu_f.shape
     dev = mu_f.device
     Y = Y.reshape(-1)
-    _check(Y, "Y"), _check(lik_var, "lik_var")
+    _check(Y, "Y")
+    if multiclass_eps is None:
+        _check(lik_var, "lik_var")
     if G is None:
         G = padded(4 * K, N, dev).unflatten(0, (4, K))
-    glv = torch.empty(K, dtype=torch.float64, device=dev)
+    glv = torch.empty(K, dtype=torch.float64, device=dev) if multiclass_eps is None else None
     glva = torch.empty(K, dtype=torch.float64, device=dev) if assign_lik_var is not None else None
     nbytes = _lib.load().mgp_elbo_backward_workspace_bytes(N, K)
     if workspace is None or workspace.numel() < nbytes:
@@ -340,6 +343,14 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
         z, u = noise
         z, u = z.contiguous(), u.contiguous()
         zp, up = z.data_ptr(), u.data_ptr()
+    if multiclass_eps is not None:
+        _lib.call("mgp_elbo_terms_multiclass_backward", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
+                  var_a.data_ptr(), ldf, Y.data_ptr(), float(multiclass_eps),
+                  assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau), zp, up,
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), G.stride(1),
+                  glva.data_ptr() if glva is not None else None, workspace.data_ptr(), workspace.numel(),
+                  _stream())
+        return G, glv, glva
     _lib.call("mgp_elbo_terms_backward", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
               var_a.data_ptr(), ldf, Y.data_ptr(), lik_var.data_ptr(),
               assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau), zp, up,
@@ -494,9 +505,10 @@ def gauss_kl_white(q_mu, q_sqrt, out=None, workspace=None):
 
 # --------------------------------------------------------------------------- K6
 def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0, n_offset=0,
-               out=None, workspace=None, assign_lik_var=None):
+               out=None, workspace=None, assign_lik_var=None, multiclass_eps=None):
     """Sum over local points of logsumexp_s(sum_k W ve) - log S (float64 [1]).
-    With assign_lik_var: the SMGPModified data term (models.py:112-123)."""
+    With assign_lik_var: the SMGPModified data term (models.py:112-123).
+    multiclass_eps: the pred likelihood is MultiClass(K) / RobustMax(eps) (lik_var unused)."""
     for t, n in ((mu_f, "mu_f"), (var_f, "var_f"), (mu_a, "mu_a"), (var_a, "var_a")):
         _check(t, n, 2)
     ldf = _ld(mu_f)
@@ -505,7 +517,9 @@ def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, se
     K, N = mu_f.shape
     dev = mu_f.device
     Y = Y.reshape(-1)
-    _check(Y, "Y"), _check(lik_var, "lik_var")
+    _check(Y, "Y")
+    if multiclass_eps is None:
+        _check(lik_var, "lik_var")
     if Y.numel() != N or not Y.is_contiguous():
         raise ValueError("Y must be contiguous with N elements")
     if out is None:
@@ -521,6 +535,15 @@ def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, se
             raise ValueError("explicit noise must be [S, N, K]")
         z, u = z.contiguous(), u.contiguous()
         zp, up = z.data_ptr(), u.data_ptr()
+    if multiclass_eps is not None:
+        if assign_lik_var is not None:
+            _check(assign_lik_var, "assign_lik_var")
+        _lib.call("mgp_elbo_terms_multiclass", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
+                  var_a.data_ptr(), ldf, Y.data_ptr(), float(multiclass_eps),
+                  assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau), zp, up,
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(), workspace.data_ptr(),
+                  workspace.numel(), _stream())
+        return out
     if assign_lik_var is not None:
         _check(assign_lik_var, "assign_lik_var")
         _lib.call("mgp_elbo_terms_modified", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
@@ -580,8 +603,9 @@ def philox_normal2(seed, n_offset, N, K, S, device):
 
 
 def predict_samples(mu_f, var_f, mu_a, var_a, lik_var, S, tau=1e-2, noise=None, seed=0,
-                    n_offset=0):
-    """samples_y, samples_f [S, N] (models.py:91-103)."""
+                    n_offset=0, multiclass_eps=None):
+    """samples_y, samples_f [S, N] (models.py:91-103); multiclass_eps: MultiClass / RobustMax
+    predictive mean / variance for samples_y (lik_var unused)."""
     K, N = mu_f.shape
     dev = mu_f.device
     sy = torch.empty(S, N, dtype=F32, device=dev)
@@ -594,7 +618,25 @@ def predict_samples(mu_f, var_f, mu_a, var_a, lik_var, S, tau=1e-2, noise=None, 
             if tuple(t.shape) != (S, N, K):
                 raise ValueError("explicit noise must be [S, N, K]")
         ptrs = [t.data_ptr() for t in noise]
+    if multiclass_eps is not None:
+        _lib.call("mgp_predict_samples_multiclass", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
+                  var_a.data_ptr(), _ld(mu_f), float(multiclass_eps), N, K, S, float(tau), *ptrs,
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), sy.data_ptr(), sf.data_ptr(), _stream())
+        return sy, sf
     _lib.call("mgp_predict_samples", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
               var_a.data_ptr(), _ld(mu_f), lik_var.data_ptr(), N, K, S, float(tau), *ptrs,
               int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), sy.data_ptr(), sf.data_ptr(), _stream())
     return sy, sf
+
+
+def multiclass_predict(fmean, fvar, epsilon):
+    """MultiClass._predict_mean_and_var (GPflow 2.7): (ps, ps - ps^2), each [N, K]."""
+    _check(fmean, "fmean", 2), _check(fvar, "fvar", 2)
+    K, N = fmean.shape
+    if _ld(fvar) != _ld(fmean):
+        raise ValueError("fmean and fvar must share a leading dimension")
+    ym = torch.empty(N, K, dtype=F32, device=fmean.device)
+    yv = torch.empty(N, K, dtype=F32, device=fmean.device)
+    _lib.call("mgp_multiclass_predict", fmean.data_ptr(), fvar.data_ptr(), _ld(fmean), N, K, float(epsilon),
+              ym.data_ptr(), yv.data_ptr(), _stream())
+    return ym, yv

@@ -61,7 +61,36 @@ def _var_exp(mu, var, y, lik_var):
     return -0.5 * math.log(2 * math.pi) - 0.5 * torch.log(lik_var) - 0.5 * ((y - mu) ** 2 + var) / lik_var
 
 
-def data_term(mu_f, var_f, mu_a, var_a, Y, lik_var, z, u, assign_lik_var=None):
+_GH_X, _GH_W = np.polynomial.hermite.hermgauss(20)
+
+
+def multiclass_var_exp(mu, var, Y, eps):
+    """GPflow 2.7.0 MultiClass/RobustMax var-exp (cpu_ref.multiclass_var_exp) on
+    [N, K] latents -> [N] (differentiable)."""
+    N, K = mu.shape
+    y = torch.as_tensor(np.asarray(Y).reshape(-1).astype(np.int64))
+    oh_on = torch.zeros(N, K, dtype=mu.dtype)
+    ok = (y >= 0) & (y < K)
+    oh_on[torch.nonzero(ok).reshape(-1), y[ok]] = 1.0
+    ss = lambda v: torch.sqrt(torch.clamp(v, min=1e-10))
+    mu_sel, var_sel = (oh_on * mu).sum(1), (oh_on * var).sum(1)
+    X = mu_sel[:, None] + torch.as_tensor(_GH_X) * ss(2.0 * var_sel)[:, None]
+    dist = (X[:, None, :] - mu[:, :, None]) / ss(var)[:, :, None]
+    cdfs = 0.5 * (1.0 + torch.erf(dist / math.sqrt(2.0)))
+    cdfs = cdfs * (1 - 2e-6) + 1e-6
+    cdfs = cdfs * (1.0 - oh_on)[:, :, None] + oh_on[:, :, None]
+    p = torch.prod(cdfs, 1) @ torch.as_tensor(_GH_W / np.sqrt(np.pi)).reshape(-1, 1)
+    return (p * math.log(1.0 - eps) + (1.0 - p) * math.log(eps / (K - 1.0))).sum(-1)
+
+
+def _pred_ve(mu_f, var_f, Y, lik_var, multiclass_eps):
+    """[1, N, K] Gaussian var-exp or [1, N, 1] MultiClass var-exp (S-invariant)."""
+    if multiclass_eps is not None:
+        return multiclass_var_exp(mu_f, var_f, Y, multiclass_eps).reshape(1, -1, 1)
+    return _var_exp(mu_f[None], var_f[None], Y.reshape(1, -1, 1), lik_var)
+
+
+def data_term(mu_f, var_f, mu_a, var_a, Y, lik_var, z, u, assign_lik_var=None, multiclass_eps=None):
     """sum_n DT_n (models.py:55-67,73-74; SMGPModified :112-123 with assign_lik_var)
     as a function of the conditionals [N, K] (the K6 boundary)."""
     S = z.shape[0]
@@ -69,7 +98,7 @@ def data_term(mu_f, var_f, mu_a, var_a, Y, lik_var, z, u, assign_lik_var=None):
     logits = mu_a[None] + z * torch.sqrt(var_a[None] + 1e-6)
     g = -torch.log(-torch.log(u))
     W = torch.softmax((g + logits) / TAU, dim=-1)
-    ve = _var_exp(mu_f[None], var_f[None], y, lik_var)
+    ve = _pred_ve(mu_f, var_f, Y, lik_var, multiclass_eps)
     data = torch.logsumexp((W * ve).sum(2), 0) - math.log(S)
     if assign_lik_var is not None:
         vea = _var_exp(mu_a[None], var_a[None], y, assign_lik_var)
@@ -77,7 +106,7 @@ def data_term(mu_f, var_f, mu_a, var_a, Y, lik_var, z, u, assign_lik_var=None):
     return data.sum()
 
 
-def elbo(X, Y, pred, assign, lik_var, z, u, num_data, assign_lik_var=None, keep=None):
+def elbo(X, Y, pred, assign, lik_var, z, u, num_data, assign_lik_var=None, keep=None, multiclass_eps=None):
     """SMGP (or SMGPModified when assign_lik_var is given) ELBO, float64 scalar.
     pred/assign: dicts of tensors (LAYER_KEYS); lik_var [K]; z, u [S, N, K].
     keep: optional dict that receives the conditional tensors (retain_grad set)."""
@@ -92,7 +121,7 @@ def elbo(X, Y, pred, assign, lik_var, z, u, num_data, assign_lik_var=None, keep=
     logits = mu_a[None] + z * torch.sqrt(var_a[None] + 1e-6)
     g = -torch.log(-torch.log(u))
     W = torch.softmax((g + logits) / TAU, dim=-1)
-    ve = _var_exp(mu_f[None], var_f[None], y, lik_var)
+    ve = _pred_ve(mu_f, var_f, Y, lik_var, multiclass_eps)
     data = torch.logsumexp((W * ve).sum(2), 0) - math.log(S)
     if assign_lik_var is not None:
         vea = _var_exp(mu_a[None], var_a[None], y, assign_lik_var)

@@ -8,6 +8,9 @@
   the kmeans inducing points of ``demos/demo_tf2.py:39`` (scipy kmeans, seeds 0/1,
   stored because scipy here is 1.15 not the pinned 1.10).  Only the arrays are
   committed; no reference source travels.
+* ``toy_datasets.npz``: the outputs of the reference's other toy generators
+  (``utils/dataset_utils.py:84-166``) that the demos load, pinning the drop-in
+  ``utils/dataset_utils.py``.
 * ``case_*.npz``: inputs, parameters, explicit noise and the float64 oracle
   outputs (ELBO, KL, per-layer fmean/fvar, predict_y, predict_assign) for the
   parity tests.  Large inputs (the c2-shaped case) are not stored: the test
@@ -42,6 +45,24 @@ def demo_data(reference):
     Z20_assign = kmeans(Xtrain[:600], 20, seed=1)[0]
     return dict(N=N, Xtrain=Xtrain, Ytrain=Ytrain, Xtest=Xtest, Z=Z, Z_assign=Z_assign,
                 Z20=Z20, Z20_assign=Z20_assign)
+
+
+def toy_datasets(reference):
+    """Outputs of the reference's own toy generators (utils/dataset_utils.py:84-166):
+    numpy Generator seed 0 for the Generator-based ones, np.random.seed(0) for the
+    global-RNG association set.  Arrays only; no reference source is stored."""
+    sys.path.insert(0, reference)
+    from utils import dataset_utils as U
+    out = {}
+    for name in ("load_toy_data_categorical", "load_toy_multimodal_data", "load_toy_2d_data",
+                 "load_toy_2d_data_categorical"):
+        N, X, Y, Xt = getattr(U, name)(np.random.default_rng(0))
+        out.update({f"{name}_N": N, f"{name}_X": X, f"{name}_Y": Y, f"{name}_Xtest": Xt})
+    np.random.seed(0)
+    N, X, Y, Xt = U.load_toy_data_assoc()
+    out.update({"load_toy_data_assoc_N": N, "load_toy_data_assoc_X": X, "load_toy_data_assoc_Y": Y,
+                "load_toy_data_assoc_Xtest": Xt})
+    return out
 
 
 def perturbed_layer(Z, var, ls, K, rng):
@@ -84,7 +105,12 @@ def pack(X, Y, p, z, u, Xtest, out, store_inputs=True, extra=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", choices=("all", "toy"), default="all",
+                    help="toy: regenerate only toy_datasets.npz")
     args = ap.parse_args()
+    np.savez_compressed(os.path.join(HERE, "toy_datasets.npz"), **toy_datasets(args.reference))
+    if args.only == "toy":
+        return
     dd = demo_data(args.reference)
     np.savez_compressed(os.path.join(HERE, "demo_tf2_data.npz"), **dd)
 

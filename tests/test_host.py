@@ -33,3 +33,24 @@ def test_dataset_pipeline_semantics():
     # a small shuffle buffer still yields a permutation per pass
     small = list(Dataset.from_tensor_slices(torch.arange(50)).shuffle(8, seed=1).batch(50))
     assert sorted(small[0].tolist()) == list(range(50))
+
+
+def test_toy_datasets_match_reference_generators():
+    """utils/dataset_utils.py (drop-in) reproduces the reference's generators
+    bit-for-bit (tests/golden/toy_datasets.npz, made by make_golden.py from the
+    reference's own utils/dataset_utils.py:84-166)."""
+    import os
+    import numpy as np
+    from utils import dataset_utils as U
+    d = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "toy_datasets.npz")))
+    for name in ("load_toy_data_categorical", "load_toy_multimodal_data", "load_toy_2d_data",
+                 "load_toy_2d_data_categorical", "load_toy_data_assoc"):
+        if name == "load_toy_data_assoc":
+            np.random.seed(0)
+            out = U.load_toy_data_assoc()
+        else:
+            out = getattr(U, name)(np.random.default_rng(0))
+        for key, got in zip(("N", "X", "Y", "Xtest"), out):
+            ref = d[f"{name}_{key}"]
+            assert np.array_equal(np.asarray(got), ref), (name, key)
+            assert np.asarray(got).dtype == ref.dtype, (name, key)

@@ -185,3 +185,91 @@ def test_grad_oracle_value_matches_cpu_oracle(modified):
     assert float(e) == pytest.approx(ref, rel=1e-10)
     e.backward()
     assert pred["q_sqrt"].grad is not None and torch.isfinite(pred["q_sqrt"].grad).all()
+
+
+# ----------------------------------------------------------------------------- MultiClass
+def _phi(x):
+    from scipy.special import erf
+    return 0.5 * (1.0 + erf(x / np.sqrt(2.0)))
+
+
+def test_robustmax_two_class_closed_form(monkeypatch):
+    """K = 2: prob_is_largest(y) = (1 - 2e-6) E[Phi((X - mu_o) / s_o)] + 1e-6 with
+    X ~ N(mu_y, v_y), i.e. (1 - 2e-6) Phi((mu_y - mu_o) / sqrt(v_y + v_o)) + 1e-6.
+    GPflow's 20-point rule meets it to ~5e-7 for comparable variances (it is an
+    approximation: up to ~2e-2 when v_y >> v_o); a 150-point rule to 1e-6."""
+    rng = np.random.default_rng(0)
+    y = rng.integers(0, 2, (200, 1))
+    yi = y.reshape(-1)
+    o, r = 1 - yi, np.arange(200)
+    mu = rng.normal(0, 1.0, (200, 2))
+    for lo, hi, tol in ((0.5, 1.5, 2e-6), (0.05, 1.5, 3e-2)):
+        var = rng.uniform(lo, hi, (200, 2))
+        p = R.robustmax_prob_is_largest(y, mu, var, 2).reshape(-1)
+        exact = (1 - 2e-6) * _phi((mu[r, yi] - mu[r, o]) / np.sqrt(var[r, yi] + var[r, o])) + 1e-6
+        assert np.max(np.abs(p - exact)) < tol
+    x150, w150 = np.polynomial.hermite.hermgauss(150)
+    monkeypatch.setattr(R, "GH_X", x150)
+    monkeypatch.setattr(R, "GH_W", w150)
+    p = R.robustmax_prob_is_largest(y, mu, var, 2).reshape(-1)
+    assert np.max(np.abs(p - exact)) < 1e-6
+
+
+def test_robustmax_class_probabilities_sum_to_one():
+    """sum_i P(i is the largest) = 1 up to the squash and the quadrature."""
+    rng = np.random.default_rng(1)
+    for K in (3, 4, 6):
+        mu = rng.normal(0, 1.0, (100, K))
+        var = rng.uniform(0.3, 1.0, (100, K))
+        tot = sum(R.robustmax_prob_is_largest(np.full((100, 1), i), mu, var, K).reshape(-1) for i in range(K))
+        assert np.max(np.abs(tot - 1.0)) < 1e-3   # squash + the 20-point rule
+
+
+def test_robustmax_limits_and_predictive():
+    """Vanishing variances: p -> 1 for the largest latent (minus the squash); an
+    out-of-range label selects no class (tf.one_hot -> zero row); the MultiClass
+    predictive mean is p (1 - eps) + (1 - p) eps / (K - 1) and sums to one."""
+    mu = np.array([[2.0, 0.0, -1.0], [0.0, 3.0, 1.0]])
+    var = np.full((2, 3), 1e-12)
+    p = R.robustmax_prob_is_largest(np.array([[0], [1]]), mu, var, 3).reshape(-1)
+    assert np.allclose(p, (1 - 2e-6) ** 2 + 2e-6 * (1 - 2e-6), atol=1e-9)
+    p_out = R.robustmax_prob_is_largest(np.array([[5], [5]]), mu, var, 3).reshape(-1)
+    assert np.all(p_out < 1e-5)
+    ps, pv = R.multiclass_predict_mean_and_var(mu, np.full((2, 3), 0.3), 3, eps=1e-3)
+    assert np.allclose(ps.sum(1), 1.0, atol=1e-4)
+    assert np.allclose(pv, ps - ps ** 2)
+    ve = R.multiclass_var_exp(mu, var, np.array([[0], [1]]), 3, eps=1e-3)
+    assert np.allclose(ve, p * np.log(1 - 1e-3) + (1 - p) * np.log(1e-3 / 2), rtol=1e-12)
+
+
+@pytest.mark.parametrize("modified", [False, True])
+def test_multiclass_grad_oracle_matches_cpu_oracle(modified):
+    """grad_ref's differentiable MultiClass var-exp and ELBO equal cpu_ref's."""
+    import torch
+    from oracle import grad_ref as G
+    rng = np.random.default_rng(2)
+    mu, var = rng.normal(0, 1, (50, 3)), rng.uniform(0.05, 1.0, (50, 3))
+    y = rng.integers(0, 3, (50, 1)).astype(np.float64)
+    ref = R.multiclass_var_exp(mu, var, y, 3, eps=1e-3)
+    got = G.multiclass_var_exp(torch.tensor(mu), torch.tensor(var), y, 1e-3).numpy()
+    assert np.allclose(got, ref, rtol=1e-12, atol=1e-12)
+    X, _, p = R.synthetic_problem(300, 12, 3, 2, 0.6, state="perturbed", S=4)
+    Y = rng.integers(0, 3, (300, 1)).astype(np.float64)
+    for L in (p.pred, p.assign):
+        for k in ("Z", "q_mu", "q_sqrt"):
+            L[k] = np.asarray(L[k]).astype(np.float32).astype(np.float64)
+    p.multiclass_eps = 1e-3
+    z, u = R.explicit_noise(4, 300, 3)
+    pred, assign, lik = G.params_from_oracle(p)
+    a_var = np.array([[0.4, 0.6, 0.8]])
+    e = G.elbo(torch.tensor(X), torch.tensor(Y), pred, assign, lik, torch.tensor(z), torch.tensor(u),
+               p.num_data, assign_lik_var=torch.tensor(a_var[0]) if modified else None, multiclass_eps=1e-3)
+    for L, T in ((p.pred, pred), (p.assign, assign)):
+        L["variance"] = float(T["variance"].detach())
+        L["lengthscales"] = T["lengthscales"].detach().numpy()
+    ref = R.smgp_modified_elbo(X, Y, p, a_var, z, u) if modified else R.smgp_elbo(X, Y, p, z, u)
+    assert float(e) == pytest.approx(ref, rel=1e-10)
+    # the multiclass pred term ignores W up to sum_k W = 1: it differs from the Gaussian one
+    p.multiclass_eps = None
+    assert abs(R.smgp_elbo(X, Y, p, z, u) - R.smgp_elbo(X, Y, R.SMGPParams(
+        p.pred, p.assign, p.lik_variance, p.num_data, p.S, multiclass_eps=1e-3), z, u)) > 1e-3
