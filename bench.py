@@ -250,7 +250,12 @@ def main():
     k5_products = args.planes * (args.planes + 1) // 2   # 6 / 3 / 1 bf16 MFMA products per f32 product
     peak_k5 = PEAK_BF16_MFMA / k5_products if x6 else PEAK_F32_MFMA
     from modulatedgps_amd.distributed import init_from_env
-    rank, world, local = init_from_env("nccl")
+    # MGP_BENCH_BACKEND=gloo + MGP_BENCH_SHARE_GPU=1: rehearsal of the multi-rank path
+    # with every rank on cuda:0 (a one-GPU box); the driver's runs use RCCL, one GPU per rank
+    share = os.environ.get("MGP_BENCH_SHARE_GPU") == "1"
+    if share:
+        os.environ["LOCAL_RANK"] = "0"
+    rank, world, local = init_from_env(os.environ.get("MGP_BENCH_BACKEND", "nccl"))
     group = torch.distributed.group.WORLD if world > 1 else None
     device = torch.device("cuda", local if world > 1 else 0)
     cfg = CONFIGS[args.config]
