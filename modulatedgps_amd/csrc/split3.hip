@@ -471,71 +471,83 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restri
 // f32 K4: stats[st][0][n] = sum A^2, stats[st][1 + kk][n] = sum A q_mu[., kk]).
 template <int KMAX>
 __device__ __forceinline__ void trsm_stats_x6_item(
-    bf16x8 (*sL)[4 * 3 * 64], int t, int tn, const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes,
-    const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
+    bf16x8 (*sL)[4 * 3 * 64], float* __restrict__ sQ, int t, int tn, const bf16x8* __restrict__ Tfr,
+    uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
     const float* __restrict__ q_mu, int64_t ldq, int K, bf16x8* __restrict__ Afr, float* __restrict__ stats,
     int64_t lds_, float* __restrict__ Af32, int64_t lda) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t i0 = 128 * (int64_t)t;
+  // q_mu rows of this row tile -> LDS [128][KMAX] before the main loop (whose
+  // barriers publish it), so the epilogue never waits on a global load
+  if (stats) {
+    for (int idx = threadIdx.x; idx < 128 * KMAX; idx += 256) {
+      const int r = idx / KMAX, kk = idx % KMAX;
+      sQ[idx] = (i0 + r < M && kk < K) ? q_mu[(i0 + r) * ldq + kk] : 0.f;
+    }
+  }
   floatx16 acc[4][2];
   x6_mainloop<2>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
               img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8,
               nmk);
-
-  // ---- A image
+  if (Af32) store_acc_f32(acc, Af32, lda, i0, (int64_t)tn * kX6BN, M, N, nullptr);
+  // ---- epilogue by 32-row sub-tile i: the A image fragments of acc[i] and its
+  // contribution to the stats of 64-row stats tile i / 2 (stats[st][0][n] = sum A^2,
+  // stats[st][1 + kk][n] = sum A q_mu[., kk]); acc[i] dies after its sub-tile, which
+  // keeps the live set to the remaining accumulators + 2 (1 + KMAX) sums (no spills)
+  float a2[2], qm[2][KMAX];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int64_t nb = 8 * (int64_t)tn + 2 * w + c;
       const int64_t mk = 8 * (int64_t)t + 2 * i;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s2 = 0; s2 < 2; ++s2) {
         float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s + j];
-        store_split(Afr + ((nb * nmk + mk + s) * 3) * 64 + lane, v);
+        for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j];
+        store_split(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v);
       }
     }
-  if (Af32) store_acc_f32(acc, Af32, lda, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
-  if (!stats) return;
-  // ---- stats (rows beyond M are zero in A; tiles starting at or beyond M are not stored)
-  const int64_t i0 = 128 * (int64_t)t;
-  float* sQ = reinterpret_cast<float*>(&sL[0][0]);  // [128][KMAX]; the main loop ended on a barrier
-  for (int idx = threadIdx.x; idx < 128 * KMAX; idx += 256) {
-    const int r = idx / KMAX, kk = idx % KMAX;
-    sQ[idx] = (i0 + r < M && kk < K) ? q_mu[(i0 + r) * ldq + kk] : 0.f;
-  }
-  __syncthreads();
-  // one (column sub-tile, stats tile) at a time keeps 1 + KMAX accumulators live
+    if (!stats) continue;
+    if ((i & 1) == 0) {
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int64_t n = (int64_t)tn * kX6BN + 64 * w + 32 * c + (lane & 31);
+      for (int c = 0; c < 2; ++c) {
+        a2[c] = 0.f;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      float a2 = 0.f, qm[KMAX];
+        for (int kk = 0; kk < KMAX; ++kk) qm[c][kk] = 0.f;
+      }
+    }
 #pragma unroll
-      for (int kk = 0; kk < KMAX; ++kk) qm[kk] = 0.f;
+    for (int e = 0; e < 16; ++e) {
+      const int lr = 32 * i + acc_row(e, lane);
+      const float v0 = acc[i][0][e], v1 = acc[i][1][e];
+      a2[0] = fmaf(v0, v0, a2[0]);
+      a2[1] = fmaf(v1, v1, a2[1]);
 #pragma unroll
-      for (int i = 2 * hh; i < 2 * hh + 2; ++i)
+      for (int kk = 0; kk < KMAX; ++kk) {
+        const float q = sQ[lr * KMAX + kk];
+        qm[0][kk] = fmaf(v0, q, qm[0][kk]);
+        qm[1][kk] = fmaf(v1, q, qm[1][kk]);
+      }
+    }
+    if (i & 1) {
+      const int64_t st = 2 * (int64_t)t + (i >> 1);
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int lr = 32 * i + acc_row(e, lane);
-          const float v = acc[i][c][e];
-          a2 = fmaf(v, v, a2);
+      for (int c = 0; c < 2; ++c) {
+        const int64_t n = (int64_t)tn * kX6BN + 64 * w + 32 * c + (lane & 31);
+        const float s_a2 = a2[c] + __shfl_xor(a2[c], 32, 64);
+        float s_qm[KMAX];
 #pragma unroll
-          for (int kk = 0; kk < KMAX; ++kk) qm[kk] = fmaf(v, sQ[lr * KMAX + kk], qm[kk]);
+        for (int kk = 0; kk < KMAX; ++kk) s_qm[kk] = qm[c][kk] + __shfl_xor(qm[c][kk], 32, 64);
+        if (lane < 32 && n < N && 64 * st < M) {
+          float* dst = stats + st * (K + 1) * lds_ + n;
+          dst[0] = s_a2;
+#pragma unroll
+          for (int kk = 0; kk < KMAX; ++kk)
+            if (kk < K) dst[(int64_t)(1 + kk) * lds_] = s_qm[kk];
         }
-      a2 += __shfl_xor(a2, 32, 64);
-#pragma unroll
-      for (int kk = 0; kk < KMAX; ++kk) qm[kk] += __shfl_xor(qm[kk], 32, 64);
-      const int64_t st = 2 * (int64_t)t + hh;
-      if (lane < 32 && n < N && 64 * st < M) {
-        float* dst = stats + st * (K + 1) * lds_ + n;
-        dst[0] = a2;
-#pragma unroll
-        for (int kk = 0; kk < KMAX; ++kk)
-          if (kk < K) dst[(int64_t)(1 + kk) * lds_] = qm[kk];
       }
     }
   }
@@ -543,23 +555,24 @@ __device__ __forceinline__ void trsm_stats_x6_item(
 
 // One workgroup per (pair of row tiles t, nT - 1 - t; column tile tn): the
 // pair holds 8 t + 8 + 8 (nT - t) = 8 nT + 16 k-steps whatever t, so every
-// workgroup has the same work (the single-item grid left a tail of 64-step
-// items); both items read the same Kuf column slab.  Odd nT: the middle row
-// tile is an item alone.
+// workgroup has the same work; both items read the same Kuf column slab.  Odd
+// nT: the middle row tile is an item alone.  (c3: 385 us vs 439 us for one item
+// per workgroup, whose register count stays below 256 without spills.)
 template <int KMAX>
 __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
     const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
     int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
     bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
+  __shared__ float sQ[128 * KMAX];
   const int nT = nmk / 8, nP = (nT + 1) / 2;
   int p, tn;
   col_major_item(blockIdx.x, nP, nTn, p, tn);
-  trsm_stats_x6_item<KMAX>(sL, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr,
+  trsm_stats_x6_item<KMAX>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr,
                            stats, lds_, Af32, lda);
   if (nT - 1 - p == p) return;
-  __syncthreads();  // the epilogue's LDS reads before the next main loop's LDS stores
-  trsm_stats_x6_item<KMAX>(sL, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
+  __syncthreads();  // the epilogue's sQ reads before the next item's sQ stores
+  trsm_stats_x6_item<KMAX>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
                            lds_, Af32, lda);
 }
 
