@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--planes", type=int, default=3, choices=(1, 2, 3),
                     help="bf16 planes per operand in K5 (3: f32-accurate x6, the default; 2 / 1: the "
                          "'bf16 mixed' modes of BASELINE config 5, reported with their measured tolerance)")
+    ap.add_argument("--format", default=None, choices=("x6", "f16"),
+                    help="image format of the forward K4 -> K5 hand-off: x6 (split-bf16, 6 products) or f16 "
+                         "(split-f16, 3 products, 22-bit operands); default: modulatedgps_amd.config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-modes", action="store_true", help="skip the reduced-plane K5 side measurements")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (ELBO + gradient + Adam) leg")
@@ -182,13 +185,27 @@ def load_traffic(kernel):
     return e.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
-def k5_modes_leg(elbo_step, args, steps=10):
-    """Side measurement (never the headline): the same ELBO step with K5 on 2 and 1
-    bf16 planes (BASELINE config 5's 'bf16 mixed'); their measured fvar error vs the
-    float64 oracle at c3 shapes is asserted in tests/test_gpu_kernels.py::
-    test_expert_conditional_planes (2 planes ~3e-6, 1 plane ~2e-3 normwise)."""
-    from modulatedgps_amd.config import set_expert_planes
+def k5_modes_leg(elbo_step, args, fmt, steps=10):
+    """Side measurement (never the headline): the same ELBO step with the other
+    f32-accurate image format, and with K5 on 2 and 1 bf16 planes (BASELINE config
+    5's 'bf16 mixed'); their measured fvar error vs the float64 oracle at c3 shapes
+    is asserted in tests/test_gpu_kernels.py::test_expert_conditional_planes (2
+    planes ~3e-6, 1 plane ~2e-3 normwise) and tests/test_gpu_f16.py."""
+    from modulatedgps_amd.config import set_expert_format, set_expert_planes
     out = {}
+    other = "x6" if fmt == "f16" else "f16"
+    set_expert_format(other)
+    for _ in range(2):
+        elbo_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        elbo_step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out[other] = {"value": 1.0 / dt, "unit": "ELBO steps/s", "ms_per_step": dt * 1e3,
+                  "k5_products": 6 if other == "x6" else 3, "accuracy": "f32 class (tests/test_gpu_f16.py)"}
+    set_expert_format("x6")
     for planes in (2, 1):
         set_expert_planes(planes)
         for _ in range(2):
@@ -203,6 +220,7 @@ def k5_modes_leg(elbo_step, args, steps=10):
                                   "k5_products": planes * (planes + 1) // 2,
                                   "fvar_normwise_err_vs_f64": {2: "3.3e-6", 1: "2.1e-3"}[planes]}
     set_expert_planes(3)
+    set_expert_format(fmt)
     return out
 
 
@@ -244,10 +262,14 @@ def train_leg(model, X, Y, kw, args, barrier, world, device):
 
 def main():
     args = parse()
-    from modulatedgps_amd.config import conditional_mode, set_expert_planes
+    from modulatedgps_amd.config import conditional_mode, expert_format, set_expert_format, set_expert_planes
     x6 = conditional_mode() == "x6"
     set_expert_planes(args.planes)
-    k5_products = args.planes * (args.planes + 1) // 2   # 6 / 3 / 1 bf16 MFMA products per f32 product
+    fmt = args.format or expert_format()
+    set_expert_format(fmt)
+    f16 = x6 and fmt == "f16" and args.planes == 3
+    # 6 / 3 / 1 bf16 MFMA products per f32 product; split-f16: 3 f16 products (same rate)
+    k5_products = 3 if f16 else args.planes * (args.planes + 1) // 2
     peak_k5 = PEAK_BF16_MFMA / k5_products if x6 else PEAK_F32_MFMA
     from modulatedgps_amd.distributed import init_from_env
     # MGP_BENCH_BACKEND=gloo + MGP_BENCH_SHARE_GPU=1: rehearsal of the multi-rank path
@@ -342,7 +364,9 @@ def main():
                 "unit": "TFLOP/s", "frac": ek.get("frac"), "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_per_launch": f"K*M^2*N = {expert_flops:.4g} f32 flop",
-                "peak_note": (f"split-bf16: each f32 product is {k5_products} bf16 MFMA products, peak = "
+                "peak_note": ("split-f16: each f32 product is 3 f16 MFMA products, peak = 2.5 PF f16 dense / 3"
+                              if f16 else
+                              f"split-bf16: each f32 product is {k5_products} bf16 MFMA products, peak = "
                               f"2.5 PF bf16 dense / {k5_products}" if x6 else "f32 MFMA dense peak")}
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -350,7 +374,7 @@ def main():
     train = None if (args.no_train or expert) else train_leg(model, X, Y, kw, args, barrier, world, device)
     modes = None
     if world == 1 and x6 and args.planes == 3 and not args.no_modes:
-        modes = k5_modes_leg(elbo_step, args)
+        modes = k5_modes_leg(elbo_step, args, fmt)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, tuple(args.cpu_sample))
@@ -363,7 +387,10 @@ def main():
             "scaling": "strong" if expert else "weak", "vs_baseline": None,
             "dtype": {3: "f32", 2: "f32/bf16x3 mixed", 1: "f32/bf16 mixed"}[args.planes] if x6 else "f32",
             "data": "synthetic",
-            "dtype_note": (("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
+            "dtype_note": (("f32 operands and accumulation; K1/K4 products on bf16 MFMA via an exact 3-plane "
+                            "split (6 products); K5 on f16 MFMA via a scaled 2-plane fp16 split (22-bit "
+                            "operands, 3 products); K3 in f64") if f16 else
+                           ("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
                             "3-plane split (6 products, f32-accurate); K3 in f64") if x6 and args.planes == 3 else
                            (f"K1-K4 f32-accurate (x6 split-bf16), K5 on the leading {args.planes} bf16 plane(s) "
                             f"({k5_products} product(s), f32 accumulation); K3 in f64") if x6 else
@@ -382,6 +409,7 @@ def main():
             "cpu_baseline": cpu,
             "train": train,
             "k5_modes": modes,
+            "k5_image_format": fmt if x6 else None,
             "elbo": elbo_val, "cholesky_info": info,
         }
         print(json.dumps(out))

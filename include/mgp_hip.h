@@ -175,6 +175,33 @@ int mgp_expert_conditional_planes(const void* Afr, size_t afr_bytes, const void*
                                   int64_t N, int32_t K, int32_t planes, float* fmean, float* fvar,
                                   int64_t ldf, void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 
+/* ---------------------------------------------------------------- K5, split-f16 ("f16x3")
+ * The same conditional from split-f16 images: each operand, scaled by a power
+ * of two 2^e that puts its largest magnitude in [2^13, 2^14), is split into
+ * fp16 hi + lo (22 significant bits) and a product is the three f16 MFMA plane
+ * products hi.hi + hi.lo + lo.hi (dropped lo.lo <= 2^-22 of it), f32-accumulated:
+ * half the matrix-core work of x6 at an operand error of 2^-22 (x6: 2^-24,
+ * the f32 input rounding itself).  Same buffer sizes as the x6 images; the
+ * image trailer (after the planes) carries the bound from which e is derived.
+ *   mgp_split_lower_f16:   q_sqrt -> Lfr (bound = max |tril(q_sqrt)|, computed on device);
+ *   mgp_split_cols_f16:    A -> Afr (bound = max |A|);
+ *   mgp_trsm_stats_x6_f16: K4 as mgp_trsm_stats_x6 (x6 inputs) writing A's
+ *       split-f16 image, bound sqrt(variance) (|A[m][n]| <= sqrt(k(x_n, x_n)));
+ *   mgp_expert_conditional_f16: K5 on the two split-f16 images, outputs and
+ *       workspace as mgp_expert_conditional_x6.
+ * Replaces the same call sites (GPflow base_conditional, models.py:141-143). */
+int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
+                        void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
+int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr, size_t afr_bytes,
+                       mgp_stream_t stream);
+int mgp_trsm_stats_x6_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
+                          int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
+                          void* Afr, size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream);
+int mgp_expert_conditional_f16(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                               const float* stats, int64_t lds, const float* variance, int64_t M,
+                               int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                               void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+
 /* ---------------------------------------------------------------- backward of K1-K5
  * Gram products over the data dimension (float32 MFMA, deterministic split-K):
  *   out[i][j] = alpha * sum_n X[i][n] Y[j][n]   (tri != 0: j <= i only, zeros above)

@@ -96,6 +96,12 @@ SIGNATURES = {
     "mgp_expert_conditional_planes": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
                                                      c_i64, c_i32, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
                                                      c_ptr]),
+    "mgp_split_lower_f16": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_size, c_ptr]),
+    "mgp_split_cols_f16": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_trsm_stats_x6_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
+                                             c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr]),
+    "mgp_expert_conditional_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
+                                                  c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_kl_workspace_bytes": (c_size, [c_i64, c_i32]),
     "mgp_gauss_kl_white": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr,
                                           c_ptr, c_size, c_ptr]),

@@ -12,8 +12,16 @@ import torch
 # expert_planes (x6 mode): bf16 planes per operand in K5 -- 3 (default: six
 #              products, f32-accurate), 2 (three products, ~16-bit operands) or
 #              1 (bf16 operands): BASELINE config 5's "bf16 mixed" (K1-K4 stay x6).
+# expert_format (x6 mode, forward evaluations): the A and tril(q_sqrt) images K5
+#              reads -- "f16" (default: split-f16, three f16 products at 22-bit
+#              operands; csrc/mgp_common.hpp) or "x6" (split-bf16, six bf16
+#              products).  Both measure the same error against the float64 oracle
+#              (tests/test_gpu_f16.py: 1.0e-7 normwise on K5's term, 7.3e-7 on fvar
+#              at c3 shapes -- the f32 inputs' own rounding); f16 is half the MFMA
+#              work.  The training step and the reduced-plane modes use "x6".
 _CFG = {"jitter": 1e-6, "device": None, "conditional": os.environ.get("MGP_CONDITIONAL", "x6"),
-        "expert_planes": int(os.environ.get("MGP_K5_PLANES", "3"))}
+        "expert_planes": int(os.environ.get("MGP_K5_PLANES", "3")),
+        "expert_format": os.environ.get("MGP_K5_FORMAT", "f16")}
 
 
 def default_jitter():
@@ -58,3 +66,21 @@ def set_expert_planes(planes):
     if planes not in (1, 2, 3):
         raise ValueError("expert_planes must be 1, 2 or 3")
     _CFG["expert_planes"] = int(planes)
+
+
+def expert_format():
+    return _CFG["expert_format"]
+
+
+def set_expert_format(fmt):
+    if fmt not in ("x6", "f16"):
+        raise ValueError("expert_format must be 'x6' or 'f16'")
+    _CFG["expert_format"] = fmt
+
+
+def forward_image_format(train=False):
+    """Image format of the forward K4 -> K5 hand-off: "f16" only for forward-only
+    evaluations at full planes with expert_format() == "f16"."""
+    if train or expert_planes() != 3:
+        return "x6"
+    return expert_format()

@@ -98,6 +98,53 @@ __device__ __forceinline__ floatx16 mfma_planes(const bf16x8 (&a)[3], const bf16
   }
 }
 
+// ------------------------------------------------------------------ split-f16 ("f16x3") images
+// Same fragment geometry, planes 0 and 1 hold fp16 hi / lo of x 2^e (plane 2
+// unused): x 2^e = hi + lo + |x 2^e| 2^-22 at most, and the product
+// a b ~ a_hi b_hi + a_hi b_lo + a_lo b_hi drops a_lo b_lo (<= 2^-22 of it):
+// three v_mfma_f32_32x32x16_f16 per block instead of six bf16 ones.  The image
+// scale e (a power of two, so exact) keeps the operand's largest magnitude in
+// [2^13, 2^14): hi never overflows (4x headroom below 65504) and lo stays a
+// normal fp16 down to 2^-16 of that maximum.  e comes from the image trailer
+// (the float bound |x| <= trailer, see img_exp) that the producer writes.
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int img_exp(float bound) {
+  if (!(bound > 0.f) || !(bound < 3.0e38f)) return 0;  // zero / inf / nan: unscaled
+  return 13 - ilogbf(bound);
+}
+
+__device__ __forceinline__ void store_split_f16(bf16x8* __restrict__ dst, const float (&v)[8], float scale) {
+  halfx8 h, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = v[j] * scale;
+    const _Float16 hi = (_Float16)x;
+    h[j] = hi;
+    l[j] = (_Float16)(x - (float)hi);  // exact difference in f32
+  }
+  dst[0] = __builtin_bit_cast(bf16x8, h);
+  dst[64] = __builtin_bit_cast(bf16x8, l);
+}
+
+__device__ __forceinline__ floatx16 mfma_f16(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c,
+                                                0, 0, 0);
+}
+
+// F16 images (NPL = 2): a_hi b_hi + a_hi b_lo + a_lo b_hi, smallest first.
+template <int NPL, bool F16>
+__device__ __forceinline__ floatx16 mfma_fmt(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 acc) {
+  if constexpr (F16) {
+    static_assert(NPL == 2, "f16 images have two planes");
+    acc = mfma_f16(a[1], b[0], acc);
+    acc = mfma_f16(a[0], b[1], acc);
+    return mfma_f16(a[0], b[0], acc);
+  } else {
+    return mfma_planes<NPL>(a, b, acc);
+  }
+}
+
 // ------------------------------------------------------------------ reductions
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

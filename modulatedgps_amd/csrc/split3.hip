@@ -38,6 +38,7 @@
 // straight from global into registers one k-step ahead; 48 MFMAs per wave.
 // The triangle is exploited at row-tile granularity (k-steps start at 128 t);
 // the zero blocks inside the diagonal tile come from Lfr's zero fill.
+#include <algorithm>
 #include <type_traits>
 
 #include "mgp_common.hpp"
@@ -53,10 +54,12 @@ constexpr int kFragBytes = 1024;
 // (upper: LinvT, K4's T[k][i] = L^-T[k][i]).  One wave per fragment block
 // (b, mb, mk): grid.x = batch * nmb * nmk / 4.
 // TRANS: the source is stored transposed (element (m, m') read at S[m' ld + m]).
+// bound != nullptr: split-f16 image, scaled by 2^img_exp(*bound).
 template <bool LOWER, bool TRANS = false, bool FULL = false>
 __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict__ src, int64_t ld,
                                                         int64_t stride, int64_t M, int nmb, int nmk,
-                                                        int64_t nfrag, bf16x8* __restrict__ img) {
+                                                        int64_t nfrag, bf16x8* __restrict__ img,
+                                                        const float* __restrict__ bound = nullptr) {
   const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= nfrag) return;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -73,13 +76,17 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
     const bool keep = FULL || (LOWER ? (m >= mc) : (m <= mc));
     v[j] = (m < M && mc < M && keep) ? S[TRANS ? mc * ld + m : m * ld + mc] : 0.f;
   }
-  store_split(img + f * 3 * 64 + lane, v);
+  if (bound)
+    store_split_f16(img + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
+  else
+    store_split(img + f * 3 * 64 + lane, v);
 }
 
 // One wave per fragment block (nb, mk): grid.x = nnb * nmk / 4.
 __global__ __launch_bounds__(256) void split_cols_kernel(const float* __restrict__ A, int64_t lda, int64_t M,
                                                          int64_t N, int nmk, int64_t nfrag,
-                                                         bf16x8* __restrict__ Afr) {
+                                                         bf16x8* __restrict__ Afr,
+                                                         const float* __restrict__ bound = nullptr) {
   const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= nfrag) return;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -91,7 +98,34 @@ __global__ __launch_bounds__(256) void split_cols_kernel(const float* __restrict
     const int64_t m = 16 * (int64_t)mk + kperm(h, j);
     v[j] = (m < M && n < N) ? A[m * lda + n] : 0.f;
   }
-  store_split(Afr + f * 3 * 64 + lane, v);
+  if (bound)
+    store_split_f16(Afr + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
+  else
+    store_split(Afr + f * 3 * 64 + lane, v);
+}
+
+// max |x| over a batch of row-major matrices (rows x cols, LOWER: entries with
+// column <= row only) -> *out as float bits through atomicMax (non-negative
+// floats order as their bit patterns; *out zeroed beforehand).  One wave per row.
+template <bool LOWER>
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ src, int64_t ld, int64_t stride,
+                                                     int64_t rows, int64_t cols, int64_t nrows_total,
+                                                     unsigned int* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  float m = 0.f;
+  for (int64_t gr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); gr < nrows_total; gr += (int64_t)gridDim.x * 4) {
+    const int64_t b = gr / rows, r = gr % rows;
+    const float* row = src + b * stride + r * ld;
+    const int64_t nc = LOWER ? (r + 1 < cols ? r + 1 : cols) : cols;
+    for (int64_t c = lane; c < nc; c += 64) m = fmaxf(m, fabsf(row[c]));
+  }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 8, 64));
+  m = fmaxf(m, __shfl_xor(m, 4, 64));
+  m = fmaxf(m, __shfl_xor(m, 2, 64));
+  m = fmaxf(m, __shfl_xor(m, 1, 64));
+  if (lane == 0) atomicMax(out, __float_as_uint(m));
 }
 
 __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -150,7 +184,8 @@ using ic = std::integral_constant<int, V>;
 // NC: column sub-tiles (32 wide) per wave (B blocks nb0 .. nb0 + NC - 1).
 // NPL: planes used (3 = x6 products; 2, 1 = K5's reduced modes, mfma_planes):
 // only those planes are loaded and staged.
-template <int DIAG, int NC = 2, int NPL = 3>
+// F16: the images are split-f16 (mfma_fmt), NPL must be 2.
+template <int DIAG, int NC = 2, int NPL = 3, bool F16 = false>
 __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)[4 * 3 * 64],
                                             __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
                                             __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
@@ -203,7 +238,7 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
 #pragma unroll
       for (int p = 0; p < NPL; ++p) a[p] = sL[buf][(i * 3 + p) * 64 + lane];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[i][c] = mfma_planes<NPL>(a, b[c], acc[i][c]);
+      for (int c = 0; c < NC; ++c) acc[i][c] = mfma_fmt<NPL, F16>(a, b[c], acc[i][c]);
     }
   };
 
@@ -258,13 +293,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const void* p, uint32
 }
 
 // ------------------------------------------------------------------ K5 (x6)
-template <int NPL>
+// F16: split-f16 images (NPL = 2) scaled by 2^img_exp(*a_bound), 2^img_exp(*l_bound).
+template <int NPL, bool F16 = false>
 __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
                                                                 const bf16x8* __restrict__ Lfr,
                                                                 uint32_t afr_bytes, uint32_t lfr_bytes,
                                                                 int nmk, int nmb, int nTn, int K,
                                                                 int64_t N, float* __restrict__ part,
-                                                                int64_t ldp) {
+                                                                int64_t ldp, const float* __restrict__ a_bound,
+                                                                const float* __restrict__ l_bound) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];  // 2 x 12 KiB: [row sub-tile][plane][lane]
   int t, tn, k;
   x6_item(blockIdx.x, nTn, K, t, tn, k);
@@ -272,12 +309,14 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   floatx16 acc[4][2];
-  x6_mainloop<1, 2, NPL>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+  x6_mainloop<1, 2, NPL, F16>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
               img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
   const int64_t nbase = (int64_t)tn * kX6BN + 64 * w + (lane & 31);
   float* dst = part + ((int64_t)k * nTp + t) * ldp;
+  float unscale = 1.f;
+  if constexpr (F16) unscale = ldexpf(1.f, -2 * (img_exp(*a_bound) + img_exp(*l_bound)));
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     float s = 0.f;
@@ -286,6 +325,7 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
 #pragma unroll
       for (int e = 0; e < 16; ++e) s = fmaf(acc[i][c][e], acc[i][c][e], s);
     s += __shfl_xor(s, 32, 64);
+    if constexpr (F16) s *= unscale;
     const int64_t n = nbase + 32 * c;
     if (lane < 32 && n < N) dst[n] = s;
   }
@@ -469,15 +509,20 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restri
 // (registers 8 s .. 8 s + 7 of each 32x32 tile are one B fragment of K5) and
 // the stats of the two 64-row stats tiles 2 t, 2 t + 1 (same layout as the
 // f32 K4: stats[st][0][n] = sum A^2, stats[st][1 + kk][n] = sum A q_mu[., kk]).
-template <int KMAX>
+// a_var != nullptr: A's image is split-f16, scaled by 2^img_exp(sqrt(*a_var))
+// (|A[m][n]| <= ||A[:, n]|| <= sqrt(k(x_n, x_n)) = sqrt(variance): the Nystrom
+// bound; the image trailer a_bound receives sqrt(*a_var) for the consumer).
+template <int KMAX, bool F16OUT = false>
 __device__ __forceinline__ void trsm_stats_x6_item(
     bf16x8 (*sL)[4 * 3 * 64], float* __restrict__ sQ, int t, int tn, const bf16x8* __restrict__ Tfr,
     uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
     const float* __restrict__ q_mu, int64_t ldq, int K, bf16x8* __restrict__ Afr, float* __restrict__ stats,
-    int64_t lds_, float* __restrict__ Af32, int64_t lda) {
+    int64_t lds_, float* __restrict__ Af32, int64_t lda, const float* __restrict__ a_var) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = 128 * (int64_t)t;
+  float a_scale = 1.f;
+  if constexpr (F16OUT) a_scale = ldexpf(1.f, img_exp(sqrtf(*a_var)));
   // q_mu rows of this row tile -> LDS [128][KMAX] before the main loop (whose
   // barriers publish it), so the epilogue never waits on a global load
   if (stats) {
@@ -507,7 +552,10 @@ __device__ __forceinline__ void trsm_stats_x6_item(
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j];
-        store_split(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v);
+        if constexpr (F16OUT)
+          store_split_f16(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v, a_scale);
+        else
+          store_split(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v);
       }
     }
     if (!stats) continue;
@@ -558,22 +606,25 @@ __device__ __forceinline__ void trsm_stats_x6_item(
 // workgroup has the same work; both items read the same Kuf column slab.  Odd
 // nT: the middle row tile is an item alone.  (c3: 385 us vs 439 us for one item
 // per workgroup, whose register count stays below 256 without spills.)
-template <int KMAX>
+template <int KMAX, bool F16OUT = false>
 __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
     const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
     int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
-    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda) {
+    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda,
+    const float* __restrict__ a_var, float* __restrict__ a_bound) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   __shared__ float sQ[128 * KMAX];
   const int nT = nmk / 8, nP = (nT + 1) / 2;
   int p, tn;
+  if constexpr (F16OUT)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a_bound = sqrtf(*a_var);
   col_major_item(blockIdx.x, nP, nTn, p, tn);
-  trsm_stats_x6_item<KMAX>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr,
-                           stats, lds_, Af32, lda);
+  trsm_stats_x6_item<KMAX, F16OUT>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq,
+                                   K, Afr, stats, lds_, Af32, lda, a_var);
   if (nT - 1 - p == p) return;
   __syncthreads();  // the epilogue's sQ reads before the next item's sQ stores
-  trsm_stats_x6_item<KMAX>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
-                           lds_, Af32, lda);
+  trsm_stats_x6_item<KMAX, F16OUT>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr,
+                                   stats, lds_, Af32, lda, a_var);
 }
 
 }  // namespace mgp
@@ -583,15 +634,26 @@ using namespace mgp;
 static int64_t x6_mp(int64_t M) { return (M + kX6BM - 1) / kX6BM * kX6BM; }
 static int64_t x6_np(int64_t N) { return (N + kX6BN - 1) / kX6BN * kX6BN; }
 
-extern "C" size_t mgp_x6_lower_bytes(int64_t M, int32_t K) {
-  if (M <= 0 || K <= 0) return 0;
+// Image = fragment planes + a 256-byte trailer whose first float is the
+// split-f16 scale bound (unused by split-bf16 images).
+constexpr size_t kTrailer = 256;
+static size_t lower_planes(int64_t M, int32_t K) {
   const int64_t Mp = x6_mp(M);
   return (size_t)K * (size_t)(Mp / 32) * (size_t)(Mp / 16) * 3 * kFragBytes;
+}
+static size_t cols_planes(int64_t M, int64_t N) {
+  return (size_t)(x6_np(N) / 32) * (size_t)(x6_mp(M) / 16) * 3 * kFragBytes;
+}
+static float* trailer(void* img, size_t planes) { return (float*)((char*)img + planes); }
+
+extern "C" size_t mgp_x6_lower_bytes(int64_t M, int32_t K) {
+  if (M <= 0 || K <= 0) return 0;
+  return lower_planes(M, K) + kTrailer;
 }
 
 extern "C" size_t mgp_x6_cols_bytes(int64_t M, int64_t N) {
   if (M <= 0 || N <= 0) return 0;
-  return (size_t)(x6_np(N) / 32) * (size_t)(x6_mp(M) / 16) * 3 * kFragBytes;
+  return cols_planes(M, N) + kTrailer;
 }
 
 extern "C" int mgp_split_lower_x6(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
@@ -656,7 +718,7 @@ extern "C" size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K)
 static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
                               const float* stats, int64_t lds, const float* variance, int64_t M, int64_t N,
                               int32_t K, int planes, float* fmean, float* fvar, int64_t ldf, void* workspace,
-                              size_t workspace_bytes, mgp_stream_t stream) {
+                              size_t workspace_bytes, mgp_stream_t stream, bool f16 = false) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!Lfr) return -3;
@@ -681,14 +743,18 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
   const int64_t ldp = (N + 3) / 4 * 4;
   float* part = (float*)workspace;
   const dim3 grid((unsigned)(K * nTp * nTn));
-#define MGP_K5_CASE(NP)                                                                                 \
-  if (planes == NP)                                                                                     \
-    hipLaunchKernelGGL(expert_cond_x6_kernel<NP>, grid, dim3(256), 0, s, (const bf16x8*)Afr,            \
+  const float* a_bound = trailer(const_cast<void*>(Afr), cols_planes(M, N));
+  const float* l_bound = trailer(const_cast<void*>(Lfr), lower_planes(M, K));
+#define MGP_K5_CASE(NP, F16)                                                                            \
+  if (planes == NP && f16 == F16)                                                                       \
+    hipLaunchKernelGGL((expert_cond_x6_kernel<NP, F16>), grid, dim3(256), 0, s, (const bf16x8*)Afr,     \
                        (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N),                           \
-                       (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N, part, ldp);
-  MGP_K5_CASE(3)
-  MGP_K5_CASE(2)
-  MGP_K5_CASE(1)
+                       (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N, part, ldp, a_bound,     \
+                       l_bound);
+  MGP_K5_CASE(3, false)
+  MGP_K5_CASE(2, false)
+  MGP_K5_CASE(1, false)
+  MGP_K5_CASE(2, true)
 #undef MGP_K5_CASE
   int st = launch_status();
   if (st) return st;
@@ -718,12 +784,19 @@ extern "C" int mgp_expert_conditional_planes(const void* Afr, size_t afr_bytes, 
 template <int KMAX>
 static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb, int64_t M, int64_t N,
                           const float* q_mu, int64_t ldq, int K, void* Afr, float* stats, int64_t lds,
-                          float* A, int64_t lda, hipStream_t s) {
+                          float* A, int64_t lda, hipStream_t s, const float* a_var = nullptr) {
   const int64_t Mp = x6_mp(M);
   const int nmk = (int)(Mp / 16), nT = (int)(Mp / kX6BM), nTn = (int)(x6_np(N) / kX6BN);
-  hipLaunchKernelGGL(trsm_stats_x6_kernel<KMAX>, dim3((unsigned)((nT + 1) / 2 * nTn)), dim3(256), 0, s,
-                     (const bf16x8*)Tfr, (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu,
-                     ldq, K, (bf16x8*)Afr, stats, lds, A, lda);
+  const dim3 grid((unsigned)((nT + 1) / 2 * nTn));
+  float* a_bound = trailer(Afr, cols_planes(M, N));
+  if (a_var)
+    hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
+                       (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
+                       (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound);
+  else
+    hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, false>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
+                       (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
+                       (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound);
   return launch_status();
 }
 
@@ -754,6 +827,99 @@ extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* 
   if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s);
   if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s);
   return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s);
+}
+
+// ------------------------------------------------------------------ split-f16 ("f16x3") K5 path
+extern "C" int mgp_trsm_stats_x6_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes,
+                                     int64_t M, int64_t N, const float* q_mu, int64_t ldq, int32_t K,
+                                     const float* variance, void* Afr, size_t afr_bytes, float* stats,
+                                     int64_t lds, mgp_stream_t stream) {
+  if (!Tfr) return -1;
+  if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return -2;
+  if (!Kfr) return -3;
+  if (kfr_bytes < mgp_x6_cols_bytes(M, N)) return -4;
+  if (M < 0) return -5;
+  if (N < 0) return -6;
+  if (!q_mu) return -7;
+  if (ldq < K) return -8;
+  if (K < 1) return -9;
+  if (K > 16) return MGP_ERR_UNSUPPORTED;
+  if (!variance) return -10;
+  if (!Afr) return -11;
+  if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -12;
+  if (!stats) return -13;
+  if (lds < N) return -14;
+  if (!aligned16(Tfr) || !aligned16(Kfr) || !aligned16(Afr)) return MGP_ERR_ALIGN;
+  if (mgp_x6_cols_bytes(M, N) >= ((size_t)1 << 32) || mgp_x6_lower_bytes(M, 1) >= ((size_t)1 << 32))
+    return MGP_ERR_UNSUPPORTED;
+  if (M == 0 || N == 0) return MGP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t tb = mgp_x6_lower_bytes(M, 1), kb = mgp_x6_cols_bytes(M, N);
+  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance);
+  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance);
+  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance);
+}
+
+// absmax of the source into the trailer, then the scaled split.
+extern "C" int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
+                                   void* Lfr, size_t lfr_bytes, mgp_stream_t stream) {
+  if (!q_sqrt) return -1;
+  if (ldqs < M) return -2;
+  if (K > 1 && strideq < ldqs * M) return -3;
+  if (M < 0) return -4;
+  if (K < 0) return -5;
+  if (!Lfr) return -6;
+  if (M == 0 || K == 0) return MGP_OK;
+  if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(Lfr)) return MGP_ERR_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  float* bound = trailer(Lfr, lower_planes(M, K));
+  int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
+  if (st) return st;
+  const int64_t rows = (int64_t)K * M;
+  hipLaunchKernelGGL(absmax_kernel<true>, dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 2048)), dim3(256), 0,
+                     s, q_sqrt, ldqs, strideq, M, M, rows, (unsigned int*)bound);
+  st = launch_status();
+  if (st) return st;
+  const int64_t Mp = x6_mp(M);
+  const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
+  const int64_t nfrag = (int64_t)K * nmb * nmk;
+  hipLaunchKernelGGL(split_tri_kernel<true>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt, ldqs,
+                     strideq, M, nmb, nmk, nfrag, (bf16x8*)Lfr, (const float*)bound);
+  return launch_status();
+}
+
+extern "C" int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr,
+                                  size_t afr_bytes, mgp_stream_t stream) {
+  if (!A) return -1;
+  if (lda < N) return -2;
+  if (M < 0) return -3;
+  if (N < 0) return -4;
+  if (!Afr) return -5;
+  if (M == 0 || N == 0) return MGP_OK;
+  if (afr_bytes < mgp_x6_cols_bytes(M, N)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(Afr)) return MGP_ERR_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  float* bound = trailer(Afr, cols_planes(M, N));
+  int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
+  if (st) return st;
+  hipLaunchKernelGGL(absmax_kernel<false>, dim3((unsigned)std::min<int64_t>((M + 3) / 4, 2048)), dim3(256), 0, s,
+                     A, lda, (int64_t)0, M, N, M, (unsigned int*)bound);
+  st = launch_status();
+  if (st) return st;
+  const int nmk = (int)(x6_mp(M) / 16);
+  const int64_t nfrag = (x6_np(N) / 32) * nmk;
+  hipLaunchKernelGGL(split_cols_kernel, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, A, lda, M, N, nmk,
+                     nfrag, (bf16x8*)Afr, (const float*)bound);
+  return launch_status();
+}
+
+extern "C" int mgp_expert_conditional_f16(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                          const float* stats, int64_t lds, const float* variance, int64_t M,
+                                          int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                                          void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  return expert_cond_planes(Afr, afr_bytes, Lfr, lfr_bytes, stats, lds, variance, M, N, K, 2, fmean, fvar, ldf,
+                            workspace, workspace_bytes, stream, true);
 }
 
 // ------------------------------------------------------------------ conditional backward (x6)

@@ -37,7 +37,7 @@ import torch
 
 from . import ops
 from .broadcasting_lik import BroadcastingLikelihood
-from .config import conditional_mode, default_device, default_jitter, expert_planes
+from .config import conditional_mode, default_device, default_jitter, expert_planes, forward_image_format
 from .kernels import SquaredExponential
 from .likelihoods import MultiClass
 
@@ -149,20 +149,20 @@ class SVGPModified:
         """GPflow SVGP.prior_kl -> gauss_kl(q_mu, q_sqrt) whitened (models.py:79); float64 [1]."""
         return ops.gauss_kl_white(self.q_mu, self.q_sqrt, out=out)
 
-    def operand_images(self, X, bufs=None, timing=None):
+    def operand_images(self, X, bufs=None, timing=None, fmt="x6"):
         """x6 mode: the split-bf16 images that do not depend on the Cholesky --
-        Kuf (K1) and tril(q_sqrt) -- so a caller can build them on a side
-        stream while K3 runs.  Returns (Kfr, Lfr)."""
+        Kuf (K1) and tril(q_sqrt) (split-f16 when fmt == "f16") -- so a caller
+        can build them on a side stream while K3 runs.  Returns (Kfr, Lfr)."""
         bufs = bufs or {}
         X = self.kernel._x(X)
         with _Stage(timing, "rbf_kuf"):
             Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
                                  out=bufs.get("Kfr"))
         with _Stage(timing, "split_tri"):
-            Lfr = ops.split_lower_x6(self.q_sqrt, out=bufs.get("Lfr"))
+            Lfr = ops.split_lower_x6(self.q_sqrt, out=bufs.get("Lfr"), fmt=fmt)
         return Kfr, Lfr
 
-    def conditional_kn(self, X, LinvT=None, bufs=None, timing=None, images=None):
+    def conditional_kn(self, X, LinvT=None, bufs=None, timing=None, images=None, fmt=None):
         """Whitened conditional for X [N, D]: fmean, fvar as expert-major [K, N] views.
 
         LinvT: (L^-1)^T of this layer's Kuu if already factorised (the SMGP
@@ -174,8 +174,9 @@ class SVGPModified:
             self._last_info = info
             LinvT = LinvT[0]
         bufs = bufs or {}
+        fmt = fmt or forward_image_format()
         if conditional_mode() == "x6":
-            Kfr, Lfr = images if images is not None else self.operand_images(X, bufs, timing)
+            Kfr, Lfr = images if images is not None else self.operand_images(X, bufs, timing, fmt)
         else:
             with _Stage(timing, "rbf_kuf"):
                 Kuf = ops.rbf_kuf(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
@@ -188,24 +189,26 @@ class SVGPModified:
                 return ops.expert_conditional(A, self.q_sqrt, stats, self.kernel.variance,
                                               fmean=bufs.get("fmean"), fvar=bufs.get("fvar"),
                                               workspace=bufs.get("ws_expert"))
-        Afr, stats = self.x6_trsm(X.shape[0], LinvT, Kfr, bufs, timing)
-        return self.x6_expert(X.shape[0], Afr, Lfr, stats, bufs, timing)
+        Afr, stats = self.x6_trsm(X.shape[0], LinvT, Kfr, bufs, timing, fmt)
+        return self.x6_expert(X.shape[0], Afr, Lfr, stats, bufs, timing, fmt)
 
-    def x6_trsm(self, N, LinvT, Kfr, bufs, timing=None):
-        """K4 on images: A's image and the column statistics (x6 mode)."""
+    def x6_trsm(self, N, LinvT, Kfr, bufs, timing=None, fmt="x6"):
+        """K4 on images: A's image (split-f16 when fmt == "f16") and the column
+        statistics (x6 mode)."""
         with _Stage(timing, "split_tri"):
             Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"))
         with _Stage(timing, "trsm_stats"):
             return ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, self.num_inducing, N, Afr=bufs.get("Afr"),
-                                     stats=bufs.get("stats"), A=bufs.get("A32"))
+                                     stats=bufs.get("stats"), A=bufs.get("A32"),
+                                     f16_variance=self.kernel.variance if fmt == "f16" else None)
 
-    def x6_expert(self, N, Afr, Lfr, stats, bufs, timing=None):
+    def x6_expert(self, N, Afr, Lfr, stats, bufs, timing=None, fmt="x6"):
         """K5 on images: fmean, fvar [K, N] (x6 mode)."""
         with _Stage(timing, "expert_cond"):
             return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, self.num_inducing, N,
                                              self.num_latent_gps, fmean=bufs.get("fmean"),
                                              fvar=bufs.get("fvar"), workspace=bufs.get("ws_expert"),
-                                             planes=expert_planes())
+                                             planes=expert_planes(), fmt=fmt)
 
     def conditional_experts(self, X, k0, k1, LinvT=None):
         """fmean, fvar [k1 - k0, N] of experts k0 .. k1 - 1 only (the expert-parallel
@@ -220,12 +223,14 @@ class SVGPModified:
             _, LinvT, info = self.factorise()
             self._last_info = info
             LinvT = LinvT[0]
+        fmt = forward_image_format()
         Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales)
         Tfr = ops.split_upper_x6(LinvT)
-        Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu[:, k0:k1], M, N)
-        Lfr = ops.split_lower_x6(self.q_sqrt[k0:k1])
+        Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu[:, k0:k1], M, N,
+                                       f16_variance=self.kernel.variance if fmt == "f16" else None)
+        Lfr = ops.split_lower_x6(self.q_sqrt[k0:k1], fmt=fmt)
         return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, k1 - k0,
-                                         planes=expert_planes())
+                                         planes=expert_planes(), fmt=fmt)
 
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
         """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior
@@ -397,6 +402,7 @@ class SMGP(SGP):
         b = self._buffers(N, train)
         layers = (("f", self.pred_layer), ("a", self.assign_layer))
         images = {}
+        fmt = forward_image_format(train)
         if b["x6"]:
             main = torch.cuda.current_stream(self.device)
             side = self._side_stream()
@@ -404,7 +410,7 @@ class SMGP(SGP):
             with torch.cuda.stream(side):
                 for L, layer in layers:
                     images[L] = layer.operand_images(X, {"Kfr": b["Kfr_" + L], "Lfr": b["Lfr_" + L]},
-                                                     timing)
+                                                     timing, fmt)
                 if kl_out is not None:
                     with _Stage(timing, "gauss_kl"):
                         self.pred_layer.prior_kl(out=kl_out[0:1])
@@ -424,14 +430,14 @@ class SMGP(SGP):
             pf, pa = self.pred_layer, self.assign_layer
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing)
-            Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing)
-            pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing)
+                Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt)
+            Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing, fmt)
+            pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
             main.wait_stream(side)
-            pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing)
+            pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)
         else:
             for L, layer in layers:
-                layer.conditional_kn(X, LinvT[L], bufs=bufs[L], timing=timing, images=images.get(L))
+                layer.conditional_kn(X, LinvT[L], bufs=bufs[L], timing=timing, images=images.get(L), fmt=fmt)
         if kl_out is not None and not b["x6"]:
             with _Stage(timing, "gauss_kl"):
                 self.pred_layer.prior_kl(out=kl_out[0:1])

@@ -210,9 +210,11 @@ def split_upper_x6(LinvT, out=None):
     return out
 
 
-def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None):
+def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_variance=None):
     """K4 on images: A's image (for expert_conditional_x6) and the stats [T, K+1, N];
-    also the f32 A when a buffer `A` [M, N] is given (training)."""
+    also the f32 A when a buffer `A` [M, N] is given (training).  f16_variance
+    (the layer's kernel variance): A's image is split-f16 instead
+    (mgp_trsm_stats_x6_f16, for expert_conditional_x6(..., fmt="f16"))."""
     _check(q_mu, "q_mu", 2)
     K = q_mu.shape[1]
     dev = q_mu.device
@@ -222,6 +224,13 @@ def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None):
     if stats is None:
         T = stats_tiles(M)
         stats = padded(T * (K + 1), N, dev).unflatten(0, (T, K + 1))
+    if f16_variance is not None:
+        if A is not None:
+            raise ValueError("the split-f16 K4 does not write the f32 A")
+        _lib.call("mgp_trsm_stats_x6_f16", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
+                  q_mu.data_ptr(), _ld(q_mu), K, f16_variance.data_ptr(), Afr.data_ptr(), Afr.numel(),
+                  stats.data_ptr(), _ld(stats), _stream())
+        return Afr, stats
     _lib.call("mgp_trsm_stats_x6", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
               q_mu.data_ptr(), _ld(q_mu), K, Afr.data_ptr(), Afr.numel(), stats.data_ptr(), _ld(stats),
               A.data_ptr() if A is not None else None, _ld(A) if A is not None else N, _stream())
@@ -267,32 +276,43 @@ def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None, worksp
 
 
 # ------------------------------------------------------------ K5, split-bf16 (x6)
-def split_lower_x6(q_sqrt, out=None):
-    """Fragment image (uint8 device tensor) of L_k = tril(q_sqrt[k]) for the split-bf16 K5."""
+def _fmt(fmt):
+    if fmt not in ("x6", "f16"):
+        raise ValueError("image format must be 'x6' (split-bf16) or 'f16' (split-f16)")
+    return fmt
+
+
+def split_lower_x6(q_sqrt, out=None, fmt="x6"):
+    """Fragment image (uint8 device tensor) of L_k = tril(q_sqrt[k]) for the split-bf16
+    K5 (fmt "f16": the split-f16 image, mgp_split_lower_f16)."""
     _check(q_sqrt, "q_sqrt", 3)
     K, M = q_sqrt.shape[0], q_sqrt.shape[1]
     nbytes = _lib.load().mgp_x6_lower_bytes(M, K)
     if out is None or out.numel() < nbytes:
         out = _ws(nbytes, q_sqrt.device)
-    _lib.call("mgp_split_lower_x6", q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), M, K, out.data_ptr(),
-              out.numel(), _stream())
+    _lib.call("mgp_split_lower_" + _fmt(fmt), q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), M, K,
+              out.data_ptr(), out.numel(), _stream())
     return out
 
 
-def split_cols_x6(A, out=None):
-    """Fragment image (uint8 device tensor) of A [M, N] for the split-bf16 K5."""
+def split_cols_x6(A, out=None, fmt="x6"):
+    """Fragment image (uint8 device tensor) of A [M, N] for the split-bf16 K5
+    (fmt "f16": the split-f16 image, mgp_split_cols_f16)."""
     _check(A, "A", 2)
     M, N = A.shape
     nbytes = _lib.load().mgp_x6_cols_bytes(M, N)
     if out is None or out.numel() < nbytes:
         out = _ws(nbytes, A.device)
-    _lib.call("mgp_split_cols_x6", A.data_ptr(), _ld(A), M, N, out.data_ptr(), out.numel(), _stream())
+    _lib.call("mgp_split_cols_" + _fmt(fmt), A.data_ptr(), _ld(A), M, N, out.data_ptr(), out.numel(),
+              _stream())
     return out
 
 
-def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=None, workspace=None, planes=3):
+def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=None, workspace=None, planes=3,
+                          fmt="x6"):
     """fmean, fvar [K, N] of the whitened K-expert conditional from split-bf16 images
-    (planes < 3: K5 on the leading bf16 planes only, mgp_expert_conditional_planes)."""
+    (planes < 3: K5 on the leading bf16 planes only, mgp_expert_conditional_planes;
+    fmt "f16": from split-f16 images, mgp_expert_conditional_f16)."""
     _check(stats, "stats", 3)
     dev = stats.device
     if fmean is None:
@@ -304,7 +324,11 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
     nbytes = _lib.load().mgp_expert_x6_workspace_bytes(M, N, K)
     if workspace is None or workspace.numel() < nbytes:
         workspace = _ws(nbytes, dev)
-    if planes == 3:
+    if _fmt(fmt) == "f16":
+        _lib.call("mgp_expert_conditional_f16", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
+                  stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(),
+                  fvar.data_ptr(), _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
+    elif planes == 3:
         _lib.call("mgp_expert_conditional_x6", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
                   stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(),
                   fvar.data_ptr(), _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())

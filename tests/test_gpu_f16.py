@@ -1,0 +1,139 @@
+"""Split-f16 ("f16x3") K4 -> K5 hand-off (mgp_trsm_stats_x6_f16,
+mgp_split_lower_f16 / mgp_split_cols_f16, mgp_expert_conditional_f16) against
+the float64 oracle, at the north_star gate (ELBO 1e-4 relative, fmean/fvar 1e-4
+normwise) and against the split-bf16 x6 path's own error."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref as R
+from tests.helpers import build_model, dev_noise, load_golden, normwise, params_from_golden, to_np
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def f16_mode():
+    from modulatedgps_amd import config
+    old = config.expert_format()
+    config.set_expert_format("f16")
+    yield
+    config.set_expert_format(old)
+
+
+def _t(a, device):
+    return torch.as_tensor(np.asarray(a, np.float32), device=device)
+
+
+def _k5_only(ops, A, qs, M, N, K, fmt, device):
+    """K5's own term: fvar = sum_m' (L^T A)^2 with zero stats and zero variance."""
+    Afr = ops.split_cols_x6(A, fmt=fmt)
+    Lfr = ops.split_lower_x6(qs, fmt=fmt)
+    T = ops.stats_tiles(M)
+    stats = ops.padded(T * (K + 1), N, device).unflatten(0, (T, K + 1))
+    stats.zero_()
+    zero = torch.zeros(1, dtype=torch.float32, device=device)
+    fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, zero, M, N, K, fmt=fmt)
+    return to_np(fm), to_np(fv)
+
+
+@pytest.mark.parametrize("sa,sl", [(1.0, 1.0), (3e-4, 7e2), (2.0 ** 20, 2.0 ** -18), (1e3, 1e-5)])
+def test_expert_f16_scale_invariance(device, sa, sl):
+    """Ragged M, N; operands far from unit scale: the power-of-two image scale
+    keeps the split-f16 K5 at its relative accuracy whatever the magnitudes."""
+    from modulatedgps_amd import ops
+    M, N, K = 200, 1000, 3
+    rng = np.random.default_rng(3)
+    A = rng.standard_normal((M, N)) * sa
+    qs = np.tril(rng.standard_normal((K, M, M))) * sl
+    qs += np.triu(np.full((M, M), 1e30), 1)          # upper triangle is ignored (band_part)
+    A32, qs32 = A.astype(np.float32), qs.astype(np.float32)
+    ref = np.einsum("kmi,mn->kin", np.tril(qs32.astype(np.float64)), A32.astype(np.float64))
+    ref = (ref ** 2).sum(1)                         # [K, N]
+    Ad = ops.as_padded(_t(A32, device))
+    qd = ops.as_padded(_t(qs32, device))
+    fm, fv = _k5_only(ops, Ad, qd, M, N, K, "f16", device)
+    assert np.all(fm == 0)
+    err16 = normwise(fv, ref)
+    _, fv6 = _k5_only(ops, Ad, qd, M, N, K, "x6", device)
+    err6 = normwise(fv6, ref)
+    print(f"scale ({sa:g}, {sl:g}): f16x3 {err16:.2e}  x6 {err6:.2e}")
+    assert err16 < 3e-7 and err16 < 1.5 * err6       # measured 1.0e-7 (x6 1.0e-7) at every scale
+    assert np.all(np.isfinite(fv))
+
+
+def test_expert_conditional_f16_accuracy(device):
+    """Config-3 shapes at reduced N: K4 (x6 inputs, split-f16 A image) -> K5 f16
+    against the float64 oracle, beside the x6 path."""
+    from modulatedgps_amd import ops
+    N, M, K, D, ls = 8192, 1024, 8, 8, 1.0
+    X, _, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
+    L = p.pred
+    mu_ref, var_ref = R.svgp_predict_f_dedup(X, L["Z"], L["variance"], L["lengthscales"], L["q_mu"], L["q_sqrt"])
+    var, lsc, Zt = _t([L["variance"]], device), _t([ls], device), _t(L["Z"], device)
+    _, LinvT, _ = ops.kuu_potrf_trtri([Zt], [var], [lsc], 1e-6)
+    Kfr = ops.rbf_kuf_x6(_t(X, device), Zt, var, lsc)
+    Tfr = ops.split_upper_x6(LinvT[0])
+    qm, qs = _t(L["q_mu"], device), ops.as_padded(_t(L["q_sqrt"], device))
+    errs = {}
+    for fmt in ("x6", "f16"):
+        Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, qm, M, N, f16_variance=var if fmt == "f16" else None)
+        Lfr = ops.split_lower_x6(qs, fmt=fmt)
+        fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmt=fmt)
+        errs[fmt] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))
+    print("fmean / fvar normwise error vs float64:", errs)
+    assert errs["f16"][0] == errs["x6"][0]            # fmean comes from K4's stats in both
+    assert errs["f16"][1] < 1e-4
+    assert errs["f16"][1] < 1.5 * errs["x6"][1]        # measured 7.34e-7 vs x6 7.31e-7
+
+
+@pytest.mark.parametrize("case", ["case_demo_init", "case_demo_perturbed", "case_c1"])
+def test_golden_elbo_f16(device, f16_mode, case):
+    d = load_golden(case + ".npz")
+    p = params_from_golden(d)
+    model = build_model(p, device)
+    X = torch.as_tensor(d["X"], dtype=torch.float32, device=device)
+    Y = torch.as_tensor(d["Y"], dtype=torch.float32, device=device)
+    elbo = float(model._build_likelihood(X, Y, noise=dev_noise(d["z"], d["u"], device)).cpu())
+    assert elbo == pytest.approx(float(d["elbo"]), rel=1e-4)
+    mu_f, var_f, mu_a, var_a = model.conditionals(X)
+    assert normwise(to_np(var_f).T, d["var_f"]) < 1e-4
+    assert normwise(to_np(var_a).T, d["var_a"]) < 1e-4
+    Xt = torch.as_tensor(d["Xtest"], dtype=torch.float32, device=device)
+    ym, yv = model.predict_y(Xt)
+    assert normwise(to_np(yv), d["predict_y_var"]) < 1e-4
+
+
+@pytest.mark.parametrize("N,M,K,D,ls,S", [(8192, 256, 4, 2, 0.15, 25),      # BASELINE config 2
+                                           (8192, 1024, 8, 8, 1.0, 25),      # config-3 shapes, N reduced
+                                           (4096, 2048, 16, 16, 2.0, 25),    # config-5 shapes, N reduced
+                                           (1001, 33, 2, 3, 0.8, 7)])        # ragged sizes
+def test_elbo_configs_f16(device, f16_mode, N, M, K, D, ls, S):
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
+    z, u = R.explicit_noise(S, N, K, seed=5)
+    ref, parts = R.smgp_elbo(X, Y, p, z, u, return_parts=True)
+    model = build_model(p, device)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    e = float(model._build_likelihood(Xd, Y, noise=dev_noise(z, u, device)).cpu())
+    assert e == pytest.approx(ref, rel=1e-4)
+    mu_f, var_f, mu_a, var_a = model.conditionals(Xd)
+    assert normwise(to_np(mu_f).T, parts["mu_f"]) < 1e-4
+    assert normwise(to_np(var_f).T, parts["var_f"]) < 1e-4
+    assert normwise(to_np(mu_a).T, parts["mu_a"]) < 1e-4
+    assert normwise(to_np(var_a).T, parts["var_a"]) < 1e-4
+
+
+def test_training_step_ignores_f16_format(device, f16_mode):
+    """elbo_and_grad keeps the x6 images (its backward consumes them): identical
+    to the x6-mode result."""
+    from modulatedgps_amd import config
+    X, Y, p = R.synthetic_problem(2048, 64, 3, 2, 0.8, state="perturbed", S=5)
+    z, u = R.explicit_noise(5, 2048, 3, seed=5)
+    model = build_model(p, device)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    e16, g16 = model.elbo_and_grad(Xd, Y, noise=dev_noise(z, u, device))
+    config.set_expert_format("x6")
+    e6, g6 = model.elbo_and_grad(Xd, Y, noise=dev_noise(z, u, device))
+    assert float(e16.cpu()) == float(e6.cpu())
+    for n in g6:
+        assert torch.equal(g16[n], g6[n]), n
