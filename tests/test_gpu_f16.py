@@ -12,6 +12,17 @@ from tests.helpers import build_model, dev_noise, load_golden, normwise, params_
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["x6", "f16"])
+def fmt_mode(request):
+    """Both forward image formats end to end (tests/test_gpu_model.py runs the
+    default one)."""
+    from modulatedgps_amd import config
+    old = config.expert_format()
+    config.set_expert_format(request.param)
+    yield request.param
+    config.set_expert_format(old)
+
+
 @pytest.fixture
 def f16_mode():
     from modulatedgps_amd import config
@@ -88,7 +99,7 @@ def test_expert_conditional_f16_accuracy(device):
 
 
 @pytest.mark.parametrize("case", ["case_demo_init", "case_demo_perturbed", "case_c1"])
-def test_golden_elbo_f16(device, f16_mode, case):
+def test_golden_elbo_formats(device, fmt_mode, case):
     d = load_golden(case + ".npz")
     p = params_from_golden(d)
     model = build_model(p, device)
@@ -108,7 +119,7 @@ def test_golden_elbo_f16(device, f16_mode, case):
                                            (8192, 1024, 8, 8, 1.0, 25),      # config-3 shapes, N reduced
                                            (4096, 2048, 16, 16, 2.0, 25),    # config-5 shapes, N reduced
                                            (1001, 33, 2, 3, 0.8, 7)])        # ragged sizes
-def test_elbo_configs_f16(device, f16_mode, N, M, K, D, ls, S):
+def test_elbo_configs_formats(device, fmt_mode, N, M, K, D, ls, S):
     X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
     z, u = R.explicit_noise(S, N, K, seed=5)
     ref, parts = R.smgp_elbo(X, Y, p, z, u, return_parts=True)
