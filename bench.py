@@ -357,9 +357,10 @@ def main():
             kernels[name] = {"avg_us": st[name][0] * 1e3}
 
     ek = kernels.get("expert_cond", {})
-    kname = "expert_cond_x6_kernel" if x6 else "expert_cond_kernel"
+    kname = ("expert_cond_f16_kernel" if f16 else "expert_cond_x6_kernel") if x6 else "expert_cond_kernel"
     traffic, traffic_src = load_traffic(kname)
-    roofline = {"kernel": f"{kname} (K5, L_k^T A + sum of squares, + cond_finalize)", "bound": "mfma",
+    klabel = "expert_cond_x6_kernel<2, true> (split-f16 instance)" if kname == "expert_cond_f16_kernel" else kname
+    roofline = {"kernel": f"{klabel} (K5, L_k^T A + sum of squares, + cond_finalize)", "bound": "mfma",
                 "achieved": ek.get("achieved"), "peak": peak_k5 / 1e12,
                 "unit": "TFLOP/s", "frac": ek.get("frac"), "traffic": traffic,
                 "traffic_source": traffic_src,

@@ -57,6 +57,11 @@ def main():
     Afr, st6 = ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N)
     Lfr = ops.split_lower_x6(q_sqrt)
     fm6, fv6 = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K)
+    # split-f16 forward hand-off (the default forward format)
+    Ahr = torch.empty_like(Afr)
+    sth = torch.empty_like(st6)
+    Lhr = ops.split_lower_x6(q_sqrt, fmt="f16")
+    ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var)
     # backward operands
     A32 = ops.padded(M, N, dev)
     ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Afr, stats=st6, A=A32)
@@ -85,6 +90,10 @@ def main():
                                                  Afr.numel(), None, N, None, N, ops._stream()),
         "split_lower_x6": lambda: ops.split_lower_x6(q_sqrt, out=Lfr),
         "expert_cond_x6": lambda: ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmean=fm6, fvar=fv6),
+        "trsm_stats_f16": lambda: ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var),
+        "split_lower_f16": lambda: ops.split_lower_x6(q_sqrt, out=Lhr, fmt="f16"),
+        "expert_cond_f16": lambda: ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmean=fm6, fvar=fv6,
+                                                             fmt="f16"),
         "gram_x6_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg),
         "gram_x6_Lm": lambda: ops.gram_x6(gK, A32, None, mode=1, N=N, out=gLm, workspace=wsg),
         "rbf_bwd": lambda: ops.rbf_backward(X, Z, var, lsc, gK),
@@ -104,8 +113,11 @@ def main():
         out["expert_cond"]["tflops"] = K * M * M * N / (out["expert_cond"]["median_ms"] * 1e-3) / 1e12
     if "expert_cond_x6" in out:
         out["expert_cond_x6"]["tflops"] = K * M * M * N / (out["expert_cond_x6"]["median_ms"] * 1e-3) / 1e12
-    if "trsm_stats_x6" in out:
-        out["trsm_stats_x6"]["tflops"] = M * M * N / (out["trsm_stats_x6"]["median_ms"] * 1e-3) / 1e12
+    if "expert_cond_f16" in out:
+        out["expert_cond_f16"]["tflops"] = K * M * M * N / (out["expert_cond_f16"]["median_ms"] * 1e-3) / 1e12
+    for name in ("trsm_stats_x6", "trsm_stats_f16"):
+        if name in out:
+            out[name]["tflops"] = M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
     for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N),
                      ("cond_bwd_x6", (2 * K + 1) * M * M * N)):
         if name in out:

@@ -28,6 +28,16 @@ def load(root, name):
     return per, dur, names
 
 
+def kernel_key(name):
+    """Kernel base name; the split-f16 instances of K4/K5 (template flag `true`)
+    are kept apart from their split-bf16 instances."""
+    base = name.split("::")[-1].split("<")[0]
+    args = name.split("<", 1)[1] if "<" in name else ""
+    if base in ("expert_cond_x6_kernel", "trsm_stats_x6_kernel") and "true" in args:
+        return base.replace("_x6_", "_f16_")
+    return base
+
+
 def main(root, out):
     res = collections.defaultdict(lambda: collections.defaultdict(list))
     for group in ("SQ_WAVE_CYCLES", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum"):
@@ -35,14 +45,16 @@ def main(root, out):
         for d, cs in per.items():
             if "mgp::" not in names[d]:
                 continue
-            k = names[d].split("::")[-1].split("<")[0]
+            k = kernel_key(names[d])
             for c, v in cs.items():
                 res[k][c].append(v)
             res[k]["duration_s"].append(dur[d])
     summary = {}
     for k, cs in res.items():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
-        e = {"launches_sampled": len(cs.get("FETCH_SIZE", [])), "avg_duration_us": avg["duration_s"] * 1e6}
+        e = {"launches_sampled": len(cs.get("FETCH_SIZE", []))}
+        if avg["duration_s"] > 0:  # PMC-mode timestamps are zero for some dispatches (durations: kernel-trace stats)
+            e["avg_duration_us"] = avg["duration_s"] * 1e6
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             rd = 2.0 * avg["FETCH_SIZE"] * 1024
             wr = avg["WRITE_SIZE"] * 1024
