@@ -150,7 +150,7 @@ def cpu_baseline(cfg, sizes):
             "seconds_per_step": t_full}
 
 
-def probe_kuf(model, X, x6, reps=20):
+def probe_kuf(model, X, x6, reps=20, fmt="x6"):
     """K1 launch time without the step's concurrency: `reps` back-to-back launches
     between two HIP events on the current stream (in the step, K1 shares the GPU
     with K3 on a side stream and its event bracket includes host submission)."""
@@ -159,7 +159,7 @@ def probe_kuf(model, X, x6, reps=20):
     b = model._buffers(X.shape[0])
     if x6:
         fn = lambda: ops.rbf_kuf_x6(X, layer.Z, layer.kernel.variance, layer.kernel.lengthscales,
-                                    out=b["Kfr_f"])
+                                    out=b["Kfr_f"], fmt=fmt)
     else:
         fn = lambda: ops.rbf_kuf(X, layer.Z, layer.kernel.variance, layer.kernel.lengthscales,
                                  out=b["Kuf_f"])
@@ -324,9 +324,10 @@ def main():
     st = stage_stats(timing)
 
     # algorithmic work per launch
-    if x6:   # K1 writes the split-bf16 image of Kuf (6 B per element of the padded [Mp, Np])
+    if x6:   # K1 writes the split-bf16 image of Kuf (6 B per element of the padded [Mp, Np];
+        # split-f16: 4 B)
         Mp, Np = -(-M // 128) * 128, -(-N // 256) * 256
-        kuf_bytes = 4.0 * (N * D + M * D) + 6.0 * Mp * Np
+        kuf_bytes = 4.0 * (N * D + M * D) + (4.0 if f16 else 6.0) * Mp * Np
     else:
         kuf_bytes = 4.0 * (N * D + M * D + M * N)
     trsm_flops = float(M) * M * N
@@ -334,13 +335,13 @@ def main():
     chol_flops = 2 * (2.0 * M ** 3 / 3.0)        # potrf + trtri, both layers (one batched sweep)
     kernels = {}
     if "rbf_kuf" in st:
-        ms = probe_kuf(model, X, x6)
+        ms = probe_kuf(model, X, x6, fmt="f16" if f16 else "x6")
         kernels["rbf_kuf"] = {"bound": "hbm", "avg_us": ms * 1e3, "bytes": kuf_bytes,
                               "achieved": kuf_bytes / (ms * 1e-3) / 1e9, "unit": "GB/s",
                               "peak": PEAK_HBM / 1e9, "frac": kuf_bytes / (ms * 1e-3) / PEAK_HBM,
                               "timing": "20 back-to-back launches after the timed steps",
                               "in_step_avg_us": st["rbf_kuf"][0] * 1e3}
-    for name, fl, peak in (("trsm_stats", trsm_flops, PEAK_X6 if x6 else PEAK_F32_MFMA),
+    for name, fl, peak in (("trsm_stats", trsm_flops, (PEAK_BF16_MFMA / 3 if f16 else PEAK_X6) if x6 else PEAK_F32_MFMA),
                            ("expert_cond", expert_flops, peak_k5)):
         if name in st:
             ms = st[name][0]
@@ -389,8 +390,9 @@ def main():
             "dtype": {3: "f32", 2: "f32/bf16x3 mixed", 1: "f32/bf16 mixed"}[args.planes] if x6 else "f32",
             "data": "synthetic",
             "dtype_note": (("f32 operands and accumulation; K1/K4 products on bf16 MFMA via an exact 3-plane "
-                            "split (6 products); K5 on f16 MFMA via a scaled 2-plane fp16 split (22-bit "
-                            "operands, 3 products); K3 in f64") if f16 else
+                            "split (6 products) in training; the forward chain K1 -> K4 -> K5 on f16 MFMA via "
+                            "power-of-two-scaled 2-plane fp16 splits (22-bit operands, 3 products); K3 in f64")
+                           if f16 else
                            ("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
                             "3-plane split (6 products, f32-accurate); K3 in f64") if x6 and args.planes == 3 else
                            (f"K1-K4 f32-accurate (x6 split-bf16), K5 on the leading {args.planes} bf16 plane(s) "

@@ -189,7 +189,22 @@ int mgp_expert_conditional_planes(const void* Afr, size_t afr_bytes, const void*
  *       split-f16 image, bound sqrt(variance) (|A[m][n]| <= sqrt(k(x_n, x_n)));
  *   mgp_expert_conditional_f16: K5 on the two split-f16 images, outputs and
  *       workspace as mgp_expert_conditional_x6.
+ * The whole forward chain in split-f16 (K1 -> K4 -> K5, three f16 products per
+ * block in K4 as well):
+ *   mgp_rbf_kuf_f16:     K1 writing Kuf's split-f16 image (bound = variance,
+ *       Kuf <= variance; replaces kernel.K(Z, Xnew), models.py:139);
+ *   mgp_split_upper_f16: LinvT (upper triangle) -> Tfr (bound = its max |.|);
+ *   mgp_trsm_stats_f16:  K4 as mgp_trsm_stats_x6_f16 on split-f16 Tfr / Kfr
+ *       (the triangular solve of base_conditional, models.py:141-143).
  * Replaces the same call sites (GPflow base_conditional, models.py:141-143). */
+int mgp_rbf_kuf_f16(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                    int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                    void* Kfr, size_t kfr_bytes, mgp_stream_t stream);
+int mgp_split_upper_f16(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, size_t tfr_bytes,
+                        mgp_stream_t stream);
+int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
+                       int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
+                       void* Afr, size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream);
 int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
                         void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
 int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr, size_t afr_bytes,

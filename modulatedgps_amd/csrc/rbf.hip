@@ -89,11 +89,13 @@ __global__ __launch_bounds__(kRbfThreads) void rbf_kernel(
 // expanded form GPflow's square_distance uses), splits them and stores 6 x 16 B.
 // Workgroup = 4 waves x 32 columns x 128 rows (4 row tiles per wave).
 // Rows >= M and columns >= N of the padded image are written as zeros.
-template <int DMAX>
+// F16: split-f16 image instead (mgp_rbf_kuf_f16): Kuf <= variance, so the image
+// scale is 2^img_exp(variance) and the trailer `bound` receives the variance.
+template <int DMAX, bool F16 = false>
 __global__ __launch_bounds__(kRbfThreads) void rbf_kuf_x6_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ Z, int64_t ldz, int64_t N,
     int64_t M, int D, const float* __restrict__ variance, const float* __restrict__ ls, int n_ls, int nmk,
-    bf16x8* __restrict__ Kfr) {
+    bf16x8* __restrict__ Kfr, float* __restrict__ bound = nullptr) {
   constexpr int KS = (DMAX + 1) / 2;     // MFMA k-steps (2 dims each)
   constexpr int DP = 2 * KS + 1;         // LDS row pitch (odd: spreads banks)
   __shared__ float zs[128 * DP];
@@ -129,6 +131,11 @@ __global__ __launch_bounds__(kRbfThreads) void rbf_kuf_x6_kernel(
   __syncthreads();
   const float var = variance[0];
   const bool colok = n < N;
+  float scale = 1.f;
+  if constexpr (F16) {
+    scale = ldexpf(1.f, img_exp(var));
+    if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0) *bound = var;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     floatx16 acc;
@@ -147,7 +154,10 @@ __global__ __launch_bounds__(kRbfThreads) void rbf_kuf_x6_kernel(
         const float r2 = fmaf(-2.f, acc[8 * half + j], zz[row] + xx);
         v[j] = (colok && m0 + row < M) ? var * exp2f(-r2) : 0.f;
       }
-      store_split(Kfr + ((nb * nmk + 2 * mb + half) * 3) * 64 + lane, v);
+      if constexpr (F16)
+        store_split_f16(Kfr + ((nb * nmk + 2 * mb + half) * 3) * 64 + lane, v, scale);
+      else
+        store_split(Kfr + ((nb * nmk + 2 * mb + half) * 3) * 64 + lane, v);
     }
   }
 }
@@ -350,9 +360,9 @@ extern "C" int mgp_rbf_kuu(const float* Z, int64_t ldz, int64_t M, int32_t D, co
 
 extern "C" size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
 
-extern "C" int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
-                              int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
-                              void* Kfr, size_t kfr_bytes, mgp_stream_t stream) {
+static int rbf_kuf_image(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M, int32_t D,
+                         const float* variance, const float* lengthscales, int32_t n_ls, void* Kfr,
+                         size_t kfr_bytes, mgp_stream_t stream, bool f16) {
   if (!X) return -1;
   if (ldx < D) return -2;
   if (!Z) return -3;
@@ -372,11 +382,16 @@ extern "C" int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64
   const int nmk = (int)(Mp / 16);
   const dim3 grid((unsigned)(Np / 128), (unsigned)(Mp / 128)), block(kRbfThreads);
   hipStream_t s = (hipStream_t)stream;
-#define MGP_RBF_X6_CASE(DM)                                                                          \
-  if (D <= DM) {                                                                                     \
-    hipLaunchKernelGGL(rbf_kuf_x6_kernel<DM>, grid, block, 0, s, X, ldx, Z, ldz, N, M, D, variance,  \
-                       lengthscales, n_ls, nmk, (bf16x8*)Kfr);                                       \
-    return launch_status();                                                                          \
+  float* bound = (float*)((char*)Kfr + mgp_x6_cols_bytes(M, N) - 256);  // image trailer (split3.hip)
+#define MGP_RBF_X6_CASE(DM)                                                                            \
+  if (D <= DM) {                                                                                       \
+    if (f16)                                                                                           \
+      hipLaunchKernelGGL((rbf_kuf_x6_kernel<DM, true>), grid, block, 0, s, X, ldx, Z, ldz, N, M, D,    \
+                         variance, lengthscales, n_ls, nmk, (bf16x8*)Kfr, bound);                      \
+    else                                                                                               \
+      hipLaunchKernelGGL((rbf_kuf_x6_kernel<DM, false>), grid, block, 0, s, X, ldx, Z, ldz, N, M, D,   \
+                         variance, lengthscales, n_ls, nmk, (bf16x8*)Kfr, nullptr);                    \
+    return launch_status();                                                                            \
   }
   MGP_RBF_X6_CASE(1)
   MGP_RBF_X6_CASE(2)
@@ -386,6 +401,18 @@ extern "C" int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64
   MGP_RBF_X6_CASE(32)
 #undef MGP_RBF_X6_CASE
   return MGP_ERR_UNSUPPORTED;
+}
+
+extern "C" int mgp_rbf_kuf_x6(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                              int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                              void* Kfr, size_t kfr_bytes, mgp_stream_t stream) {
+  return rbf_kuf_image(X, ldx, Z, ldz, N, M, D, variance, lengthscales, n_ls, Kfr, kfr_bytes, stream, false);
+}
+
+extern "C" int mgp_rbf_kuf_f16(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
+                               int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
+                               void* Kfr, size_t kfr_bytes, mgp_stream_t stream) {
+  return rbf_kuf_image(X, ldx, Z, ldz, N, M, D, variance, lengthscales, n_ls, Kfr, kfr_bytes, stream, true);
 }
 
 static int64_t rbf_bwd_chunk(int64_t N) { return 4096; }

@@ -104,20 +104,24 @@ __global__ __launch_bounds__(256) void split_cols_kernel(const float* __restrict
     store_split(Afr + f * 3 * 64 + lane, v);
 }
 
-// max |x| over a batch of row-major matrices (rows x cols, LOWER: entries with
-// column <= row only) -> *out as float bits through atomicMax (non-negative
-// floats order as their bit patterns; *out zeroed beforehand).  One wave per row.
-template <bool LOWER>
+// max |x| over a batch of row-major matrices (rows x cols; TRI 0: all entries,
+// 1: column <= row, 2: column >= row) -> *out as float bits through atomicMax
+// (non-negative floats order as their bit patterns; *out zeroed beforehand).
+// Waves stride over rows; one atomic per workgroup after an LDS reduction (a
+// same-address atomic per wave serialises at the L2: 96 us at K M = 8192 rows).
+template <int TRI>
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ src, int64_t ld, int64_t stride,
                                                      int64_t rows, int64_t cols, int64_t nrows_total,
                                                      unsigned int* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float m = 0.f;
-  for (int64_t gr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); gr < nrows_total; gr += (int64_t)gridDim.x * 4) {
+  for (int64_t gr = (int64_t)blockIdx.x * 4 + w; gr < nrows_total; gr += (int64_t)gridDim.x * 4) {
     const int64_t b = gr / rows, r = gr % rows;
     const float* row = src + b * stride + r * ld;
-    const int64_t nc = LOWER ? (r + 1 < cols ? r + 1 : cols) : cols;
-    for (int64_t c = lane; c < nc; c += 64) m = fmaxf(m, fabsf(row[c]));
+    const int64_t c0 = TRI == 2 ? r : 0;
+    const int64_t c1 = TRI == 1 ? (r + 1 < cols ? r + 1 : cols) : cols;
+    for (int64_t c = c0 + lane; c < c1; c += 64) m = fmaxf(m, fabsf(row[c]));
   }
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   m = fmaxf(m, __shfl_xor(m, 16, 64));
@@ -125,7 +129,9 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
   m = fmaxf(m, __shfl_xor(m, 4, 64));
   m = fmaxf(m, __shfl_xor(m, 2, 64));
   m = fmaxf(m, __shfl_xor(m, 1, 64));
-  if (lane == 0) atomicMax(out, __float_as_uint(m));
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -512,12 +518,16 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restri
 // a_var != nullptr: A's image is split-f16, scaled by 2^img_exp(sqrt(*a_var))
 // (|A[m][n]| <= ||A[:, n]|| <= sqrt(k(x_n, x_n)) = sqrt(variance): the Nystrom
 // bound; the image trailer a_bound receives sqrt(*a_var) for the consumer).
-template <int KMAX, bool F16OUT = false>
+// F16IN: Tfr and Kfr are split-f16 images (scales 2^img_exp(*t_bound),
+// 2^img_exp(*k_bound)): three f16 products per block instead of six bf16 ones;
+// the accumulators are unscaled (exact power of two) before the epilogue.
+template <int KMAX, bool F16OUT = false, bool F16IN = false>
 __device__ __forceinline__ void trsm_stats_x6_item(
     bf16x8 (*sL)[4 * 3 * 64], float* __restrict__ sQ, int t, int tn, const bf16x8* __restrict__ Tfr,
     uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
     const float* __restrict__ q_mu, int64_t ldq, int K, bf16x8* __restrict__ Afr, float* __restrict__ stats,
-    int64_t lds_, float* __restrict__ Af32, int64_t lda, const float* __restrict__ a_var) {
+    int64_t lds_, float* __restrict__ Af32, int64_t lda, const float* __restrict__ a_var,
+    const float* __restrict__ t_bound = nullptr, const float* __restrict__ k_bound = nullptr) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = 128 * (int64_t)t;
@@ -532,9 +542,18 @@ __device__ __forceinline__ void trsm_stats_x6_item(
     }
   }
   floatx16 acc[4][2];
-  x6_mainloop<2>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
-              img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8,
-              nmk);
+  x6_mainloop<2, 2, F16IN ? 2 : 3, F16IN>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
+                                          img_rsrc(Kfr, kfr_bytes),
+                                          (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0, 8 * t + 8, nmk);
+  if constexpr (F16IN) {
+    const float unscale = ldexpf(1.f, -(img_exp(*t_bound) + img_exp(*k_bound)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][c][e] *= unscale;
+  }
   if (Af32) store_acc_f32(acc, Af32, lda, i0, (int64_t)tn * kX6BN, M, N, nullptr);
   // ---- epilogue by 32-row sub-tile i: the A image fragments of acc[i] and its
   // contribution to the stats of 64-row stats tile i / 2 (stats[st][0][n] = sum A^2,
@@ -606,12 +625,13 @@ __device__ __forceinline__ void trsm_stats_x6_item(
 // workgroup has the same work; both items read the same Kuf column slab.  Odd
 // nT: the middle row tile is an item alone.  (c3: 385 us vs 439 us for one item
 // per workgroup, whose register count stays below 256 without spills.)
-template <int KMAX, bool F16OUT = false>
+template <int KMAX, bool F16OUT = false, bool F16IN = false>
 __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
     const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
     int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
     bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda,
-    const float* __restrict__ a_var, float* __restrict__ a_bound) {
+    const float* __restrict__ a_var, float* __restrict__ a_bound, const float* __restrict__ t_bound = nullptr,
+    const float* __restrict__ k_bound = nullptr) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   __shared__ float sQ[128 * KMAX];
   const int nT = nmk / 8, nP = (nT + 1) / 2;
@@ -619,12 +639,12 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
   if constexpr (F16OUT)
     if (blockIdx.x == 0 && threadIdx.x == 0) *a_bound = sqrtf(*a_var);
   col_major_item(blockIdx.x, nP, nTn, p, tn);
-  trsm_stats_x6_item<KMAX, F16OUT>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq,
-                                   K, Afr, stats, lds_, Af32, lda, a_var);
+  trsm_stats_x6_item<KMAX, F16OUT, F16IN>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu,
+                                          ldq, K, Afr, stats, lds_, Af32, lda, a_var, t_bound, k_bound);
   if (nT - 1 - p == p) return;
   __syncthreads();  // the epilogue's sQ reads before the next item's sQ stores
-  trsm_stats_x6_item<KMAX, F16OUT>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr,
-                                   stats, lds_, Af32, lda, a_var);
+  trsm_stats_x6_item<KMAX, F16OUT, F16IN>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K,
+                                          Afr, stats, lds_, Af32, lda, a_var, t_bound, k_bound);
 }
 
 }  // namespace mgp
@@ -784,12 +804,19 @@ extern "C" int mgp_expert_conditional_planes(const void* Afr, size_t afr_bytes, 
 template <int KMAX>
 static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb, int64_t M, int64_t N,
                           const float* q_mu, int64_t ldq, int K, void* Afr, float* stats, int64_t lds,
-                          float* A, int64_t lda, hipStream_t s, const float* a_var = nullptr) {
+                          float* A, int64_t lda, hipStream_t s, const float* a_var = nullptr,
+                          bool f16in = false) {
   const int64_t Mp = x6_mp(M);
   const int nmk = (int)(Mp / 16), nT = (int)(Mp / kX6BM), nTn = (int)(x6_np(N) / kX6BN);
   const dim3 grid((unsigned)((nT + 1) / 2 * nTn));
   float* a_bound = trailer(Afr, cols_planes(M, N));
-  if (a_var)
+  if (f16in) {
+    const float* t_bound = trailer(const_cast<void*>(Tfr), lower_planes(M, 1));
+    const float* k_bound = trailer(const_cast<void*>(Kfr), cols_planes(M, N));
+    hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
+                       (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
+                       (bf16x8*)Afr, stats, lds, nullptr, lda, a_var, a_bound, t_bound, k_bound);
+  } else if (a_var)
     hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                        (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
                        (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound);
@@ -830,10 +857,9 @@ extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* 
 }
 
 // ------------------------------------------------------------------ split-f16 ("f16x3") K5 path
-extern "C" int mgp_trsm_stats_x6_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes,
-                                     int64_t M, int64_t N, const float* q_mu, int64_t ldq, int32_t K,
-                                     const float* variance, void* Afr, size_t afr_bytes, float* stats,
-                                     int64_t lds, mgp_stream_t stream) {
+static int trsm_stats_f16_out(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
+                              int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance, void* Afr,
+                              size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream, bool f16in) {
   if (!Tfr) return -1;
   if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return -2;
   if (!Kfr) return -3;
@@ -855,9 +881,27 @@ extern "C" int mgp_trsm_stats_x6_f16(const void* Tfr, size_t tfr_bytes, const vo
   if (M == 0 || N == 0) return MGP_OK;
   hipStream_t s = (hipStream_t)stream;
   const size_t tb = mgp_x6_lower_bytes(M, 1), kb = mgp_x6_cols_bytes(M, N);
-  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance);
-  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance);
-  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance);
+  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance, f16in);
+  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance, f16in);
+  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance, f16in);
+}
+
+// x6 images in (Tfr, Kfr), split-f16 A image out (K5's operand).
+extern "C" int mgp_trsm_stats_x6_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes,
+                                     int64_t M, int64_t N, const float* q_mu, int64_t ldq, int32_t K,
+                                     const float* variance, void* Afr, size_t afr_bytes, float* stats,
+                                     int64_t lds, mgp_stream_t stream) {
+  return trsm_stats_f16_out(Tfr, tfr_bytes, Kfr, kfr_bytes, M, N, q_mu, ldq, K, variance, Afr, afr_bytes, stats, lds,
+                            stream, false);
+}
+
+// split-f16 images in (mgp_split_upper_f16, mgp_rbf_kuf_f16) and out: three f16
+// products per block instead of six bf16 ones.
+extern "C" int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
+                                  int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
+                                  void* Afr, size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream) {
+  return trsm_stats_f16_out(Tfr, tfr_bytes, Kfr, kfr_bytes, M, N, q_mu, ldq, K, variance, Afr, afr_bytes, stats, lds,
+                            stream, true);
 }
 
 // absmax of the source into the trailer, then the scaled split.
@@ -877,7 +921,7 @@ extern "C" int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t st
   int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
   if (st) return st;
   const int64_t rows = (int64_t)K * M;
-  hipLaunchKernelGGL(absmax_kernel<true>, dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 2048)), dim3(256), 0,
+  hipLaunchKernelGGL(absmax_kernel<1>, dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 256)), dim3(256), 0,
                      s, q_sqrt, ldqs, strideq, M, M, rows, (unsigned int*)bound);
   st = launch_status();
   if (st) return st;
@@ -886,6 +930,33 @@ extern "C" int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t st
   const int64_t nfrag = (int64_t)K * nmb * nmk;
   hipLaunchKernelGGL(split_tri_kernel<true>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt, ldqs,
                      strideq, M, nmb, nmk, nfrag, (bf16x8*)Lfr, (const float*)bound);
+  return launch_status();
+}
+
+// L^-T (upper triangle) as a split-f16 T image for mgp_trsm_stats_f16: absmax
+// of the triangle into the trailer, then the scaled split.
+extern "C" int mgp_split_upper_f16(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, size_t tfr_bytes,
+                                   mgp_stream_t stream) {
+  if (!LinvT) return -1;
+  if (ldl < M) return -2;
+  if (M < 0) return -3;
+  if (!Tfr) return -4;
+  if (M == 0) return MGP_OK;
+  if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(Tfr)) return MGP_ERR_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  float* bound = trailer(Tfr, lower_planes(M, 1));
+  int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
+  if (st) return st;
+  hipLaunchKernelGGL(absmax_kernel<2>, dim3((unsigned)std::min<int64_t>((M + 3) / 4, 256)), dim3(256), 0, s, LinvT,
+                     ldl, (int64_t)0, M, M, M, (unsigned int*)bound);
+  st = launch_status();
+  if (st) return st;
+  const int64_t Mp = x6_mp(M);
+  const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
+  const int64_t nfrag = (int64_t)nmb * nmk;
+  hipLaunchKernelGGL(split_tri_kernel<false>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, LinvT, ldl,
+                     (int64_t)0, M, nmb, nmk, nfrag, (bf16x8*)Tfr, (const float*)bound);
   return launch_status();
 }
 
@@ -903,7 +974,7 @@ extern "C" int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_
   float* bound = trailer(Afr, cols_planes(M, N));
   int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
   if (st) return st;
-  hipLaunchKernelGGL(absmax_kernel<false>, dim3((unsigned)std::min<int64_t>((M + 3) / 4, 2048)), dim3(256), 0, s,
+  hipLaunchKernelGGL(absmax_kernel<0>, dim3((unsigned)std::min<int64_t>((M + 3) / 4, 256)), dim3(256), 0, s,
                      A, lda, (int64_t)0, M, N, M, (unsigned int*)bound);
   st = launch_status();
   if (st) return st;

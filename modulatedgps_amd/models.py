@@ -15,6 +15,9 @@ arguments and method names).  The SMGP ELBO hot path
        mgp_split_upper_x6 / mgp_split_lower_x6   images of L^-T and tril(q_sqrt)
     K4 mgp_trsm_stats_x6    A image + stats         models.py:141-143 (triangular_solve, A^T q_mu)
     K5 mgp_expert_conditional_x6  fmean, fvar [K, N]  models.py:141-143 (LTA, fvar)
+    (forward evaluations, config expert_format "f16" = the default: the same chain
+     on split-f16 images, K1 mgp_rbf_kuf_f16, mgp_split_upper_f16 /
+     mgp_split_lower_f16, K4 mgp_trsm_stats_f16, K5 mgp_expert_conditional_f16)
     (config.set_conditional_mode("f32"): K1 mgp_rbf_kuf + K4 mgp_trsm_stats +
      K5 mgp_expert_conditional on the exact-f32 MFMA instead)
     K7 mgp_gauss_kl_white   KL                      models.py:79 (prior_kl)
@@ -157,7 +160,7 @@ class SVGPModified:
         X = self.kernel._x(X)
         with _Stage(timing, "rbf_kuf"):
             Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales,
-                                 out=bufs.get("Kfr"))
+                                 out=bufs.get("Kfr"), fmt=fmt)
         with _Stage(timing, "split_tri"):
             Lfr = ops.split_lower_x6(self.q_sqrt, out=bufs.get("Lfr"), fmt=fmt)
         return Kfr, Lfr
@@ -196,11 +199,11 @@ class SVGPModified:
         """K4 on images: A's image (split-f16 when fmt == "f16") and the column
         statistics (x6 mode)."""
         with _Stage(timing, "split_tri"):
-            Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"))
+            Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"), fmt=fmt)
         with _Stage(timing, "trsm_stats"):
             return ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, self.num_inducing, N, Afr=bufs.get("Afr"),
                                      stats=bufs.get("stats"), A=bufs.get("A32"),
-                                     f16_variance=self.kernel.variance if fmt == "f16" else None)
+                                     f16_variance=self.kernel.variance if fmt == "f16" else None, in_fmt=fmt)
 
     def x6_expert(self, N, Afr, Lfr, stats, bufs, timing=None, fmt="x6"):
         """K5 on images: fmean, fvar [K, N] (x6 mode)."""
@@ -224,10 +227,10 @@ class SVGPModified:
             self._last_info = info
             LinvT = LinvT[0]
         fmt = forward_image_format()
-        Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales)
-        Tfr = ops.split_upper_x6(LinvT)
+        Kfr = ops.rbf_kuf_x6(X, self.Z, self.kernel.variance, self.kernel.lengthscales, fmt=fmt)
+        Tfr = ops.split_upper_x6(LinvT, fmt=fmt)
         Afr, stats = ops.trsm_stats_x6(Tfr, Kfr, self.q_mu[:, k0:k1], M, N,
-                                       f16_variance=self.kernel.variance if fmt == "f16" else None)
+                                       f16_variance=self.kernel.variance if fmt == "f16" else None, in_fmt=fmt)
         Lfr = ops.split_lower_x6(self.q_sqrt[k0:k1], fmt=fmt)
         return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, k1 - k0,
                                          planes=expert_planes(), fmt=fmt)

@@ -186,35 +186,39 @@ def trsm_stats(LinvT, Kuf, q_mu, A=None, stats=None):
     return A, stats
 
 
-def rbf_kuf_x6(X, Z, variance, lengthscales, out=None):
-    """K1 writing the split-bf16 image of Kuf = K(Z, X) (uint8 device tensor)."""
+def rbf_kuf_x6(X, Z, variance, lengthscales, out=None, fmt="x6"):
+    """K1 writing the split-bf16 image of Kuf = K(Z, X) (uint8 device tensor);
+    fmt "f16": the split-f16 image (mgp_rbf_kuf_f16) for trsm_stats_x6(..., in_fmt="f16")."""
     _check(X, "X", 2), _check(Z, "Z", 2)
     N, D = X.shape
     M = Z.shape[0]
     nbytes = _lib.load().mgp_x6_cols_bytes(M, N)
     if out is None or out.numel() < nbytes:
         out = _ws(nbytes, X.device)
-    _lib.call("mgp_rbf_kuf_x6", X.data_ptr(), _ld(X), Z.data_ptr(), _ld(Z), N, M, D, variance.data_ptr(),
+    _lib.call("mgp_rbf_kuf_" + _fmt(fmt), X.data_ptr(), _ld(X), Z.data_ptr(), _ld(Z), N, M, D, variance.data_ptr(),
               lengthscales.data_ptr(), lengthscales.numel(), out.data_ptr(), out.numel(), _stream())
     return out
 
 
-def split_upper_x6(LinvT, out=None):
-    """Split-bf16 image of (L^-1)^T [M, M] (upper triangle) as K4's T operand."""
+def split_upper_x6(LinvT, out=None, fmt="x6"):
+    """Split-bf16 image of (L^-1)^T [M, M] (upper triangle) as K4's T operand
+    (fmt "f16": the split-f16 image, mgp_split_upper_f16)."""
     _check(LinvT, "LinvT", 2)
     M = LinvT.shape[0]
     nbytes = _lib.load().mgp_x6_lower_bytes(M, 1)
     if out is None or out.numel() < nbytes:
         out = _ws(nbytes, LinvT.device)
-    _lib.call("mgp_split_upper_x6", LinvT.data_ptr(), _ld(LinvT), M, out.data_ptr(), out.numel(), _stream())
+    _lib.call("mgp_split_upper_" + _fmt(fmt), LinvT.data_ptr(), _ld(LinvT), M, out.data_ptr(), out.numel(), _stream())
     return out
 
 
-def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_variance=None):
+def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_variance=None, in_fmt="x6"):
     """K4 on images: A's image (for expert_conditional_x6) and the stats [T, K+1, N];
     also the f32 A when a buffer `A` [M, N] is given (training).  f16_variance
     (the layer's kernel variance): A's image is split-f16 instead
-    (mgp_trsm_stats_x6_f16, for expert_conditional_x6(..., fmt="f16"))."""
+    (mgp_trsm_stats_x6_f16, for expert_conditional_x6(..., fmt="f16")).
+    in_fmt "f16": Tfr and Kfr are split-f16 images (split_upper_x6 / rbf_kuf_x6 with
+    fmt "f16"; mgp_trsm_stats_f16, needs f16_variance)."""
     _check(q_mu, "q_mu", 2)
     K = q_mu.shape[1]
     dev = q_mu.device
@@ -227,10 +231,12 @@ def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_varian
     if f16_variance is not None:
         if A is not None:
             raise ValueError("the split-f16 K4 does not write the f32 A")
-        _lib.call("mgp_trsm_stats_x6_f16", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
+        _lib.call("mgp_trsm_stats_x6_f16" if _fmt(in_fmt) == "x6" else "mgp_trsm_stats_f16", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
                   q_mu.data_ptr(), _ld(q_mu), K, f16_variance.data_ptr(), Afr.data_ptr(), Afr.numel(),
                   stats.data_ptr(), _ld(stats), _stream())
         return Afr, stats
+    if _fmt(in_fmt) != "x6":
+        raise ValueError("split-f16 K4 inputs need the split-f16 output (f16_variance)")
     _lib.call("mgp_trsm_stats_x6", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
               q_mu.data_ptr(), _ld(q_mu), K, Afr.data_ptr(), Afr.numel(), stats.data_ptr(), _ld(stats),
               A.data_ptr() if A is not None else None, _ld(A) if A is not None else N, _stream())

@@ -1,5 +1,6 @@
-"""Split-f16 ("f16x3") K4 -> K5 hand-off (mgp_trsm_stats_x6_f16,
-mgp_split_lower_f16 / mgp_split_cols_f16, mgp_expert_conditional_f16) against
+"""Split-f16 ("f16x3") forward chain (mgp_rbf_kuf_f16, mgp_split_upper_f16,
+mgp_trsm_stats_f16 / mgp_trsm_stats_x6_f16, mgp_split_lower_f16 /
+mgp_split_cols_f16, mgp_expert_conditional_f16) against
 the float64 oracle, at the north_star gate (ELBO 1e-4 relative, fmean/fvar 1e-4
 normwise) and against the split-bf16 x6 path's own error."""
 import numpy as np
@@ -92,10 +93,19 @@ def test_expert_conditional_f16_accuracy(device):
         Lfr = ops.split_lower_x6(qs, fmt=fmt)
         fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmt=fmt)
         errs[fmt] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))
+    # the whole forward chain in split-f16: K1 (mgp_rbf_kuf_f16), L^-T image
+    # (mgp_split_upper_f16), K4 on f16 inputs (mgp_trsm_stats_f16), K5 f16
+    Khr = ops.rbf_kuf_x6(_t(X, device), Zt, var, lsc, fmt="f16")
+    Thr = ops.split_upper_x6(LinvT[0], fmt="f16")
+    Afr, stats = ops.trsm_stats_x6(Thr, Khr, qm, M, N, f16_variance=var, in_fmt="f16")
+    fm, fv = ops.expert_conditional_x6(Afr, ops.split_lower_x6(qs, fmt="f16"), stats, var, M, N, K, fmt="f16")
+    errs["f16 chain"] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))
     print("fmean / fvar normwise error vs float64:", errs)
     assert errs["f16"][0] == errs["x6"][0]            # fmean comes from K4's stats in both
     assert errs["f16"][1] < 1e-4
     assert errs["f16"][1] < 1.5 * errs["x6"][1]        # measured 7.34e-7 vs x6 7.31e-7
+    assert errs["f16 chain"][0] < 1e-4 and errs["f16 chain"][1] < 1e-4
+    assert errs["f16 chain"][0] < 8 * errs["x6"][0] and errs["f16 chain"][1] < 8 * errs["x6"][1]
 
 
 @pytest.mark.parametrize("case", ["case_demo_init", "case_demo_perturbed", "case_c1"])

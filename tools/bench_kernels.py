@@ -62,6 +62,9 @@ def main():
     sth = torch.empty_like(st6)
     Lhr = ops.split_lower_x6(q_sqrt, fmt="f16")
     ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var)
+    Khr = ops.rbf_kuf_x6(X, Z, var, lsc, fmt="f16")
+    Thr = ops.split_upper_x6(LinvT[0], fmt="f16")
+    ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var, in_fmt="f16")
     # backward operands
     A32 = ops.padded(M, N, dev)
     ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Afr, stats=st6, A=A32)
@@ -90,7 +93,11 @@ def main():
                                                  Afr.numel(), None, N, None, N, ops._stream()),
         "split_lower_x6": lambda: ops.split_lower_x6(q_sqrt, out=Lfr),
         "expert_cond_x6": lambda: ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmean=fm6, fvar=fv6),
-        "trsm_stats_f16": lambda: ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var),
+        "trsm_stats_x6f16": lambda: ops.trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var),
+        "rbf_kuf_f16": lambda: ops.rbf_kuf_x6(X, Z, var, lsc, out=Khr, fmt="f16"),
+        "split_upper_f16": lambda: ops.split_upper_x6(LinvT[0], out=Thr, fmt="f16"),
+        "trsm_stats_f16": lambda: ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var,
+                                                    in_fmt="f16"),
         "split_lower_f16": lambda: ops.split_lower_x6(q_sqrt, out=Lhr, fmt="f16"),
         "expert_cond_f16": lambda: ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmean=fm6, fvar=fv6,
                                                              fmt="f16"),
@@ -115,7 +122,7 @@ def main():
         out["expert_cond_x6"]["tflops"] = K * M * M * N / (out["expert_cond_x6"]["median_ms"] * 1e-3) / 1e12
     if "expert_cond_f16" in out:
         out["expert_cond_f16"]["tflops"] = K * M * M * N / (out["expert_cond_f16"]["median_ms"] * 1e-3) / 1e12
-    for name in ("trsm_stats_x6", "trsm_stats_f16"):
+    for name in ("trsm_stats_x6", "trsm_stats_x6f16", "trsm_stats_f16"):
         if name in out:
             out[name]["tflops"] = M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
     for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N),
@@ -126,6 +133,8 @@ def main():
         out["rbf_bwd"]["GBps"] = 4 * M * N / (out["rbf_bwd"]["median_ms"] * 1e-3) / 1e9
     if "rbf_kuf_x6" in out:
         out["rbf_kuf_x6"]["GBps"] = (4 * (N * D + M * D) + 6 * M * N) / (out["rbf_kuf_x6"]["median_ms"] * 1e-3) / 1e9
+    if "rbf_kuf_f16" in out:
+        out["rbf_kuf_f16"]["GBps"] = (4 * (N * D + M * D) + 4 * M * N) / (out["rbf_kuf_f16"]["median_ms"] * 1e-3) / 1e9
     if "trsm_stats" in out:
         out["trsm_stats"]["tflops"] = M * M * N / (out["trsm_stats"]["median_ms"] * 1e-3) / 1e12
     if "rbf_kuf" in out:

@@ -29,11 +29,16 @@ def load(root, name):
 
 
 def kernel_key(name):
-    """Kernel base name; the split-f16 instances of K4/K5 (template flag `true`)
-    are kept apart from their split-bf16 instances."""
+    """Kernel base name; the split-f16 instances of K1/K4/K5 (template flags
+    `true`) are kept apart from their split-bf16 instances."""
     base = name.split("::")[-1].split("<")[0]
     args = name.split("<", 1)[1] if "<" in name else ""
-    if base in ("expert_cond_x6_kernel", "trsm_stats_x6_kernel") and "true" in args:
+    flags = [a.strip() for a in args.split(">")[0].split(",")]
+    if base == "trsm_stats_x6_kernel" and flags[1:] == ["true", "true"]:
+        return "trsm_stats_f16_kernel"          # split-f16 images in and out
+    if base == "trsm_stats_x6_kernel" and flags[1:2] == ["true"]:
+        return "trsm_stats_x6f16_kernel"        # split-bf16 in, split-f16 A image out
+    if base in ("expert_cond_x6_kernel", "rbf_kuf_x6_kernel") and "true" in flags:
         return base.replace("_x6_", "_f16_")
     return base
 
