@@ -195,7 +195,10 @@ int mgp_expert_conditional_planes(const void* Afr, size_t afr_bytes, const void*
  *       Kuf <= variance; replaces kernel.K(Z, Xnew), models.py:139);
  *   mgp_split_upper_f16: LinvT (upper triangle) -> Tfr (bound = its max |.|);
  *   mgp_trsm_stats_f16:  K4 as mgp_trsm_stats_x6_f16 on split-f16 Tfr / Kfr
- *       (the triangular solve of base_conditional, models.py:141-143).
+ *       (the triangular solve of base_conditional, models.py:141-143); also
+ *       the f32 A [M][lda] when A is not NULL (training);
+ *   mgp_conditional_backward_f16: mgp_conditional_backward_x6 with Afr =
+ *       A's split-f16 image (mgp_trsm_stats_f16); S_k A runs on f16 products.
  * Replaces the same call sites (GPflow base_conditional, models.py:141-143). */
 int mgp_rbf_kuf_f16(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,
                     int32_t D, const float* variance, const float* lengthscales, int32_t n_ls,
@@ -204,7 +207,8 @@ int mgp_split_upper_f16(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, s
                         mgp_stream_t stream);
 int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
                        int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
-                       void* Afr, size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream);
+                       void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A, int64_t lda,
+                       mgp_stream_t stream);
 int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
                         void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
 int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr, size_t afr_bytes,
@@ -261,6 +265,17 @@ int mgp_conditional_backward_x6(const void* Afr, size_t afr_bytes, const float* 
                                 int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm,
                                 int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
                                 mgp_stream_t stream);
+/* Same, with Afr = A's split-f16 image (mgp_trsm_stats_f16): S_k = L_k L_k^T is
+ * split the same way (bound = max |S_k| on device) and S_k A runs on three f16
+ * products per block. */
+int mgp_conditional_backward_f16(const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+                                 const float* q_sqrt, int64_t ldqs,
+                                 int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+                                 int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M,
+                                 int64_t N, int32_t K, float* g_q_mu, int64_t ldgq, float* g_q_sqrt,
+                                 int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm,
+                                 int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
+                                 mgp_stream_t stream);
 
 /* Reverse mode of Lm = chol(Kuu) (models.py:141): gKuu = sym(Lm^-T Phi(Lm^T gL) Lm^-1),
  * Phi = lower triangle with halved diagonal, in float64 from the float32 L,

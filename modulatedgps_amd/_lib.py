@@ -83,6 +83,10 @@ SIGNATURES = {
                                                    c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                                                    c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64,
                                                    c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_conditional_backward_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
+                                                   c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                                   c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64,
+                                                   c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
     "mgp_split_upper_x6": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_rbf_kuf_x6": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i32,
                                       c_ptr, c_size, c_ptr]),
@@ -104,7 +108,7 @@ SIGNATURES = {
                                        c_ptr, c_size, c_ptr]),
     "mgp_split_upper_f16": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_trsm_stats_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
-                                          c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr]),
+                                          c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "mgp_expert_conditional_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
                                                   c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_kl_workspace_bytes": (c_size, [c_i64, c_i32]),

@@ -18,7 +18,8 @@ import torch
 #              products).  Both measure the same error against the float64 oracle
 #              (tests/test_gpu_f16.py: 1.0e-7 normwise on K5's term, 7.3e-7 on fvar
 #              at c3 shapes -- the f32 inputs' own rounding); f16 is half the MFMA
-#              work.  The training step and the reduced-plane modes use "x6".
+#              work.  The training step follows it (A's image, S_k A in the
+#              backward); the reduced-plane modes use "x6".
 _CFG = {"jitter": 1e-6, "device": None, "conditional": os.environ.get("MGP_CONDITIONAL", "x6"),
         "expert_planes": int(os.environ.get("MGP_K5_PLANES", "3")),
         "expert_format": os.environ.get("MGP_K5_FORMAT", "f16")}
@@ -79,8 +80,8 @@ def set_expert_format(fmt):
 
 
 def forward_image_format(train=False):
-    """Image format of the forward K4 -> K5 hand-off: "f16" only for forward-only
-    evaluations at full planes with expert_format() == "f16"."""
-    if train or expert_planes() != 3:
+    """Image format of the K1 -> K4 -> K5 chain (and of the training step's A
+    image): expert_format() at full planes, "x6" for the reduced-plane modes."""
+    if expert_planes() != 3:
         return "x6"
     return expert_format()

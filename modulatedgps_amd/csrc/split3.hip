@@ -435,12 +435,17 @@ __global__ __launch_bounds__(256) void grad_a_base_kernel(const float* __restric
 // product runs through the K5 main loop (full T, one column sub-tile per
 // wave) and is folded into the output registers with its column weights, so
 // no per-expert intermediate is written.
+// F16: Sfr and Afr are split-f16 images (scales 2^img_exp(*s_bound), 2^img_exp(*a_bound)):
+// three f16 products per block; the unscale folds into the column weights.
+template <bool F16 = false>
 __global__ __launch_bounds__(256, 2) void grad_a_s_kernel(const bf16x8* __restrict__ Sfr, uint32_t s_bytes,
                                                           const bf16x8* __restrict__ Afr, uint32_t afr_bytes,
                                                           int nmk, int nTn, int K, int64_t M, int64_t N,
                                                           const float* __restrict__ Gv, int64_t ldg,
                                                           const float* __restrict__ gA0, int64_t ld0,
-                                                          bf16x8* __restrict__ gAfr) {
+                                                          bf16x8* __restrict__ gAfr,
+                                                          const float* __restrict__ s_bound = nullptr,
+                                                          const float* __restrict__ a_bound = nullptr) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   const int nT = nmk / 8, nmb = nmk / 2;
   int t, tn;
@@ -455,10 +460,13 @@ __global__ __launch_bounds__(256, 2) void grad_a_s_kernel(const bf16x8* __restri
 #pragma unroll
     for (int e = 0; e < 16; ++e) out[i][0][e] = 0.f;
   const int64_t s_elems = (int64_t)nmb * nmk * 3 * 64;  // one expert's S image (bf16x8 units)
+  float unscale = 1.f;
+  if constexpr (F16) unscale = ldexpf(1.f, -(img_exp(*s_bound) + img_exp(*a_bound)));
   for (int k = 0; k < K; ++k) {
-    x6_mainloop<0, 1>(acc, sL, img_rsrc(Sfr + k * s_elems, s_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
-                      img_rsrc(Afr, afr_bytes), (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, nmk, nmk);
-    const float g = n < N ? Gv[(int64_t)k * ldg + n] : 0.f;
+    x6_mainloop<0, 1, F16 ? 2 : 3, F16>(acc, sL, img_rsrc(Sfr + k * s_elems, s_bytes),
+                                        (uint32_t)(4 * t * nmk) * 3u * kFragBytes, img_rsrc(Afr, afr_bytes),
+                                        (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, nmk, nmk);
+    const float g = n < N ? Gv[(int64_t)k * ldg + n] * unscale : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -815,7 +823,7 @@ static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb
     const float* k_bound = trailer(const_cast<void*>(Kfr), cols_planes(M, N));
     hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                        (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
-                       (bf16x8*)Afr, stats, lds, nullptr, lda, a_var, a_bound, t_bound, k_bound);
+                       (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
   } else if (a_var)
     hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                        (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
@@ -859,7 +867,8 @@ extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* 
 // ------------------------------------------------------------------ split-f16 ("f16x3") K5 path
 static int trsm_stats_f16_out(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
                               int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance, void* Afr,
-                              size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream, bool f16in) {
+                              size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream, bool f16in,
+                              float* A = nullptr, int64_t lda = 0) {
   if (!Tfr) return -1;
   if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return -2;
   if (!Kfr) return -3;
@@ -881,9 +890,9 @@ static int trsm_stats_f16_out(const void* Tfr, size_t tfr_bytes, const void* Kfr
   if (M == 0 || N == 0) return MGP_OK;
   hipStream_t s = (hipStream_t)stream;
   const size_t tb = mgp_x6_lower_bytes(M, 1), kb = mgp_x6_cols_bytes(M, N);
-  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance, f16in);
-  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance, f16in);
-  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, nullptr, 0, s, variance, f16in);
+  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in);
+  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in);
+  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in);
 }
 
 // x6 images in (Tfr, Kfr), split-f16 A image out (K5's operand).
@@ -899,9 +908,11 @@ extern "C" int mgp_trsm_stats_x6_f16(const void* Tfr, size_t tfr_bytes, const vo
 // products per block instead of six bf16 ones.
 extern "C" int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
                                   int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
-                                  void* Afr, size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream) {
+                                  void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A, int64_t lda,
+                                  mgp_stream_t stream) {
+  if (A && lda < N) return -16;
   return trsm_stats_f16_out(Tfr, tfr_bytes, Kfr, kfr_bytes, M, N, q_mu, ldq, K, variance, Afr, afr_bytes, stats, lds,
-                            stream, true);
+                            stream, true, A, lda);
 }
 
 // absmax of the source into the trailer, then the scaled split.
@@ -1085,12 +1096,13 @@ extern "C" size_t mgp_conditional_backward_workspace_bytes(int64_t M, int64_t N,
   return cond_bwd_layout(M, N, K).total;
 }
 
-extern "C" int mgp_conditional_backward_x6(
+static int conditional_backward(
     const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
     const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
     int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
     float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
-    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream,
+    bool f16) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!A) return -3;
@@ -1145,8 +1157,14 @@ extern "C" int mgp_conditional_backward_x6(
   if (st) return st;
   {
     const int64_t nfrag = (int64_t)K * nmb * nmk;
+    float* s_bound = trailer(Sfr, lower_planes(M, K));
+    if (f16) {  // max |S_k| over the experts into the image trailer, then the scaled split
+      if ((st = hip_status(hipMemsetAsync(s_bound, 0, sizeof(float), s)))) return st;
+      hipLaunchKernelGGL(absmax_kernel<0>, dim3((unsigned)std::min<int64_t>(((int64_t)K * M + 3) / 4, 256)),
+                         dim3(256), 0, s, LT, ldm, M * ldm, M, M, (int64_t)K * M, (unsigned int*)s_bound);
+    }
     hipLaunchKernelGGL((split_tri_kernel<true, false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, LT,
-                       ldm, M * ldm, M, nmb, nmk, nfrag, Sfr);
+                       ldm, M * ldm, M, nmb, nmk, nfrag, Sfr, f16 ? (const float*)s_bound : nullptr);
     const int64_t nf1 = (int64_t)nmb * nmk;
     hipLaunchKernelGGL((split_tri_kernel<true, true>), dim3((unsigned)((nf1 + 3) / 4)), dim3(256), 0, s, LinvT, ldl,
                        (int64_t)0, M, nmb, nmk, nf1, LIfr);
@@ -1168,9 +1186,15 @@ extern "C" int mgp_conditional_backward_x6(
     if ((st = launch_status())) return st;
   }
   // 3. gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0
-  hipLaunchKernelGGL(grad_a_s_kernel, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
-                     (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes, nmk, 2 * nTn, K, M,
-                     N, Gv, ldg, gA0, ldn, gAfr);
+  if (f16)
+    hipLaunchKernelGGL(grad_a_s_kernel<true>, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
+                       (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes, nmk, 2 * nTn, K,
+                       M, N, Gv, ldg, gA0, ldn, gAfr, (const float*)trailer(Sfr, lower_planes(M, K)),
+                       (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)));
+  else
+    hipLaunchKernelGGL(grad_a_s_kernel<false>, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
+                       (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes, nmk, 2 * nTn, K,
+                       M, N, Gv, ldg, gA0, ldn, gAfr, nullptr, nullptr);
   if ((st = launch_status())) return st;
   // 4. gKuf = Linv^T gA
   hipLaunchKernelGGL(trsm_bwd_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)gAfr,
@@ -1196,4 +1220,28 @@ extern "C" int mgp_conditional_backward_x6(
   hipLaunchKernelGGL(row_sums_kernel, dim3((unsigned)K), dim3(1024), 0, s, Gv, N, ldg, part);
   hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1), 0, s, part, (int)K, g_var);
   return launch_status();
+}
+
+extern "C" int mgp_conditional_backward_x6(
+    const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+    const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+    int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
+    float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
+    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
+                              N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
+                              workspace_bytes, stream, false);
+}
+
+// Afr is A's split-f16 image (mgp_trsm_stats_f16); S_k = L_k L_k^T is split the same
+// way, so the S_k A product (B-b) runs on three f16 products per block.
+extern "C" int mgp_conditional_backward_f16(
+    const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+    const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+    int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
+    float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
+    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
+                              N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
+                              workspace_bytes, stream, true);
 }

@@ -544,7 +544,7 @@ class SMGP(SGP):
             with _Stage(timing, "conditional_bwd"):
                 g = ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], layer.q_sqrt,
                                                 layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
-                                                workspace=b["ws_cbwd"])
+                                                workspace=b["ws_cbwd"], fmt=forward_image_format(True))
             with _Stage(timing, "chol_bwd"):
                 gKuu = ops.chol_backward(b["L_" + L], b["LinvT_" + L], g["g_Lm"])
             with _Stage(timing, "rbf_bwd"):

@@ -229,11 +229,17 @@ def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_varian
         T = stats_tiles(M)
         stats = padded(T * (K + 1), N, dev).unflatten(0, (T, K + 1))
     if f16_variance is not None:
-        if A is not None:
-            raise ValueError("the split-f16 K4 does not write the f32 A")
-        _lib.call("mgp_trsm_stats_x6_f16" if _fmt(in_fmt) == "x6" else "mgp_trsm_stats_f16", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
-                  q_mu.data_ptr(), _ld(q_mu), K, f16_variance.data_ptr(), Afr.data_ptr(), Afr.numel(),
-                  stats.data_ptr(), _ld(stats), _stream())
+        if _fmt(in_fmt) == "x6":
+            if A is not None:
+                raise ValueError("the split-bf16 -> split-f16 K4 does not write the f32 A")
+            _lib.call("mgp_trsm_stats_x6_f16", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
+                      q_mu.data_ptr(), _ld(q_mu), K, f16_variance.data_ptr(), Afr.data_ptr(), Afr.numel(),
+                      stats.data_ptr(), _ld(stats), _stream())
+        else:
+            _lib.call("mgp_trsm_stats_f16", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
+                      q_mu.data_ptr(), _ld(q_mu), K, f16_variance.data_ptr(), Afr.data_ptr(), Afr.numel(),
+                      stats.data_ptr(), _ld(stats), A.data_ptr() if A is not None else None,
+                      _ld(A) if A is not None else N, _stream())
         return Afr, stats
     if _fmt(in_fmt) != "x6":
         raise ValueError("split-f16 K4 inputs need the split-f16 output (f16_variance)")
@@ -492,9 +498,10 @@ def conditional_backward_workspace_bytes(M, N, K):
     return int(_lib.load().mgp_conditional_backward_workspace_bytes(M, N, K))
 
 
-def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None):
+def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None, fmt="x6"):
     """Backward of one layer's conditional (see include/mgp_hip.h): returns dict of
-    g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1])."""
+    g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1]).
+    fmt: format of A's image Afr ("f16": mgp_conditional_backward_f16)."""
     K = q_mu.shape[1]
     dev = q_mu.device
     if out is None:
@@ -507,7 +514,7 @@ def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None
     if _ld(Gmu) != _ld(Gv):
         raise ValueError("Gmu and Gv must share a leading dimension")
     o = out
-    _lib.call("mgp_conditional_backward_x6", Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A),
+    _lib.call("mgp_conditional_backward_" + _fmt(fmt), Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A),
               q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), q_mu.data_ptr(), _ld(q_mu),
               LinvT.data_ptr(), _ld(LinvT), Gmu.data_ptr(), Gv.data_ptr(), _ld(Gmu), M, N, K,
               o["g_q_mu"].data_ptr(), _ld(o["g_q_mu"]), o["g_q_sqrt"].data_ptr(), _ld(o["g_q_sqrt"]),

@@ -24,15 +24,6 @@ def fmt_mode(request):
     config.set_expert_format(old)
 
 
-@pytest.fixture
-def f16_mode():
-    from modulatedgps_amd import config
-    old = config.expert_format()
-    config.set_expert_format("f16")
-    yield
-    config.set_expert_format(old)
-
-
 def _t(a, device):
     return torch.as_tensor(np.asarray(a, np.float32), device=device)
 
@@ -142,19 +133,3 @@ def test_elbo_configs_formats(device, fmt_mode, N, M, K, D, ls, S):
     assert normwise(to_np(var_f).T, parts["var_f"]) < 1e-4
     assert normwise(to_np(mu_a).T, parts["mu_a"]) < 1e-4
     assert normwise(to_np(var_a).T, parts["var_a"]) < 1e-4
-
-
-def test_training_step_ignores_f16_format(device, f16_mode):
-    """elbo_and_grad keeps the x6 images (its backward consumes them): identical
-    to the x6-mode result."""
-    from modulatedgps_amd import config
-    X, Y, p = R.synthetic_problem(2048, 64, 3, 2, 0.8, state="perturbed", S=5)
-    z, u = R.explicit_noise(5, 2048, 3, seed=5)
-    model = build_model(p, device)
-    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
-    e16, g16 = model.elbo_and_grad(Xd, Y, noise=dev_noise(z, u, device))
-    config.set_expert_format("x6")
-    e6, g6 = model.elbo_and_grad(Xd, Y, noise=dev_noise(z, u, device))
-    assert float(e16.cpu()) == float(e6.cpu())
-    for n in g6:
-        assert torch.equal(g16[n], g6[n]), n

@@ -179,5 +179,10 @@ def test_multiclass_elbo_and_grad(device, N, M, K, D, ls, S, modified):
         # demo-shape case: 2.4e-4 against a gradient of norm 0.17), where the f32
         # path's absolute error (~2-6e-4, as on the Gaussian path) is the criterion.
         tiny = n.endswith(("variance", "lengthscales")) and np.linalg.norm(ref) < 1e-2 * g_norm
-        ok = err < max(3e-4, 1.5 * err32) or (tiny and np.linalg.norm(got - ref) < 1e-2 * g_norm)
+        # A block that vanishes in float64 (the saturated Gumbel-softmax at tau = 0.01
+        # leaves the assignment layer's Z gradient at ~1e-16 in this case) has no
+        # relative error to speak of: it must stay negligible against the gradient.
+        vanishing = np.linalg.norm(ref) < 1e-6 * g_norm
+        ok = (err < max(3e-4, 1.5 * err32) or (tiny and np.linalg.norm(got - ref) < 1e-2 * g_norm)
+              or (vanishing and np.linalg.norm(got - ref) < 1e-5 * g_norm))
         assert ok, (n, err, err32, float(np.linalg.norm(ref)), float(g_norm))

@@ -71,7 +71,19 @@ def _dense(name, t, M):
                                                     (1000, 25, 3, 1, 0.5, 25, True),
                                                     (4096, 130, 3, 3, 1.0, 5, False),
                                                     (2048, 2048, 16, 16, 2.0, 3, False)])   # config-5 shapes
-def test_elbo_and_grad(device, N, M, K, D, ls, S, modified):
+@pytest.mark.parametrize("fmt", ["f16", "x6"])
+def test_elbo_and_grad(device, N, M, K, D, ls, S, modified, fmt):
+    """Both image formats of the chain (split-f16, the default, and split-bf16 x6)."""
+    from modulatedgps_amd import config
+    old = config.expert_format()
+    config.set_expert_format(fmt)
+    try:
+        _check_elbo_and_grad(device, N, M, K, D, ls, S, modified)
+    finally:
+        config.set_expert_format(old)
+
+
+def _check_elbo_and_grad(device, N, M, K, D, ls, S, modified):
     X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
     a_var = np.linspace(0.3, 0.9, K)[None, :] if modified else None
     z, u = R.explicit_noise(S, N, K, seed=5)

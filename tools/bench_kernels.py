@@ -82,6 +82,7 @@ def main():
     torch.cuda.synchronize()
     runs = {
         "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
+        "kuu_chol_x1": lambda: ops.kuu_potrf_trtri([Z], [var], [lsc], 1e-6, LinvT=LinvT[0:1], info=info[0:1]),
         "rbf_kuf": lambda: ops.rbf_kuf(X, Z, var, lsc, out=Kuf),
         "trsm_stats": lambda: ops.trsm_stats(LinvT[0], Kuf, q_mu, A=A, stats=stats),
         "expert_cond": lambda: ops.expert_conditional(A, q_sqrt, stats, var, fmean=fm, fvar=fv),
