@@ -241,6 +241,16 @@ size_t mgp_gram_x6_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t ba
 int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy, int64_t sy,
                 int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha, int32_t mode,
                 float* out, int64_t ldo, int64_t so, void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+/* Same contraction on the f16 matrix cores: the chunks are split on the fly
+ * into power-of-two-scaled fp16 hi / lo planes (three products per fragment
+ * pair, 22-bit operands).  x_bound, y_bound, w_bound: DEVICE pointers to
+ * bounds of |X|, |Y| and |W| (w_bound only when W != NULL).  Workspace as
+ * mgp_gram_x6.  Used by mgp_conditional_backward_f16. */
+int mgp_gram_f16(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
+                 int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                 int32_t mode, float* out, int64_t ldo, int64_t so, const float* x_bound,
+                 const float* y_bound, const float* w_bound, void* workspace, size_t workspace_bytes,
+                 mgp_stream_t stream);
 
 /* Backward of one layer's whitened conditional (the GradientTape pass through
  * GPflow base_conditional, models.py:141-143, and SVGP's Knn = var,

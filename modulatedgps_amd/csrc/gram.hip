@@ -172,18 +172,40 @@ __device__ __forceinline__ void stash4(char* dst, floatx4 v) {
   *reinterpret_cast<bf16x4*>(dst + 2048) = l;
 }
 
+// Split-f16 variant: 4 consecutive values, scaled by a power of two, as fp16
+// hi / lo planes (see mgp_common.hpp, split-f16 images).
+__device__ __forceinline__ void stash4h(char* dst, floatx4 v, float scale) {
+  typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+  halfx4 h, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x = v[j] * scale;
+    const _Float16 hi = (_Float16)x;
+    h[j] = hi;
+    l[j] = (_Float16)(x - (float)hi);
+  }
+  *reinterpret_cast<halfx4*>(dst) = h;
+  *reinterpret_cast<halfx4*>(dst + 1024) = l;
+}
+
 // 768 threads in two roles, three waves per SIMD: one consumer (waves 0-3)
 // multiplies one LDS buffer (64 x 64 of the tile each) while two producers
 // (waves 4-11; two waves per SIMD double the VALU issue rate of one) load the
 // next f32 chunks (two chunks ahead, in registers), split them and store the
 // fragments into the other buffer.  One barrier per chunk.
-template <bool TRI, bool WEIGHT>
+// F16: the chunks are split into scaled fp16 hi / lo planes instead (xb, yb, wb:
+// device bounds of |X|, |Y| and |W|, the scales 2^img_exp(xb), 2^img_exp(yb wb)),
+// three f16 products per fragment pair; the accumulators are unscaled on store.
+template <bool TRI, bool WEIGHT, bool F16 = false>
 __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict__ X, int64_t ldx, int64_t sx,
                                                          int64_t MI, const float* __restrict__ Y, int64_t ldy,
                                                          int64_t sy, int64_t MJ, const float* __restrict__ W,
                                                          int64_t sw, int64_t N, int64_t nper, int nbj, int tiles,
                                                          int batch, int nsplit, float* __restrict__ ws,
-                                                         int64_t bstride, int64_t zstride) {
+                                                         int64_t bstride, int64_t zstride,
+                                                         const float* __restrict__ xb = nullptr,
+                                                         const float* __restrict__ yb = nullptr,
+                                                         const float* __restrict__ wb = nullptr) {
   // per buffer: [32-row block][k-step] groups of [plane][lane] 16-B fragment slots
   __shared__ __attribute__((aligned(16))) char sX[2][8 * kXG], sY[2][8 * kXG];
   // item: when the splits come in multiples of 8, split z runs on XCD z % 8 and
@@ -223,6 +245,13 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool producer = w >= 4;
+  float xs = 1.f, ys = 1.f, unscale = 1.f;
+  if constexpr (F16) {
+    const int ex = img_exp(*xb), ey = img_exp(*yb * (WEIGHT ? *wb : 1.f));
+    xs = ldexpf(1.f, ex);
+    ys = ldexpf(1.f, ey);
+    unscale = ldexpf(1.f, -(ex + ey));
+  }
 
   // ---- producer state: thread loads 4 consecutive n (column group cg) of rows
   // 32 q + rr (q = q0, q0 + 1) of both tiles.  Lane l of producer wave pw (0..7):
@@ -272,13 +301,18 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
     }
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
-      stash4(sX[buf] + 2 * (q0 + qq) * kXG + soff, r.x[qq]);
-      stash4(sY[buf] + 2 * (q0 + qq) * kXG + soff, WEIGHT ? r.y[qq] * r.w : r.y[qq]);
+      if constexpr (F16) {
+        stash4h(sX[buf] + 2 * (q0 + qq) * kXG + soff, r.x[qq], xs);
+        stash4h(sY[buf] + 2 * (q0 + qq) * kXG + soff, WEIGHT ? r.y[qq] * r.w : r.y[qq], ys);
+      } else {
+        stash4(sX[buf] + 2 * (q0 + qq) * kXG + soff, r.x[qq]);
+        stash4(sY[buf] + 2 * (q0 + qq) * kXG + soff, WEIGHT ? r.y[qq] * r.w : r.y[qq]);
+      }
     }
   };
 
   // ---- consumer state: wave w multiplies X blocks wb, wb + 1 by Y blocks vb, vb + 1
-  const int wb = (w >> 1) * 2, vb = (w & 1) * 2;
+  const int wb_ = (w >> 1) * 2, vb = (w & 1) * 2;
   floatx16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -289,20 +323,26 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
   auto compute = [&](int buf) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      constexpr int NP = F16 ? 2 : 3;
       bf16x8 c[2][3];
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           c[t2][p] = *reinterpret_cast<const bf16x8*>(sY[buf] + (2 * (vb + t2) + ks) * kXG + p * 1024 + lane * 16);
 #pragma unroll
       for (int ta = 0; ta < 2; ++ta) {
         bf16x8 a[3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          a[p] = *reinterpret_cast<const bf16x8*>(sX[buf] + (2 * (wb + ta) + ks) * kXG + p * 1024 + lane * 16);
+        for (int p = 0; p < NP; ++p)
+          a[p] = *reinterpret_cast<const bf16x8*>(sX[buf] + (2 * (wb_ + ta) + ks) * kXG + p * 1024 + lane * 16);
 #pragma unroll
-        for (int tb = 0; tb < 2; ++tb) acc[ta][tb] = mfma_x6(a, c[tb], acc[ta][tb]);
+        for (int tb = 0; tb < 2; ++tb) {
+          if constexpr (F16)
+            acc[ta][tb] = mfma_fmt<2, true>(a, c[tb], acc[ta][tb]);
+          else
+            acc[ta][tb] = mfma_x6(a, c[tb], acc[ta][tb]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the next k-step's fragment reads after these MFMAs
     }
@@ -350,8 +390,8 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
       const int64_t j = j0 + 32 * (vb + tb) + (lane & 31);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int64_t i = i0 + 32 * (wb + ta) + acc_row(e, lane);
-        if (i < MI && j < MJ) out[i * MJ + j] = acc[ta][tb][e];
+        const int64_t i = i0 + 32 * (wb_ + ta) + acc_row(e, lane);
+        if (i < MI && j < MJ) out[i * MJ + j] = F16 ? acc[ta][tb][e] * unscale : acc[ta][tb][e];
       }
     }
 }
@@ -447,10 +487,12 @@ extern "C" size_t mgp_gram_x6_workspace_bytes(int64_t MI, int64_t MJ, int64_t N,
   return (size_t)gram_x6_splits(N, (int64_t)tiles * batch) * (size_t)batch * (size_t)MI * (size_t)MJ * sizeof(float);
 }
 
-extern "C" int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
-                           int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
-                           int32_t mode, float* out, int64_t ldo, int64_t so, void* workspace,
-                           size_t workspace_bytes, mgp_stream_t stream) {
+static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
+                          int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                          int32_t mode, float* out, int64_t ldo, int64_t so, void* workspace,
+                          size_t workspace_bytes, mgp_stream_t stream, const float* xb, const float* yb,
+                          const float* wb) {
+  const bool f16 = xb != nullptr;
   if (!X) return -1;
   if (ldx < N || ldx % 4) return -2;
   if (batch > 1 && sx % 4) return -3;
@@ -481,25 +523,43 @@ extern "C" int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, 
   float* ws = (float*)workspace;
   const int64_t bstride = MI * MJ, zstride = (int64_t)batch * MI * MJ;
   const dim3 grid((unsigned)(tiles * batch * nsplit));
-  if (mode) {
-    if (W)
-      hipLaunchKernelGGL((gram_x6_kernel<true, true>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, N,
-                         nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
-    else
-      hipLaunchKernelGGL((gram_x6_kernel<true, false>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw,
-                         N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
-  } else {
-    if (W)
-      hipLaunchKernelGGL((gram_x6_kernel<false, true>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw,
-                         N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
-    else
-      hipLaunchKernelGGL((gram_x6_kernel<false, false>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw,
-                         N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride);
-  }
+#define MGP_GRAM_X6(TRI, WT, F16)                                                                              \
+  if ((mode != 0) == TRI && (W != nullptr) == WT && f16 == F16)                                               \
+    hipLaunchKernelGGL((gram_x6_kernel<TRI, WT, F16>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, \
+                       N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride, xb, yb, wb);
+  MGP_GRAM_X6(true, true, false)
+  MGP_GRAM_X6(true, false, false)
+  MGP_GRAM_X6(false, true, false)
+  MGP_GRAM_X6(false, false, false)
+  MGP_GRAM_X6(true, true, true)
+  MGP_GRAM_X6(true, false, true)
+  MGP_GRAM_X6(false, true, true)
+  MGP_GRAM_X6(false, false, true)
+#undef MGP_GRAM_X6
   int st = launch_status();
   if (st) return st;
   const int64_t total = (int64_t)batch * MI * MJ;
   hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, bstride,
                      zstride, nsplit, MI, MJ, total, alpha, (int)mode, out, ldo, so);
   return launch_status();
+}
+
+extern "C" int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
+                           int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                           int32_t mode, float* out, int64_t ldo, int64_t so, void* workspace,
+                           size_t workspace_bytes, mgp_stream_t stream) {
+  return gram_x6_launch(X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, N, batch, alpha, mode, out, ldo, so, workspace,
+                        workspace_bytes, stream, nullptr, nullptr, nullptr);
+}
+
+extern "C" int mgp_gram_f16(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
+                            int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                            int32_t mode, float* out, int64_t ldo, int64_t so, const float* x_bound,
+                            const float* y_bound, const float* w_bound, void* workspace, size_t workspace_bytes,
+                            mgp_stream_t stream) {
+  if (!x_bound) return -18;
+  if (!y_bound) return -19;
+  if (W && !w_bound) return -20;
+  return gram_x6_launch(X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, N, batch, alpha, mode, out, ldo, so, workspace,
+                        workspace_bytes, stream, x_bound, y_bound, w_bound);
 }

@@ -121,7 +121,16 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
     const float* row = src + b * stride + r * ld;
     const int64_t c0 = TRI == 2 ? r : 0;
     const int64_t c1 = TRI == 1 ? (r + 1 < cols ? r + 1 : cols) : cols;
-    for (int64_t c = c0 + lane; c < c1; c += 64) m = fmaxf(m, fabsf(row[c]));
+    if (TRI == 0 && (ld & 3) == 0 && ((uintptr_t)row & 15) == 0) {  // float4 loads, scalar tail
+      const int64_t c4 = c1 & ~(int64_t)3;
+      for (int64_t c = 4 * lane; c < c4; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(row + c);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+      for (int64_t c = c4 + lane; c < c1; c += 64) m = fmaxf(m, fabsf(row[c]));
+    } else {
+      for (int64_t c = c0 + lane; c < c1; c += 64) m = fmaxf(m, fabsf(row[c]));
+    }
   }
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   m = fmaxf(m, __shfl_xor(m, 16, 64));
@@ -1012,13 +1021,18 @@ extern "C" int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, 
                            int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
                            int32_t mode, float* out, int64_t ldo, int64_t so, void* workspace,
                            size_t workspace_bytes, mgp_stream_t stream);
+extern "C" int mgp_gram_f16(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
+                            int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                            int32_t mode, float* out, int64_t ldo, int64_t so, const float* x_bound,
+                            const float* y_bound, const float* w_bound, void* workspace, size_t workspace_bytes,
+                            mgp_stream_t stream);
 extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ldy, int64_t MJ,
                         int64_t N, float alpha, int32_t tri, float* out, int64_t ldo, void* workspace,
                         size_t workspace_bytes, mgp_stream_t stream);
 
 namespace {
 struct CondBwdWs {  // workspace carve-up (256-B aligned pieces)
-  size_t sfr, ga0, gafr, lifr, P, LT, part, gram, total;
+  size_t sfr, ga0, gafr, lifr, P, LT, part, bnd, gram, total;
 };
 size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
@@ -1033,6 +1047,7 @@ CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
   w.P = o;    o += al256((size_t)K * M * ldm * 4);
   w.LT = o;   o += al256((size_t)K * M * ldm * 4);
   w.part = o; o += al256((size_t)K * 8);
+  w.bnd = o;  o += 256;  // split-f16 bound: max |Gv|
   w.gram = o;
   size_t g = mgp_gram_x6_workspace_bytes(M, M, N, K, 2);
   g = g > mgp_gram_x6_workspace_bytes(M, M, M, K, 2) ? g : mgp_gram_x6_workspace_bytes(M, M, M, K, 2);
@@ -1202,8 +1217,20 @@ static int conditional_backward(
                      ldk);
   if ((st = launch_status())) return st;
   // 5. g_q_sqrt[k] = 2 tril(A diag(Gv_k) (L_k^T A)^T) = 2 tril(P_k L_k), P_k = A diag(Gv_k) A^T
-  //    (x6 grams over N, then over M with the transposed triangle of L_k)
-  st = mgp_gram_x6(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, gws, gwsb, stream);
+  //    (x6 grams over N, then over M with the transposed triangle of L_k); f16: the
+  //    grams over N on f16 products, bounds |A| <= sqrt(var) (Afr's trailer), max |Gv|
+  float* bnd = (float*)(ws + L.bnd);
+  const float* a_bound = trailer(const_cast<void*>(Afr), cols_planes(M, N));
+  if (f16) {
+    if ((st = hip_status(hipMemsetAsync(bnd, 0, sizeof(float), s)))) return st;
+    hipLaunchKernelGGL(absmax_kernel<0>, dim3((unsigned)std::min<int64_t>((K + 3) / 4, 256)), dim3(256), 0, s, Gv,
+                       ldg, (int64_t)0, (int64_t)K, N, (int64_t)K, (unsigned int*)bnd);
+    if ((st = launch_status())) return st;
+    st = mgp_gram_f16(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, a_bound, a_bound, bnd, gws,
+                      gwsb, stream);
+  } else {
+    st = mgp_gram_x6(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, gws, gwsb, stream);
+  }
   if (st) return st;
   hipLaunchKernelGGL(tril_transpose_kernel, dim3((unsigned)((M + 31) / 32), (unsigned)((M + 31) / 32), (unsigned)K),
                      dim3(256), 0, s, q_sqrt, ldqs, strideq, M, LT, ldm, M * ldm);
@@ -1211,7 +1238,10 @@ static int conditional_backward(
   st = mgp_gram_x6(P, ldm, M * ldm, M, LT, ldm, M * ldm, M, nullptr, 0, M, K, 2.f, 1, g_q_sqrt, ldgs, strideg, gws,
                    gwsb, stream);
   if (st) return st;
-  // 6. g_Lm = -tril(g_Kuf A^T), g_q_mu = A G_mu^T, g_var = sum G_v
+  // 6. g_Lm = -tril(g_Kuf A^T), g_q_mu = A G_mu^T, g_var = sum G_v.  g_Lm stays x6 in
+  //    both modes: it feeds the near-cancelling Z / lengthscale / variance gradients
+  //    through the Cholesky backward (split-f16 operands measured 3.6e-4 normwise on a
+  //    lengthscale gradient where float32 autograd is 2.2e-4)
   st = mgp_gram_x6(g_Kuf, ldk, 0, M, A, lda, 0, M, nullptr, 0, N, 1, -1.f, 1, g_Lm, ldgl, M * ldgl, gws, gwsb,
                    stream);
   if (st) return st;

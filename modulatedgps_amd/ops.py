@@ -469,10 +469,12 @@ def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):
     return out
 
 
-def gram_x6(X, Y, W=None, alpha=1.0, mode=0, N=None, out=None, workspace=None):
+def gram_x6(X, Y, W=None, alpha=1.0, mode=0, N=None, out=None, workspace=None, bounds=None):
     """out[b][i][j] = alpha * sum_n X[b][i][n] W[b][n] Y[b][j][n] at f32 accuracy on the bf16 MFMA.
     X [B, MI, >=N] / [MI, >=N] (Y likewise; a 2-D operand is shared by the batch); W [B, >=N] or None;
-    mode 0 full, 1 lower triangle, 2 symmetric."""
+    mode 0 full, 1 lower triangle, 2 symmetric.  bounds = (x_bound, y_bound, w_bound) float32
+    device tensors of max |X|, |Y|, |W| (w_bound None without W): the split-f16 variant
+    (mgp_gram_f16)."""
     X3 = X if X.dim() == 3 else X.unsqueeze(0)
     Y3 = Y if Y.dim() == 3 else Y.unsqueeze(0)
     B = max(X3.shape[0], Y3.shape[0], W.shape[0] if W is not None and W.dim() == 2 else 1)
@@ -488,6 +490,13 @@ def gram_x6(X, Y, W=None, alpha=1.0, mode=0, N=None, out=None, workspace=None):
     if workspace is None or workspace.numel() < nbytes:
         workspace = _ws(nbytes, dev)
     so = out.stride(0) if out.dim() == 3 else MI * _ld(out)
+    if bounds is not None:
+        xb, yb, wb = bounds
+        _lib.call("mgp_gram_f16", X3.data_ptr(), X3.stride(1), sx, MI, Y3.data_ptr(), Y3.stride(1), sy, MJ,
+                  W.data_ptr() if W is not None else None, sw, N, B, float(alpha), int(mode), out.data_ptr(),
+                  out.stride(-2), so, xb.data_ptr(), yb.data_ptr(), wb.data_ptr() if wb is not None else None,
+                  workspace.data_ptr(), workspace.numel(), _stream())
+        return out
     _lib.call("mgp_gram_x6", X3.data_ptr(), X3.stride(1), sx, MI, Y3.data_ptr(), Y3.stride(1), sy, MJ,
               W.data_ptr() if W is not None else None, sw, N, B, float(alpha), int(mode), out.data_ptr(),
               out.stride(-2), so, workspace.data_ptr(), workspace.numel(), _stream())

@@ -187,3 +187,11 @@ def test_gram_x6(device, MI, MJ, N, B, mode, weighted):
         ref = torch.tril(ref) + torch.tril(ref, -1).transpose(1, 2)
     got = to_np(out).reshape(B, MI, -1)[:, :, :MJ]
     assert normwise(got, ref.numpy()) < 2e-6
+    # split-f16 variant (mgp_gram_f16) with loose bounds (4x max |X|, the exact max |Y|, |W|):
+    # 22-bit operands, the same f32 accumulation
+    bx = torch.tensor([4 * float(X.abs().max())], device=device)
+    by = torch.tensor([float(Y.abs().max())], device=device)
+    bw = torch.tensor([float(W.abs().max())], device=device) if weighted else None
+    out16 = ops.gram_x6(Xd, Yd, Wd, alpha=-0.5, mode=mode, N=N, bounds=(bx, by, bw))
+    got16 = to_np(out16).reshape(B, MI, -1)[:, :, :MJ]
+    assert normwise(got16, ref.numpy()) < 4e-6
