@@ -79,6 +79,9 @@ def main():
                           ops._lib.load().mgp_gram_x6_workspace_bytes(M, M, N, 1, 1)), dtype=torch.uint8, device=dev)
     cb = ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N)
     wsc = torch.empty(ops.conditional_backward_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev)
+    A32h = ops.padded(M, N, dev)   # the f16 chain's training K4: f16 A image + f32 A
+    ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, A=A32h, f16_variance=var, in_fmt="f16")
+    cbh = ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N, fmt="f16")
     torch.cuda.synchronize()
     runs = {
         "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
@@ -107,6 +110,8 @@ def main():
         "rbf_bwd": lambda: ops.rbf_backward(X, Z, var, lsc, gK),
         "cond_bwd_x6": lambda: ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
                                                            out=cb, workspace=wsc),
+        "cond_bwd_f16": lambda: ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
+                                                            out=cbh, workspace=wsc, fmt="f16"),
     }
     if a.only:
         runs = {k: v for k, v in runs.items() if k in a.only.split(",")}
@@ -127,7 +132,7 @@ def main():
         if name in out:
             out[name]["tflops"] = M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
     for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N),
-                     ("cond_bwd_x6", (2 * K + 1) * M * M * N)):
+                     ("cond_bwd_x6", (2 * K + 1) * M * M * N), ("cond_bwd_f16", (2 * K + 1) * M * M * N)):
         if name in out:
             out[name]["tflops"] = fl / (out[name]["median_ms"] * 1e-3) / 1e12
     if "rbf_bwd" in out:

@@ -38,6 +38,10 @@ def kernel_key(name):
         return "trsm_stats_f16_kernel"          # split-f16 images in and out
     if base == "trsm_stats_x6_kernel" and flags[1:2] == ["true"]:
         return "trsm_stats_x6f16_kernel"        # split-bf16 in, split-f16 A image out
+    if base == "gram_x6_kernel" and flags[2:3] == ["true"]:
+        return "gram_f16_kernel"
+    if base == "grad_a_s_kernel" and flags[:1] == ["true"]:
+        return "grad_a_s_f16_kernel"
     if base in ("expert_cond_x6_kernel", "rbf_kuf_x6_kernel") and "true" in flags:
         return base.replace("_x6_", "_f16_")
     return base
