@@ -115,15 +115,21 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
                                                      unsigned int* __restrict__ out) {
   __shared__ float red[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // TRI 0: blockIdx.y strides over column chunks of kAbsChunk (few long rows)
+  constexpr int64_t kAbsChunk = 8192;
   float m = 0.f;
   for (int64_t gr = (int64_t)blockIdx.x * 4 + w; gr < nrows_total; gr += (int64_t)gridDim.x * 4) {
     const int64_t b = gr / rows, r = gr % rows;
     const float* row = src + b * stride + r * ld;
-    const int64_t c0 = TRI == 2 ? r : 0;
-    const int64_t c1 = TRI == 1 ? (r + 1 < cols ? r + 1 : cols) : cols;
-    if (TRI == 0 && (ld & 3) == 0 && ((uintptr_t)row & 15) == 0) {  // float4 loads, scalar tail
-      const int64_t c4 = c1 & ~(int64_t)3;
-      for (int64_t c = 4 * lane; c < c4; c += 256) {
+    int64_t c0 = TRI == 2 ? r : 0;
+    int64_t c1 = TRI == 1 ? (r + 1 < cols ? r + 1 : cols) : cols;
+    if (TRI == 0) {
+      c0 = (int64_t)blockIdx.y * kAbsChunk;
+      c1 = c0 + kAbsChunk < cols ? c0 + kAbsChunk : cols;
+    }
+    if (TRI != 2 && (ld & 3) == 0 && ((uintptr_t)row & 15) == 0) {  // float4 loads (c0 % 4 == 0), scalar tail
+      const int64_t c4 = c0 + ((c1 - c0) & ~(int64_t)3);
+      for (int64_t c = c0 + 4 * lane; c < c4; c += 256) {
         const float4 v = *reinterpret_cast<const float4*>(row + c);
         m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       }
@@ -141,6 +147,17 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
   if (lane == 0) red[w] = m;
   __syncthreads();
   if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+// Launch shape of absmax_kernel<TRI>: <= 256 row groups (one atomic per workgroup);
+// TRI 0 adds column chunks so a few long rows still fill the chip.
+template <int TRI>
+static void launch_absmax(const float* src, int64_t ld, int64_t stride, int64_t rows, int64_t cols,
+                          int64_t nrows_total, float* out, hipStream_t s) {
+  const int64_t gx = std::min<int64_t>((nrows_total + 3) / 4, TRI == 0 ? 64 : 256);
+  const int64_t gy = TRI == 0 ? std::min<int64_t>((cols + 8191) / 8192, 64) : 1;
+  hipLaunchKernelGGL(absmax_kernel<TRI>, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, src, ld, stride, rows,
+                     cols, nrows_total, (unsigned int*)out);
 }
 
 __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -941,8 +958,7 @@ extern "C" int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t st
   int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
   if (st) return st;
   const int64_t rows = (int64_t)K * M;
-  hipLaunchKernelGGL(absmax_kernel<1>, dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 256)), dim3(256), 0,
-                     s, q_sqrt, ldqs, strideq, M, M, rows, (unsigned int*)bound);
+  launch_absmax<1>(q_sqrt, ldqs, strideq, M, M, rows, bound, s);
   st = launch_status();
   if (st) return st;
   const int64_t Mp = x6_mp(M);
@@ -968,8 +984,7 @@ extern "C" int mgp_split_upper_f16(const float* LinvT, int64_t ldl, int64_t M, v
   float* bound = trailer(Tfr, lower_planes(M, 1));
   int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
   if (st) return st;
-  hipLaunchKernelGGL(absmax_kernel<2>, dim3((unsigned)std::min<int64_t>((M + 3) / 4, 256)), dim3(256), 0, s, LinvT,
-                     ldl, (int64_t)0, M, M, M, (unsigned int*)bound);
+  launch_absmax<2>(LinvT, ldl, (int64_t)0, M, M, M, bound, s);
   st = launch_status();
   if (st) return st;
   const int64_t Mp = x6_mp(M);
@@ -994,8 +1009,7 @@ extern "C" int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_
   float* bound = trailer(Afr, cols_planes(M, N));
   int st = hip_status(hipMemsetAsync(bound, 0, sizeof(float), s));
   if (st) return st;
-  hipLaunchKernelGGL(absmax_kernel<0>, dim3((unsigned)std::min<int64_t>((M + 3) / 4, 256)), dim3(256), 0, s,
-                     A, lda, (int64_t)0, M, N, M, (unsigned int*)bound);
+  launch_absmax<0>(A, lda, (int64_t)0, M, N, M, bound, s);
   st = launch_status();
   if (st) return st;
   const int nmk = (int)(x6_mp(M) / 16);
@@ -1175,8 +1189,7 @@ static int conditional_backward(
     float* s_bound = trailer(Sfr, lower_planes(M, K));
     if (f16) {  // max |S_k| over the experts into the image trailer, then the scaled split
       if ((st = hip_status(hipMemsetAsync(s_bound, 0, sizeof(float), s)))) return st;
-      hipLaunchKernelGGL(absmax_kernel<0>, dim3((unsigned)std::min<int64_t>(((int64_t)K * M + 3) / 4, 256)),
-                         dim3(256), 0, s, LT, ldm, M * ldm, M, M, (int64_t)K * M, (unsigned int*)s_bound);
+      launch_absmax<0>(LT, ldm, M * ldm, M, M, (int64_t)K * M, s_bound, s);
     }
     hipLaunchKernelGGL((split_tri_kernel<true, false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, LT,
                        ldm, M * ldm, M, nmb, nmk, nfrag, Sfr, f16 ? (const float*)s_bound : nullptr);
@@ -1223,8 +1236,7 @@ static int conditional_backward(
   const float* a_bound = trailer(const_cast<void*>(Afr), cols_planes(M, N));
   if (f16) {
     if ((st = hip_status(hipMemsetAsync(bnd, 0, sizeof(float), s)))) return st;
-    hipLaunchKernelGGL(absmax_kernel<0>, dim3((unsigned)std::min<int64_t>((K + 3) / 4, 256)), dim3(256), 0, s, Gv,
-                       ldg, (int64_t)0, (int64_t)K, N, (int64_t)K, (unsigned int*)bnd);
+    launch_absmax<0>(Gv, ldg, (int64_t)0, (int64_t)K, N, (int64_t)K, bnd, s);
     if ((st = launch_status())) return st;
     st = mgp_gram_f16(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, a_bound, a_bound, bnd, gws,
                       gwsb, stream);
