@@ -224,7 +224,7 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
                                             int mk_end, int nmk, bool init = true) {
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t vB = 16u * lane;
-  const uint32_t sB1 = sB0 + (uint32_t)nmk * 3u * kFragBytes;
+  const uint32_t sBc = (uint32_t)nmk * 3u * kFragBytes;  // B block nb0 + c at sB0 + c sBc
   // T stage: 256 NPL 16-B units per k-step, NPL per thread: unit e = tid + 256 s ->
   //   row sub-tile i = e / (64 NPL), plane p = (e / 64) % NPL, lane e % 64
   //   byte offset tbase + ((i * nmk + mk) * 192 + p * 64 + lane) * 16; LDS unit (3 i + p) * 64 + lane
@@ -248,10 +248,9 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
   auto load_b = [&](bf16x8 (&b)[NC][3], int mk) {
     const uint32_t o = (uint32_t)mk * 3u * kFragBytes;
 #pragma unroll
-    for (int p = 0; p < NPL; ++p) {
-      b[0][p] = ld_frag(rB, vB, sB0 + o + p * kFragBytes);
-      if constexpr (NC > 1) b[1][p] = ld_frag(rB, vB, sB1 + o + p * kFragBytes);
-    }
+    for (int p = 0; p < NPL; ++p)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) b[c][p] = ld_frag(rB, vB, sB0 + c * sBc + o + p * kFragBytes);
   };
   auto load_t = [&](u32x4v (&st)[NPL], int mk) {
     const uint32_t o = tbase + (uint32_t)mk * 192u * 16u;
