@@ -907,8 +907,8 @@ static int trsm_stats_f16_out(const void* Tfr, size_t tfr_bytes, const void* Kfr
   if (!variance) return -10;
   if (!Afr) return -11;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -12;
-  if (!stats) return -13;
-  if (lds < N) return -14;
+  if (stats && lds < N) return -14;  // stats may be NULL (A image only)
+  
   if (!aligned16(Tfr) || !aligned16(Kfr) || !aligned16(Afr)) return MGP_ERR_ALIGN;
   if (mgp_x6_cols_bytes(M, N) >= ((size_t)1 << 32) || mgp_x6_lower_bytes(M, 1) >= ((size_t)1 << 32))
     return MGP_ERR_UNSUPPORTED;

@@ -102,6 +102,9 @@ def main():
         "split_upper_f16": lambda: ops.split_upper_x6(LinvT[0], out=Thr, fmt="f16"),
         "trsm_stats_f16": lambda: ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var,
                                                     in_fmt="f16"),
+        "trsm_f16_nostats": lambda: ops._lib.call("mgp_trsm_stats_f16", Thr.data_ptr(), Thr.numel(), Khr.data_ptr(),
+                                                  Khr.numel(), M, N, q_mu.data_ptr(), K, K, var.data_ptr(),
+                                                  Ahr.data_ptr(), Ahr.numel(), None, N, None, N, ops._stream()),
         "split_lower_f16": lambda: ops.split_lower_x6(q_sqrt, out=Lhr, fmt="f16"),
         "expert_cond_f16": lambda: ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmean=fm6, fvar=fv6,
                                                              fmt="f16"),
