@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--format", default=None, choices=("x6", "f16"),
                     help="image format of the forward K4 -> K5 hand-off: x6 (split-bf16, 6 products) or f16 "
                          "(split-f16, 3 products, 22-bit operands); default: modulatedgps_amd.config")
+    ap.add_argument("--cross", default=None, choices=("f16", "f8"),
+                    help="split-f16 K5: cross terms a_hi b_lo + a_lo b_hi on f16 (3 f16 products) or on one "
+                         "e4m3 MFMA per two k-steps (f16x8); default: modulatedgps_amd.config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-modes", action="store_true", help="skip the reduced-plane K5 side measurements")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (ELBO + gradient + Adam) leg")
@@ -191,8 +194,24 @@ def k5_modes_leg(elbo_step, args, fmt, steps=10):
     5's 'bf16 mixed'); their measured fvar error vs the float64 oracle at c3 shapes
     is asserted in tests/test_gpu_kernels.py::test_expert_conditional_planes (2
     planes ~3e-6, 1 plane ~2e-3 normwise) and tests/test_gpu_f16.py."""
-    from modulatedgps_amd.config import set_expert_format, set_expert_planes
+    from modulatedgps_amd.config import expert_cross, set_expert_cross, set_expert_format, set_expert_planes
     out = {}
+    cross = expert_cross()
+    if fmt == "f16":  # the other cross-term precision on the same images
+        set_expert_cross("f16" if cross == "f8" else "f8")
+        for _ in range(2):
+            elbo_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            elbo_step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        out["f16x3" if cross == "f8" else "f16x8"] = {
+            "value": 1.0 / dt, "unit": "ELBO steps/s", "ms_per_step": dt * 1e3,
+            "k5_f16_product_equivalents": 3 if cross == "f8" else 2,
+            "accuracy": "f32 class (tests/test_gpu_f16.py)"}
+        set_expert_cross(cross)
     other = "x6" if fmt == "f16" else "f16"
     set_expert_format(other)
     for _ in range(2):
@@ -262,14 +281,18 @@ def train_leg(model, X, Y, kw, args, barrier, world, device):
 
 def main():
     args = parse()
-    from modulatedgps_amd.config import conditional_mode, expert_format, set_expert_format, set_expert_planes
+    from modulatedgps_amd.config import (conditional_mode, expert_cross, expert_format, set_expert_cross,
+                                         set_expert_format, set_expert_planes)
     x6 = conditional_mode() == "x6"
     set_expert_planes(args.planes)
     fmt = args.format or expert_format()
     set_expert_format(fmt)
+    set_expert_cross(args.cross or expert_cross())
     f16 = x6 and fmt == "f16" and args.planes == 3
-    # 6 / 3 / 1 bf16 MFMA products per f32 product; split-f16: 3 f16 products (same rate)
-    k5_products = 3 if f16 else args.planes * (args.planes + 1) // 2
+    f16x8 = f16 and expert_cross() == "f8"
+    # 6 / 3 / 1 bf16 MFMA products per f32 product; split-f16: 3 f16 products (same rate);
+    # f16x8: 1 f16 product + half an e4m3 32x32x64 MFMA (2x rate) = 2 f16-product equivalents
+    k5_products = (2 if f16x8 else 3) if f16 else args.planes * (args.planes + 1) // 2
     peak_k5 = PEAK_BF16_MFMA / k5_products if x6 else PEAK_F32_MFMA
     from modulatedgps_amd.distributed import init_from_env
     # MGP_BENCH_BACKEND=gloo + MGP_BENCH_SHARE_GPU=1: rehearsal of the multi-rank path
@@ -358,15 +381,20 @@ def main():
             kernels[name] = {"avg_us": st[name][0] * 1e3}
 
     ek = kernels.get("expert_cond", {})
-    kname = ("expert_cond_f16_kernel" if f16 else "expert_cond_x6_kernel") if x6 else "expert_cond_kernel"
+    kname = (("expert_cond_f16x8_kernel" if f16x8 else "expert_cond_f16_kernel") if f16 else
+             "expert_cond_x6_kernel") if x6 else "expert_cond_kernel"
     traffic, traffic_src = load_traffic(kname)
-    klabel = "expert_cond_x6_kernel<2, true> (split-f16 instance)" if kname == "expert_cond_f16_kernel" else kname
+    klabel = {"expert_cond_f16_kernel": "expert_cond_x6_kernel<2, true, false> (split-f16 instance)",
+              "expert_cond_f16x8_kernel": "expert_cond_x6_kernel<2, true, true> (split-f16 + e4m3 cross terms)"
+              }.get(kname, kname)
     roofline = {"kernel": f"{klabel} (K5, L_k^T A + sum of squares, + cond_finalize)", "bound": "mfma",
                 "achieved": ek.get("achieved"), "peak": peak_k5 / 1e12,
                 "unit": "TFLOP/s", "frac": ek.get("frac"), "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_per_launch": f"K*M^2*N = {expert_flops:.4g} f32 flop",
-                "peak_note": ("split-f16: each f32 product is 3 f16 MFMA products, peak = 2.5 PF f16 dense / 3"
+                "peak_note": ("split-f16 + e4m3 cross terms: each f32 product is 1 f16 MFMA product + both "
+                              "cross products at e4m3 (2x rate), peak = 2.5 PF f16 dense / 2" if f16x8 else
+                              "split-f16: each f32 product is 3 f16 MFMA products, peak = 2.5 PF f16 dense / 3"
                               if f16 else
                               f"split-bf16: each f32 product is {k5_products} bf16 MFMA products, peak = "
                               f"2.5 PF bf16 dense / {k5_products}" if x6 else "f32 MFMA dense peak")}
@@ -392,6 +420,8 @@ def main():
             "dtype_note": (("f32 operands and accumulation; K1/K4 products on bf16 MFMA via an exact 3-plane "
                             "split (6 products) in training; the forward chain K1 -> K4 -> K5 on f16 MFMA via "
                             "power-of-two-scaled 2-plane fp16 splits (22-bit operands, 3 products); K3 in f64")
+                           + ("; K5's two cross terms (2^-11 of the leading product) on the e4m3 MFMA"
+                              if f16x8 else "")
                            if f16 else
                            ("f32 operands and accumulation; K5 products on bf16 MFMA via an exact "
                             "3-plane split (6 products, f32-accurate); K3 in f64") if x6 and args.planes == 3 else
@@ -413,6 +443,7 @@ def main():
             "train": train,
             "k5_modes": modes,
             "k5_image_format": fmt if x6 else None,
+            "k5_cross_terms": expert_cross() if f16 else None,
             "elbo": elbo_val, "cholesky_info": info,
         }
         print(json.dumps(out))

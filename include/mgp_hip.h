@@ -220,6 +220,16 @@ int mgp_expert_conditional_f16(const void* Afr, size_t afr_bytes, const void* Lf
                                const float* stats, int64_t lds, const float* variance, int64_t M,
                                int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
                                void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+/* K5 "f16x8": the same split-f16 images (every split-f16 producer also writes
+ * plane 2 = e4m3(hi 2^-6) | e4m3(lo 2^6) of each fragment); the hi products on
+ * the f16 MFMA, both cross terms of two k-steps on one e4m3 MFMA
+ * (v_mfma_scale_f32_32x32x64_f8f6f4, unit scales): 4 f16-product-equivalents
+ * per k-step pair instead of 6.  Cross terms are <= 2^-11 of the leading one,
+ * so e4m3's 3-bit mantissas cost ~2^-15 relative per product. */
+int mgp_expert_conditional_f16x8(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                 const float* stats, int64_t lds, const float* variance, int64_t M,
+                                 int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                                 void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- backward of K1-K5
  * Gram products over the data dimension (float32 MFMA, deterministic split-K):

@@ -114,6 +114,8 @@ SIGNATURES = {
                                           c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "mgp_expert_conditional_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
                                                   c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_expert_conditional_f16x8": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
+                                                    c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_kl_workspace_bytes": (c_size, [c_i64, c_i32]),
     "mgp_gauss_kl_white": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr,
                                           c_ptr, c_size, c_ptr]),

@@ -22,7 +22,13 @@ import torch
 #              backward); the reduced-plane modes use "x6".
 _CFG = {"jitter": 1e-6, "device": None, "conditional": os.environ.get("MGP_CONDITIONAL", "x6"),
         "expert_planes": int(os.environ.get("MGP_K5_PLANES", "3")),
-        "expert_format": os.environ.get("MGP_K5_FORMAT", "f16")}
+        "expert_format": os.environ.get("MGP_K5_FORMAT", "f16"),
+        "expert_cross": os.environ.get("MGP_K5_CROSS", "f16")}
+# expert_cross (f16 images): the precision of K5's two cross-term products
+#              a_hi b_lo + a_lo b_hi -- "f16" (three f16 products) or "f8" (one
+#              e4m3 MFMA per two k-steps for both, mgp_expert_conditional_f16x8:
+#              the cross terms are 2^-11 of the leading product, so their 3-bit
+#              mantissas cost ~2^-15 relative; tests/test_gpu_f16.py measures it).
 
 
 def default_jitter():
@@ -77,6 +83,16 @@ def set_expert_format(fmt):
     if fmt not in ("x6", "f16"):
         raise ValueError("expert_format must be 'x6' or 'f16'")
     _CFG["expert_format"] = fmt
+
+
+def expert_cross():
+    return _CFG["expert_cross"]
+
+
+def set_expert_cross(cross):
+    if cross not in ("f16", "f8"):
+        raise ValueError("expert_cross must be 'f16' or 'f8'")
+    _CFG["expert_cross"] = cross
 
 
 def forward_image_format(train=False):

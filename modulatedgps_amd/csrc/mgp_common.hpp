@@ -114,6 +114,11 @@ __device__ __forceinline__ int img_exp(float bound) {
   return 13 - ilogbf(bound);
 }
 
+// X8: plane 2 also gets the fp8 cross-term plane of the same 8 values (K5's
+// "f16x8" mode, mfma_f8x): dwords 0-1 = e4m3(hi 2^-6), dwords 2-3 = e4m3(lo 2^6).
+// With the image maximum in [2^13, 2^14) both land in e4m3's range (<= 2^8):
+// hi 2^-6 keeps 3 mantissa bits down to 2^-14 of the maximum, lo 2^6 likewise.
+template <bool X8 = false>
 __device__ __forceinline__ void store_split_f16(bf16x8* __restrict__ dst, const float (&v)[8], float scale) {
   halfx8 h, l;
 #pragma unroll
@@ -125,11 +130,39 @@ __device__ __forceinline__ void store_split_f16(bf16x8* __restrict__ dst, const 
   }
   dst[0] = __builtin_bit_cast(bf16x8, h);
   dst[64] = __builtin_bit_cast(bf16x8, l);
+  if constexpr (X8) {
+    u32x4v x8;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      int wh = 0, wl = 0;
+      wh = __builtin_amdgcn_cvt_pk_fp8_f32((float)h[4 * q] * 0x1p-6f, (float)h[4 * q + 1] * 0x1p-6f, wh, false);
+      wh = __builtin_amdgcn_cvt_pk_fp8_f32((float)h[4 * q + 2] * 0x1p-6f, (float)h[4 * q + 3] * 0x1p-6f, wh, true);
+      wl = __builtin_amdgcn_cvt_pk_fp8_f32((float)l[4 * q] * 0x1p6f, (float)l[4 * q + 1] * 0x1p6f, wl, false);
+      wl = __builtin_amdgcn_cvt_pk_fp8_f32((float)l[4 * q + 2] * 0x1p6f, (float)l[4 * q + 3] * 0x1p6f, wl, true);
+      x8[q] = (uint32_t)wh;
+      x8[2 + q] = (uint32_t)wl;
+    }
+    dst[128] = __builtin_bit_cast(bf16x8, x8);
+  }
 }
 
 __device__ __forceinline__ floatx16 mfma_f16(bf16x8 a, bf16x8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c,
                                                 0, 0, 0);
+}
+
+// Cross terms of two k-steps (k, k') of split-f16 images on one e4m3 MFMA
+// (2x the f16 rate per flop): a_hi b_lo + a_lo b_hi over 64 k.  ax, bx are the
+// X8 planes (store_split_f16<true>); b's hi/lo halves are swapped so that every
+// a_hi 2^-6 byte meets the b_lo 2^6 byte of the same k (the scales cancel; A
+// and B share the per-lane k distribution, so any consistent pairing works).
+typedef int intx8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ floatx16 mfma_f8x(bf16x8 ax0, bf16x8 ax1, bf16x8 bx0, bf16x8 bx1, floatx16 acc) {
+  const u32x4v a0 = __builtin_bit_cast(u32x4v, ax0), a1 = __builtin_bit_cast(u32x4v, ax1);
+  const u32x4v b0 = __builtin_bit_cast(u32x4v, bx0), b1 = __builtin_bit_cast(u32x4v, bx1);
+  const intx8 a = {(int)a0[0], (int)a0[1], (int)a0[2], (int)a0[3], (int)a1[0], (int)a1[1], (int)a1[2], (int)a1[3]};
+  const intx8 b = {(int)b0[2], (int)b0[3], (int)b0[0], (int)b0[1], (int)b1[2], (int)b1[3], (int)b1[0], (int)b1[1]};
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 0, 0, 0, 127, 0, 127);
 }
 
 // F16 images (NPL = 2): a_hi b_hi + a_hi b_lo + a_lo b_hi, smallest first.

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
     v[j] = (m < M && mc < M && keep) ? S[TRANS ? mc * ld + m : m * ld + mc] : 0.f;
   }
   if (bound)
-    store_split_f16(img + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
+    store_split_f16<true>(img + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
   else
     store_split(img + f * 3 * 64 + lane, v);
 }
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void split_cols_kernel(const float* __restrict
     v[j] = (m < M && n < N) ? A[m * lda + n] : 0.f;
   }
   if (bound)
-    store_split_f16(Afr + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
+    store_split_f16<true>(Afr + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
   else
     store_split(Afr + f * 3 * 64 + lane, v);
 }
@@ -217,11 +217,16 @@ using ic = std::integral_constant<int, V>;
 // NPL: planes used (3 = x6 products; 2, 1 = K5's reduced modes, mfma_planes):
 // only those planes are loaded and staged.
 // F16: the images are split-f16 (mfma_fmt), NPL must be 2.
-template <int DIAG, int NC = 2, int NPL = 3, bool F16 = false>
+// X8 (with F16): image planes 0 (f16 hi) and 2 (e4m3 cross terms) are loaded;
+// per k-step pair, two f16 hi products and one e4m3 MFMA for both pairs of
+// cross terms (mfma_f8x): 2 + 2 f16-product-equivalents instead of 6.
+template <int DIAG, int NC = 2, int NPL = 3, bool F16 = false, bool X8 = false>
 __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)[4 * 3 * 64],
                                             __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
                                             __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
                                             int mk_end, int nmk, bool init = true) {
+  static_assert(!X8 || (F16 && NPL == 2), "X8 reads split-f16 images");
+  auto PL = [](int p) { return (X8 && p == 1) ? 2 : p; };  // LDS / register plane -> image plane
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t vB = 16u * lane;
   const uint32_t sBc = (uint32_t)nmk * 3u * kFragBytes;  // B block nb0 + c at sB0 + c sBc
@@ -233,7 +238,7 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
 #pragma unroll
   for (int s = 0; s < NPL; ++s) {
     const int e = tid + 256 * s, i = e / (64 * NPL), p = (e / 64) % NPL;
-    vT[s] = (uint32_t)((i * nmk * 192 + p * 64 + (e & 63)) * 16);
+    vT[s] = (uint32_t)((i * nmk * 192 + PL(p) * 64 + (e & 63)) * 16);
     dT[s] = (3 * i + p) * 64 + (e & 63);
   }
   if (init) {
@@ -250,7 +255,7 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
 #pragma unroll
     for (int p = 0; p < NPL; ++p)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) b[c][p] = ld_frag(rB, vB, sB0 + c * sBc + o + p * kFragBytes);
+      for (int c = 0; c < NC; ++c) b[c][p] = ld_frag(rB, vB, sB0 + c * sBc + o + PL(p) * kFragBytes);
   };
   auto load_t = [&](u32x4v (&st)[NPL], int mk) {
     const uint32_t o = tbase + (uint32_t)mk * 192u * 16u;
@@ -273,6 +278,27 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     }
   };
 
+  // X8: the first k-step of a pair keeps its cross-term fragments for the second
+  bf16x8 ax_s[4], bx_s[NC];
+  auto compute_x8 = [&](int buf, const bf16x8 (&b)[NC][3], auto ilo, auto ihi, auto second) {
+    constexpr int ILO = decltype(ilo)::value, IHI = decltype(ihi)::value;
+    constexpr bool SECOND = decltype(second)::value;
+#pragma unroll
+    for (int i = ILO; i < IHI; ++i) {
+      const bf16x8 a_hi = sL[buf][(i * 3) * 64 + lane], a_x = sL[buf][(i * 3 + 1) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if constexpr (SECOND) acc[i][c] = mfma_f8x(ax_s[i], a_x, bx_s[c], b[c][1], acc[i][c]);
+        acc[i][c] = mfma_f16(a_hi, b[c][0], acc[i][c]);
+      }
+      if constexpr (!SECOND) ax_s[i] = a_x;
+    }
+    if constexpr (!SECOND) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) bx_s[c] = b[c][1];
+    }
+  };
+
   bf16x8 b0[NC][3], b1[NC][3];
   u32x4v st[NPL];
   load_t(st, mk_begin);
@@ -286,7 +312,10 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     load_t(st, mk + 1);
     load_b(b1, mk + 1);
     __builtin_amdgcn_sched_barrier(0);
-    compute(0, b0, ilo, ihi);
+    if constexpr (X8)
+      compute_x8(0, b0, ilo, ihi, std::false_type{});
+    else
+      compute(0, b0, ilo, ihi);
     __builtin_amdgcn_sched_barrier(0);
     store_t(1, st);
     __syncthreads();
@@ -294,7 +323,10 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     load_t(st, m2);
     load_b(b0, m2);
     __builtin_amdgcn_sched_barrier(0);
-    compute(1, b1, ilo, ihi);
+    if constexpr (X8)
+      compute_x8(1, b1, ilo, ihi, std::true_type{});
+    else
+      compute(1, b1, ilo, ihi);
     __builtin_amdgcn_sched_barrier(0);
     store_t(0, st);
     __syncthreads();
@@ -325,7 +357,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const void* p, uint32
 
 // ------------------------------------------------------------------ K5 (x6)
 // F16: split-f16 images (NPL = 2) scaled by 2^img_exp(*a_bound), 2^img_exp(*l_bound).
-template <int NPL, bool F16 = false>
+// X8: their hi planes on f16 MFMA and cross terms on e4m3 MFMA (mfma_f8x).
+template <int NPL, bool F16 = false, bool X8 = false>
 __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
                                                                 const bf16x8* __restrict__ Lfr,
                                                                 uint32_t afr_bytes, uint32_t lfr_bytes,
@@ -340,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   floatx16 acc[4][2];
-  x6_mainloop<1, 2, NPL, F16>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+  x6_mainloop<1, 2, NPL, F16, X8>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
               img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
@@ -605,7 +638,7 @@ __device__ __forceinline__ void trsm_stats_x6_item(
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j];
         if constexpr (F16OUT)
-          store_split_f16(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v, a_scale);
+          store_split_f16<true>(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v, a_scale);
         else
           store_split(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v);
       }
@@ -771,7 +804,8 @@ extern "C" size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K)
 static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
                               const float* stats, int64_t lds, const float* variance, int64_t M, int64_t N,
                               int32_t K, int planes, float* fmean, float* fvar, int64_t ldf, void* workspace,
-                              size_t workspace_bytes, mgp_stream_t stream, bool f16 = false) {
+                              size_t workspace_bytes, mgp_stream_t stream, bool f16 = false,
+                              bool x8 = false) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!Lfr) return -3;
@@ -798,16 +832,17 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
   const dim3 grid((unsigned)(K * nTp * nTn));
   const float* a_bound = trailer(const_cast<void*>(Afr), cols_planes(M, N));
   const float* l_bound = trailer(const_cast<void*>(Lfr), lower_planes(M, K));
-#define MGP_K5_CASE(NP, F16)                                                                            \
-  if (planes == NP && f16 == F16)                                                                       \
-    hipLaunchKernelGGL((expert_cond_x6_kernel<NP, F16>), grid, dim3(256), 0, s, (const bf16x8*)Afr,     \
+#define MGP_K5_CASE(NP, F16, X8)                                                                        \
+  if (planes == NP && f16 == F16 && x8 == X8)                                                           \
+    hipLaunchKernelGGL((expert_cond_x6_kernel<NP, F16, X8>), grid, dim3(256), 0, s, (const bf16x8*)Afr, \
                        (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N),                           \
                        (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N, part, ldp, a_bound,     \
                        l_bound);
-  MGP_K5_CASE(3, false)
-  MGP_K5_CASE(2, false)
-  MGP_K5_CASE(1, false)
-  MGP_K5_CASE(2, true)
+  MGP_K5_CASE(3, false, false)
+  MGP_K5_CASE(2, false, false)
+  MGP_K5_CASE(1, false, false)
+  MGP_K5_CASE(2, true, false)
+  MGP_K5_CASE(2, true, true)
 #undef MGP_K5_CASE
   int st = launch_status();
   if (st) return st;
@@ -1024,6 +1059,16 @@ extern "C" int mgp_expert_conditional_f16(const void* Afr, size_t afr_bytes, con
                                           void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
   return expert_cond_planes(Afr, afr_bytes, Lfr, lfr_bytes, stats, lds, variance, M, N, K, 2, fmean, fvar, ldf,
                             workspace, workspace_bytes, stream, true);
+}
+
+// Same images as mgp_expert_conditional_f16 (every split-f16 producer writes the
+// X8 plane): hi products on f16, cross terms on e4m3 (mfma_f8x).
+extern "C" int mgp_expert_conditional_f16x8(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                            const float* stats, int64_t lds, const float* variance, int64_t M,
+                                            int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                                            void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  return expert_cond_planes(Afr, afr_bytes, Lfr, lfr_bytes, stats, lds, variance, M, N, K, 2, fmean, fvar, ldf,
+                            workspace, workspace_bytes, stream, true, true);
 }
 
 // ------------------------------------------------------------------ conditional backward (x6)

@@ -321,10 +321,12 @@ def split_cols_x6(A, out=None, fmt="x6"):
 
 
 def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=None, workspace=None, planes=3,
-                          fmt="x6"):
+                          fmt="x6", cross=None):
     """fmean, fvar [K, N] of the whitened K-expert conditional from split-bf16 images
     (planes < 3: K5 on the leading bf16 planes only, mgp_expert_conditional_planes;
-    fmt "f16": from split-f16 images, mgp_expert_conditional_f16)."""
+    fmt "f16": from split-f16 images, mgp_expert_conditional_f16, or with cross "f8"
+    (default: config.expert_cross()) mgp_expert_conditional_f16x8, the cross terms
+    on the e4m3 MFMA)."""
     _check(stats, "stats", 3)
     dev = stats.device
     if fmean is None:
@@ -337,7 +339,9 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
     if workspace is None or workspace.numel() < nbytes:
         workspace = _ws(nbytes, dev)
     if _fmt(fmt) == "f16":
-        _lib.call("mgp_expert_conditional_f16", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
+        from .config import expert_cross
+        entry = "mgp_expert_conditional_f16x8" if (cross or expert_cross()) == "f8" else "mgp_expert_conditional_f16"
+        _lib.call(entry, Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
                   stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(),
                   fvar.data_ptr(), _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
     elif planes == 3:

@@ -13,22 +13,24 @@ from tests.helpers import build_model, dev_noise, load_golden, normwise, params_
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["x6", "f16"])
+@pytest.fixture(params=["x6", "f16", "f16x8"])
 def fmt_mode(request):
-    """Both forward image formats end to end (tests/test_gpu_model.py runs the
-    default one)."""
+    """Both forward image formats end to end, and the split-f16 K5 with its cross
+    terms on the e4m3 MFMA (tests/test_gpu_model.py runs the default one)."""
     from modulatedgps_amd import config
-    old = config.expert_format()
-    config.set_expert_format(request.param)
+    old, old_cross = config.expert_format(), config.expert_cross()
+    config.set_expert_format("x6" if request.param == "x6" else "f16")
+    config.set_expert_cross("f8" if request.param == "f16x8" else "f16")
     yield request.param
     config.set_expert_format(old)
+    config.set_expert_cross(old_cross)
 
 
 def _t(a, device):
     return torch.as_tensor(np.asarray(a, np.float32), device=device)
 
 
-def _k5_only(ops, A, qs, M, N, K, fmt, device):
+def _k5_only(ops, A, qs, M, N, K, fmt, device, cross="f16"):
     """K5's own term: fvar = sum_m' (L^T A)^2 with zero stats and zero variance."""
     Afr = ops.split_cols_x6(A, fmt=fmt)
     Lfr = ops.split_lower_x6(qs, fmt=fmt)
@@ -36,7 +38,7 @@ def _k5_only(ops, A, qs, M, N, K, fmt, device):
     stats = ops.padded(T * (K + 1), N, device).unflatten(0, (T, K + 1))
     stats.zero_()
     zero = torch.zeros(1, dtype=torch.float32, device=device)
-    fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, zero, M, N, K, fmt=fmt)
+    fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, zero, M, N, K, fmt=fmt, cross=cross)
     return to_np(fm), to_np(fv)
 
 
@@ -60,9 +62,12 @@ def test_expert_f16_scale_invariance(device, sa, sl):
     err16 = normwise(fv, ref)
     _, fv6 = _k5_only(ops, Ad, qd, M, N, K, "x6", device)
     err6 = normwise(fv6, ref)
-    print(f"scale ({sa:g}, {sl:g}): f16x3 {err16:.2e}  x6 {err6:.2e}")
+    fm8, fv8 = _k5_only(ops, Ad, qd, M, N, K, "f16", device, cross="f8")
+    err8 = normwise(fv8, ref)
+    print(f"scale ({sa:g}, {sl:g}): f16x3 {err16:.2e}  f16x8 {err8:.2e}  x6 {err6:.2e}")
     assert err16 < 3e-7 and err16 < 1.5 * err6       # measured 1.0e-7 (x6 1.0e-7) at every scale
-    assert np.all(np.isfinite(fv))
+    assert np.all(np.isfinite(fv)) and np.all(np.isfinite(fv8)) and np.all(fm8 == 0)
+    assert err8 < 1e-5
 
 
 def test_expert_conditional_f16_accuracy(device):
@@ -91,12 +96,17 @@ def test_expert_conditional_f16_accuracy(device):
     Afr, stats = ops.trsm_stats_x6(Thr, Khr, qm, M, N, f16_variance=var, in_fmt="f16")
     fm, fv = ops.expert_conditional_x6(Afr, ops.split_lower_x6(qs, fmt="f16"), stats, var, M, N, K, fmt="f16")
     errs["f16 chain"] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))
+    fm, fv = ops.expert_conditional_x6(Afr, ops.split_lower_x6(qs, fmt="f16"), stats, var, M, N, K, fmt="f16",
+                                       cross="f8")
+    errs["f16x8 chain"] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))
     print("fmean / fvar normwise error vs float64:", errs)
     assert errs["f16"][0] == errs["x6"][0]            # fmean comes from K4's stats in both
     assert errs["f16"][1] < 1e-4
     assert errs["f16"][1] < 1.5 * errs["x6"][1]        # measured 7.34e-7 vs x6 7.31e-7
     assert errs["f16 chain"][0] < 1e-4 and errs["f16 chain"][1] < 1e-4
     assert errs["f16 chain"][0] < 8 * errs["x6"][0] and errs["f16 chain"][1] < 8 * errs["x6"][1]
+    assert errs["f16x8 chain"][0] == errs["f16 chain"][0]  # fmean from K4's stats
+    assert errs["f16x8 chain"][1] < 1e-4
 
 
 @pytest.mark.parametrize("case", ["case_demo_init", "case_demo_perturbed", "case_c1"])

@@ -107,7 +107,9 @@ def main():
                                                   Ahr.data_ptr(), Ahr.numel(), None, N, None, N, ops._stream()),
         "split_lower_f16": lambda: ops.split_lower_x6(q_sqrt, out=Lhr, fmt="f16"),
         "expert_cond_f16": lambda: ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmean=fm6, fvar=fv6,
-                                                             fmt="f16"),
+                                                             fmt="f16", cross="f16"),
+        "expert_cond_f16x8": lambda: ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmean=fm6, fvar=fv6,
+                                                               fmt="f16", cross="f8"),
         "gram_x6_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg),
         "gram_x6_Lm": lambda: ops.gram_x6(gK, A32, None, mode=1, N=N, out=gLm, workspace=wsg),
         "rbf_bwd": lambda: ops.rbf_backward(X, Z, var, lsc, gK),
@@ -129,8 +131,9 @@ def main():
         out["expert_cond"]["tflops"] = K * M * M * N / (out["expert_cond"]["median_ms"] * 1e-3) / 1e12
     if "expert_cond_x6" in out:
         out["expert_cond_x6"]["tflops"] = K * M * M * N / (out["expert_cond_x6"]["median_ms"] * 1e-3) / 1e12
-    if "expert_cond_f16" in out:
-        out["expert_cond_f16"]["tflops"] = K * M * M * N / (out["expert_cond_f16"]["median_ms"] * 1e-3) / 1e12
+    for name in ("expert_cond_f16", "expert_cond_f16x8"):
+        if name in out:
+            out[name]["tflops"] = K * M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
     for name in ("trsm_stats_x6", "trsm_stats_x6f16", "trsm_stats_f16"):
         if name in out:
             out[name]["tflops"] = M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12

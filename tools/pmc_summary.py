@@ -42,6 +42,8 @@ def kernel_key(name):
         return "gram_f16_kernel"
     if base == "grad_a_s_kernel" and flags[:1] == ["true"]:
         return "grad_a_s_f16_kernel"
+    if base == "expert_cond_x6_kernel" and flags[1:] == ["true", "true"]:
+        return "expert_cond_f16x8_kernel"       # split-f16 hi products + e4m3 cross terms
     if base in ("expert_cond_x6_kernel", "rbf_kuf_x6_kernel") and "true" in flags:
         return base.replace("_x6_", "_f16_")
     return base
