@@ -210,7 +210,9 @@ def k5_modes_leg(elbo_step, args, fmt, steps=10):
         out["f16x3" if cross == "f8" else "f16x8"] = {
             "value": 1.0 / dt, "unit": "ELBO steps/s", "ms_per_step": dt * 1e3,
             "k5_f16_product_equivalents": 3 if cross == "f8" else 2,
-            "accuracy": "f32 class (tests/test_gpu_f16.py)"}
+            "accuracy": ("f32 class (tests/test_gpu_f16.py)" if cross == "f8" else
+                         "fvar 6.4e-6 normwise vs float64 at c3 shapes (f32 class: 7e-7; "
+                         "tests/test_gpu_f16.py, gate 1e-4)")}
         set_expert_cross(cross)
     other = "x6" if fmt == "f16" else "f16"
     set_expert_format(other)

@@ -209,6 +209,13 @@ int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_
                        int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
                        void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A, int64_t lda,
                        mgp_stream_t stream);
+/* mgp_trsm_stats_f16 that also writes plane 2 of A's image (e4m3 cross terms,
+ * the operand of mgp_expert_conditional_f16x8).  With A == NULL plane 1 (f16 lo)
+ * is not written: the image then feeds mgp_expert_conditional_f16x8 only. */
+int mgp_trsm_stats_f16x8(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
+                         int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
+                         void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A, int64_t lda,
+                         mgp_stream_t stream);
 int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
                         void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
 int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr, size_t afr_bytes,
@@ -220,8 +227,9 @@ int mgp_expert_conditional_f16(const void* Afr, size_t afr_bytes, const void* Lf
                                const float* stats, int64_t lds, const float* variance, int64_t M,
                                int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
                                void* workspace, size_t workspace_bytes, mgp_stream_t stream);
-/* K5 "f16x8": the same split-f16 images (every split-f16 producer also writes
- * plane 2 = e4m3(hi 2^-6) | e4m3(lo 2^6) of each fragment); the hi products on
+/* K5 "f16x8": split-f16 images that also carry plane 2 = e4m3(hi 2^-6) |
+ * e4m3(lo 2^6) of each fragment (mgp_split_lower_f16, mgp_split_cols_f16 and
+ * mgp_trsm_stats_f16x8 write it); the hi products on
  * the f16 MFMA, both cross terms of two k-steps on one e4m3 MFMA
  * (v_mfma_scale_f32_32x32x64_f8f6f4, unit scales): 4 f16-product-equivalents
  * per k-step pair instead of 6.  Cross terms are <= 2^-11 of the leading one,

@@ -118,8 +118,11 @@ __device__ __forceinline__ int img_exp(float bound) {
 // "f16x8" mode, mfma_f8x): dwords 0-1 = e4m3(hi 2^-6), dwords 2-3 = e4m3(lo 2^6).
 // With the image maximum in [2^13, 2^14) both land in e4m3's range (<= 2^8):
 // hi 2^-6 keeps 3 mantissa bits down to 2^-14 of the maximum, lo 2^6 likewise.
+// write_lo = false (X8 only): plane 1 (f16 lo) is left unwritten -- the image then
+// feeds only the f16x8 K5, which reads planes 0 and 2.
 template <bool X8 = false>
-__device__ __forceinline__ void store_split_f16(bf16x8* __restrict__ dst, const float (&v)[8], float scale) {
+__device__ __forceinline__ void store_split_f16(bf16x8* __restrict__ dst, const float (&v)[8], float scale,
+                                                bool write_lo = true) {
   halfx8 h, l;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -129,7 +132,7 @@ __device__ __forceinline__ void store_split_f16(bf16x8* __restrict__ dst, const 
     l[j] = (_Float16)(x - (float)hi);  // exact difference in f32
   }
   dst[0] = __builtin_bit_cast(bf16x8, h);
-  dst[64] = __builtin_bit_cast(bf16x8, l);
+  if (!X8 || write_lo) dst[64] = __builtin_bit_cast(bf16x8, l);
   if constexpr (X8) {
     u32x4v x8;
 #pragma unroll

@@ -587,7 +587,10 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restri
 // F16IN: Tfr and Kfr are split-f16 images (scales 2^img_exp(*t_bound),
 // 2^img_exp(*k_bound)): three f16 products per block instead of six bf16 ones;
 // the accumulators are unscaled (exact power of two) before the epilogue.
-template <int KMAX, bool F16OUT = false, bool F16IN = false>
+// X8OUT (with F16OUT): the A image also gets its e4m3 cross-term plane (K5 f16x8);
+// its f16 lo plane only when the f32 A is written too (training: the backward
+// reads planes 0-1), so a forward-only image moves 4 B per element, not 6.
+template <int KMAX, bool F16OUT = false, bool F16IN = false, bool X8OUT = false>
 __device__ __forceinline__ void trsm_stats_x6_item(
     bf16x8 (*sL)[4 * 3 * 64], float* __restrict__ sQ, int t, int tn, const bf16x8* __restrict__ Tfr,
     uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
@@ -638,7 +641,7 @@ __device__ __forceinline__ void trsm_stats_x6_item(
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j];
         if constexpr (F16OUT)
-          store_split_f16<true>(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v, a_scale);
+          store_split_f16<X8OUT>(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v, a_scale, Af32 != nullptr);
         else
           store_split(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v);
       }
@@ -691,7 +694,7 @@ __device__ __forceinline__ void trsm_stats_x6_item(
 // workgroup has the same work; both items read the same Kuf column slab.  Odd
 // nT: the middle row tile is an item alone.  (c3: 385 us vs 439 us for one item
 // per workgroup, whose register count stays below 256 without spills.)
-template <int KMAX, bool F16OUT = false, bool F16IN = false>
+template <int KMAX, bool F16OUT = false, bool F16IN = false, bool X8OUT = false>
 __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
     const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
     int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
@@ -705,11 +708,11 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
   if constexpr (F16OUT)
     if (blockIdx.x == 0 && threadIdx.x == 0) *a_bound = sqrtf(*a_var);
   col_major_item(blockIdx.x, nP, nTn, p, tn);
-  trsm_stats_x6_item<KMAX, F16OUT, F16IN>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu,
+  trsm_stats_x6_item<KMAX, F16OUT, F16IN, X8OUT>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu,
                                           ldq, K, Afr, stats, lds_, Af32, lda, a_var, t_bound, k_bound);
   if (nT - 1 - p == p) return;
   __syncthreads();  // the epilogue's sQ reads before the next item's sQ stores
-  trsm_stats_x6_item<KMAX, F16OUT, F16IN>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K,
+  trsm_stats_x6_item<KMAX, F16OUT, F16IN, X8OUT>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K,
                                           Afr, stats, lds_, Af32, lda, a_var, t_bound, k_bound);
 }
 
@@ -873,7 +876,7 @@ template <int KMAX>
 static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb, int64_t M, int64_t N,
                           const float* q_mu, int64_t ldq, int K, void* Afr, float* stats, int64_t lds,
                           float* A, int64_t lda, hipStream_t s, const float* a_var = nullptr,
-                          bool f16in = false) {
+                          bool f16in = false, bool x8 = false) {
   const int64_t Mp = x6_mp(M);
   const int nmk = (int)(Mp / 16), nT = (int)(Mp / kX6BM), nTn = (int)(x6_np(N) / kX6BN);
   const dim3 grid((unsigned)((nT + 1) / 2 * nTn));
@@ -881,9 +884,14 @@ static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb
   if (f16in) {
     const float* t_bound = trailer(const_cast<void*>(Tfr), lower_planes(M, 1));
     const float* k_bound = trailer(const_cast<void*>(Kfr), cols_planes(M, N));
-    hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
-                       (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
-                       (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
+    if (x8)
+      hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
+                         (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
+                         (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
+    else
+      hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
+                         (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
+                         (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
   } else if (a_var)
     hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                        (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
@@ -928,7 +936,7 @@ extern "C" int mgp_trsm_stats_x6(const void* Tfr, size_t tfr_bytes, const void* 
 static int trsm_stats_f16_out(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
                               int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance, void* Afr,
                               size_t afr_bytes, float* stats, int64_t lds, mgp_stream_t stream, bool f16in,
-                              float* A = nullptr, int64_t lda = 0) {
+                              float* A = nullptr, int64_t lda = 0, bool x8 = false) {
   if (!Tfr) return -1;
   if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return -2;
   if (!Kfr) return -3;
@@ -950,9 +958,11 @@ static int trsm_stats_f16_out(const void* Tfr, size_t tfr_bytes, const void* Kfr
   if (M == 0 || N == 0) return MGP_OK;
   hipStream_t s = (hipStream_t)stream;
   const size_t tb = mgp_x6_lower_bytes(M, 1), kb = mgp_x6_cols_bytes(M, N);
-  if (K <= 4) return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in);
-  if (K <= 8) return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in);
-  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in);
+  if (K <= 4)
+    return launch_trsm_x6<4>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in, x8);
+  if (K <= 8)
+    return launch_trsm_x6<8>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in, x8);
+  return launch_trsm_x6<16>(Tfr, tb, Kfr, kb, M, N, q_mu, ldq, K, Afr, stats, lds, A, lda, s, variance, f16in, x8);
 }
 
 // x6 images in (Tfr, Kfr), split-f16 A image out (K5's operand).
@@ -973,6 +983,18 @@ extern "C" int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void*
   if (A && lda < N) return -16;
   return trsm_stats_f16_out(Tfr, tfr_bytes, Kfr, kfr_bytes, M, N, q_mu, ldq, K, variance, Afr, afr_bytes, stats, lds,
                             stream, true, A, lda);
+}
+
+// mgp_trsm_stats_f16 that also writes the A image's e4m3 cross-term plane (the
+// operand of mgp_expert_conditional_f16x8).  With A == NULL the f16 lo plane is
+// not written (only the f16x8 K5 reads that image).
+extern "C" int mgp_trsm_stats_f16x8(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
+                                    int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
+                                    void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A, int64_t lda,
+                                    mgp_stream_t stream) {
+  if (A && lda < N) return -16;
+  return trsm_stats_f16_out(Tfr, tfr_bytes, Kfr, kfr_bytes, M, N, q_mu, ldq, K, variance, Afr, afr_bytes, stats, lds,
+                            stream, true, A, lda, true);
 }
 
 // absmax of the source into the trailer, then the scaled split.
@@ -1061,8 +1083,8 @@ extern "C" int mgp_expert_conditional_f16(const void* Afr, size_t afr_bytes, con
                             workspace, workspace_bytes, stream, true);
 }
 
-// Same images as mgp_expert_conditional_f16 (every split-f16 producer writes the
-// X8 plane): hi products on f16, cross terms on e4m3 (mfma_f8x).
+// Split-f16 images with the X8 plane (mgp_split_lower_f16, mgp_split_cols_f16,
+// mgp_trsm_stats_f16x8): hi products on f16, cross terms on e4m3 (mfma_f8x).
 extern "C" int mgp_expert_conditional_f16x8(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
                                             const float* stats, int64_t lds, const float* variance, int64_t M,
                                             int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,

@@ -212,13 +212,16 @@ def split_upper_x6(LinvT, out=None, fmt="x6"):
     return out
 
 
-def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_variance=None, in_fmt="x6"):
+def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_variance=None, in_fmt="x6", cross=None):
     """K4 on images: A's image (for expert_conditional_x6) and the stats [T, K+1, N];
     also the f32 A when a buffer `A` [M, N] is given (training).  f16_variance
     (the layer's kernel variance): A's image is split-f16 instead
     (mgp_trsm_stats_x6_f16, for expert_conditional_x6(..., fmt="f16")).
     in_fmt "f16": Tfr and Kfr are split-f16 images (split_upper_x6 / rbf_kuf_x6 with
-    fmt "f16"; mgp_trsm_stats_f16, needs f16_variance)."""
+    fmt "f16"; mgp_trsm_stats_f16, needs f16_variance).
+    cross "f8" (default: config.expert_cross()) with split-f16 inputs: A's image also
+    carries the e4m3 cross-term plane of expert_conditional_x6(..., cross="f8")
+    (mgp_trsm_stats_f16x8)."""
     _check(q_mu, "q_mu", 2)
     K = q_mu.shape[1]
     dev = q_mu.device
@@ -236,7 +239,9 @@ def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_varian
                       q_mu.data_ptr(), _ld(q_mu), K, f16_variance.data_ptr(), Afr.data_ptr(), Afr.numel(),
                       stats.data_ptr(), _ld(stats), _stream())
         else:
-            _lib.call("mgp_trsm_stats_f16", Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
+            from .config import expert_cross
+            entry = "mgp_trsm_stats_f16x8" if (cross or expert_cross()) == "f8" else "mgp_trsm_stats_f16"
+            _lib.call(entry, Tfr.data_ptr(), Tfr.numel(), Kfr.data_ptr(), Kfr.numel(), M, N,
                       q_mu.data_ptr(), _ld(q_mu), K, f16_variance.data_ptr(), Afr.data_ptr(), Afr.numel(),
                       stats.data_ptr(), _ld(stats), A.data_ptr() if A is not None else None,
                       _ld(A) if A is not None else N, _stream())

@@ -96,6 +96,7 @@ def test_expert_conditional_f16_accuracy(device):
     Afr, stats = ops.trsm_stats_x6(Thr, Khr, qm, M, N, f16_variance=var, in_fmt="f16")
     fm, fv = ops.expert_conditional_x6(Afr, ops.split_lower_x6(qs, fmt="f16"), stats, var, M, N, K, fmt="f16")
     errs["f16 chain"] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))
+    Afr, stats = ops.trsm_stats_x6(Thr, Khr, qm, M, N, f16_variance=var, in_fmt="f16", cross="f8")
     fm, fv = ops.expert_conditional_x6(Afr, ops.split_lower_x6(qs, fmt="f16"), stats, var, M, N, K, fmt="f16",
                                        cross="f8")
     errs["f16x8 chain"] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))

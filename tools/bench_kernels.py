@@ -80,7 +80,7 @@ def main():
     cb = ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N)
     wsc = torch.empty(ops.conditional_backward_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev)
     A32h = ops.padded(M, N, dev)   # the f16 chain's training K4: f16 A image + f32 A
-    ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, A=A32h, f16_variance=var, in_fmt="f16")
+    ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, A=A32h, f16_variance=var, in_fmt="f16", cross="f8")
     cbh = ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N, fmt="f16")
     torch.cuda.synchronize()
     runs = {
@@ -101,7 +101,9 @@ def main():
         "rbf_kuf_f16": lambda: ops.rbf_kuf_x6(X, Z, var, lsc, out=Khr, fmt="f16"),
         "split_upper_f16": lambda: ops.split_upper_x6(LinvT[0], out=Thr, fmt="f16"),
         "trsm_stats_f16": lambda: ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var,
-                                                    in_fmt="f16"),
+                                                    in_fmt="f16", cross="f16"),
+        "trsm_stats_f16x8": lambda: ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, f16_variance=var,
+                                                      in_fmt="f16", cross="f8"),
         "trsm_f16_nostats": lambda: ops._lib.call("mgp_trsm_stats_f16", Thr.data_ptr(), Thr.numel(), Khr.data_ptr(),
                                                   Khr.numel(), M, N, q_mu.data_ptr(), K, K, var.data_ptr(),
                                                   Ahr.data_ptr(), Ahr.numel(), None, N, None, N, ops._stream()),
@@ -134,7 +136,7 @@ def main():
     for name in ("expert_cond_f16", "expert_cond_f16x8"):
         if name in out:
             out[name]["tflops"] = K * M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
-    for name in ("trsm_stats_x6", "trsm_stats_x6f16", "trsm_stats_f16"):
+    for name in ("trsm_stats_x6", "trsm_stats_x6f16", "trsm_stats_f16", "trsm_stats_f16x8"):
         if name in out:
             out[name]["tflops"] = M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
     for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N),

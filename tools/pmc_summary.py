@@ -34,7 +34,9 @@ def kernel_key(name):
     base = name.split("::")[-1].split("<")[0]
     args = name.split("<", 1)[1] if "<" in name else ""
     flags = [a.strip() for a in args.split(">")[0].split(",")]
-    if base == "trsm_stats_x6_kernel" and flags[1:] == ["true", "true"]:
+    if base == "trsm_stats_x6_kernel" and flags[1:] == ["true", "true", "true"]:
+        return "trsm_stats_f16x8_kernel"        # split-f16 in and out, + the A image's e4m3 plane
+    if base == "trsm_stats_x6_kernel" and flags[1:3] == ["true", "true"]:
         return "trsm_stats_f16_kernel"          # split-f16 images in and out
     if base == "trsm_stats_x6_kernel" and flags[1:2] == ["true"]:
         return "trsm_stats_x6f16_kernel"        # split-bf16 in, split-f16 A image out
