@@ -304,6 +304,16 @@ int mgp_conditional_backward_f16(const void* Afr, size_t afr_bytes, const float*
                                  int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm,
                                  int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
                                  mgp_stream_t stream);
+/* Same, with Afr from mgp_trsm_stats_f16x8 (A non-NULL: all three planes): S_k A on
+ * f16 hi products + e4m3 cross terms (the f16x8 training step). */
+int mgp_conditional_backward_f16x8(const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+                                 const float* q_sqrt, int64_t ldqs,
+                                 int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+                                 int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M,
+                                 int64_t N, int32_t K, float* g_q_mu, int64_t ldgq, float* g_q_sqrt,
+                                 int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm,
+                                 int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
+                                 mgp_stream_t stream);
 
 /* Reverse mode of Lm = chol(Kuu) (models.py:141): gKuu = sym(Lm^-T Phi(Lm^T gL) Lm^-1),
  * Phi = lower triangle with halved diagonal, in float64 from the float32 L,

@@ -495,7 +495,9 @@ __global__ __launch_bounds__(256) void grad_a_base_kernel(const float* __restric
 // no per-expert intermediate is written.
 // F16: Sfr and Afr are split-f16 images (scales 2^img_exp(*s_bound), 2^img_exp(*a_bound)):
 // three f16 products per block; the unscale folds into the column weights.
-template <bool F16 = false>
+// X8 (with F16): the S_k A products on f16 hi products + e4m3 cross terms
+// (mfma_f8x; both images carry the e4m3 plane in the f16x8 training step).
+template <bool F16 = false, bool X8 = false>
 __global__ __launch_bounds__(256, 2) void grad_a_s_kernel(const bf16x8* __restrict__ Sfr, uint32_t s_bytes,
                                                           const bf16x8* __restrict__ Afr, uint32_t afr_bytes,
                                                           int nmk, int nTn, int K, int64_t M, int64_t N,
@@ -521,7 +523,7 @@ __global__ __launch_bounds__(256, 2) void grad_a_s_kernel(const bf16x8* __restri
   float unscale = 1.f;
   if constexpr (F16) unscale = ldexpf(1.f, -(img_exp(*s_bound) + img_exp(*a_bound)));
   for (int k = 0; k < K; ++k) {
-    x6_mainloop<0, 1, F16 ? 2 : 3, F16>(acc, sL, img_rsrc(Sfr + k * s_elems, s_bytes),
+    x6_mainloop<0, 1, F16 ? 2 : 3, F16, X8>(acc, sL, img_rsrc(Sfr + k * s_elems, s_bytes),
                                         (uint32_t)(4 * t * nmk) * 3u * kFragBytes, img_rsrc(Afr, afr_bytes),
                                         (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, nmk, nmk);
     const float g = n < N ? Gv[(int64_t)k * ldg + n] * unscale : 0.f;
@@ -1197,7 +1199,7 @@ static int conditional_backward(
     int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
     float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
     float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream,
-    bool f16) {
+    bool f16, bool x8 = false) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!A) return -3;
@@ -1280,7 +1282,12 @@ static int conditional_backward(
     if ((st = launch_status())) return st;
   }
   // 3. gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0
-  if (f16)
+  if (f16 && x8)
+    hipLaunchKernelGGL((grad_a_s_kernel<true, true>), dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s,
+                       (const bf16x8*)Sfr, (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes,
+                       nmk, 2 * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, (const float*)trailer(Sfr, lower_planes(M, K)),
+                       (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)));
+  else if (f16)
     hipLaunchKernelGGL(grad_a_s_kernel<true>, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
                        (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes, nmk, 2 * nTn, K,
                        M, N, Gv, ldg, gA0, ldn, gAfr, (const float*)trailer(Sfr, lower_planes(M, K)),
@@ -1352,4 +1359,17 @@ extern "C" int mgp_conditional_backward_f16(
   return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
                               N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
                               workspace_bytes, stream, true);
+}
+
+// Afr from mgp_trsm_stats_f16x8 with the f32 A (all three planes): S_k A on f16 hi
+// products + e4m3 cross terms (grad_a_s_kernel<true, true>).
+extern "C" int mgp_conditional_backward_f16x8(
+    const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+    const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+    int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
+    float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
+    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
+                              N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
+                              workspace_bytes, stream, true, true);
 }

@@ -516,10 +516,13 @@ def conditional_backward_workspace_bytes(M, N, K):
     return int(_lib.load().mgp_conditional_backward_workspace_bytes(M, N, K))
 
 
-def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None, fmt="x6"):
+def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None, fmt="x6",
+                            cross=None):
     """Backward of one layer's conditional (see include/mgp_hip.h): returns dict of
     g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1]).
-    fmt: format of A's image Afr ("f16": mgp_conditional_backward_f16)."""
+    fmt: format of A's image Afr ("f16": mgp_conditional_backward_f16; with cross "f8",
+    default config.expert_cross(), mgp_conditional_backward_f16x8 -- Afr then comes
+    from trsm_stats_x6(..., A=..., cross="f8"))."""
     K = q_mu.shape[1]
     dev = q_mu.device
     if out is None:
@@ -532,7 +535,11 @@ def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None
     if _ld(Gmu) != _ld(Gv):
         raise ValueError("Gmu and Gv must share a leading dimension")
     o = out
-    _lib.call("mgp_conditional_backward_" + _fmt(fmt), Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A),
+    from .config import expert_cross
+    entry = "mgp_conditional_backward_" + _fmt(fmt)
+    if entry.endswith("f16") and (cross or expert_cross()) == "f8":
+        entry += "x8"
+    _lib.call(entry, Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A),
               q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), q_mu.data_ptr(), _ld(q_mu),
               LinvT.data_ptr(), _ld(LinvT), Gmu.data_ptr(), Gv.data_ptr(), _ld(Gmu), M, N, K,
               o["g_q_mu"].data_ptr(), _ld(o["g_q_mu"]), o["g_q_sqrt"].data_ptr(), _ld(o["g_q_sqrt"]),

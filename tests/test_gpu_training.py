@@ -71,16 +71,19 @@ def _dense(name, t, M):
                                                     (1000, 25, 3, 1, 0.5, 25, True),
                                                     (4096, 130, 3, 3, 1.0, 5, False),
                                                     (2048, 2048, 16, 16, 2.0, 3, False)])   # config-5 shapes
-@pytest.mark.parametrize("fmt", ["f16", "x6"])
+@pytest.mark.parametrize("fmt", ["f16", "x6", "f16x8"])
 def test_elbo_and_grad(device, N, M, K, D, ls, S, modified, fmt):
-    """Both image formats of the chain (split-f16, the default, and split-bf16 x6)."""
+    """Both image formats of the chain (split-f16, the default, and split-bf16 x6),
+    and split-f16 with the e4m3 cross terms in K5 and in the S_k A backward (f16x8)."""
     from modulatedgps_amd import config
-    old = config.expert_format()
-    config.set_expert_format(fmt)
+    old, old_cross = config.expert_format(), config.expert_cross()
+    config.set_expert_format("x6" if fmt == "x6" else "f16")
+    config.set_expert_cross("f8" if fmt == "f16x8" else "f16")
     try:
         _check_elbo_and_grad(device, N, M, K, D, ls, S, modified)
     finally:
         config.set_expert_format(old)
+        config.set_expert_cross(old_cross)
 
 
 def _check_elbo_and_grad(device, N, M, K, D, ls, S, modified):

@@ -118,7 +118,9 @@ def main():
         "cond_bwd_x6": lambda: ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
                                                            out=cb, workspace=wsc),
         "cond_bwd_f16": lambda: ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
-                                                            out=cbh, workspace=wsc, fmt="f16"),
+                                                            out=cbh, workspace=wsc, fmt="f16", cross="f16"),
+        "cond_bwd_f16x8": lambda: ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
+                                                              out=cbh, workspace=wsc, fmt="f16", cross="f8"),
     }
     if a.only:
         runs = {k: v for k, v in runs.items() if k in a.only.split(",")}
