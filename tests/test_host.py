@@ -54,3 +54,19 @@ def test_toy_datasets_match_reference_generators():
             ref = d[f"{name}_{key}"]
             assert np.array_equal(np.asarray(got), ref), (name, key)
             assert np.asarray(got).dtype == ref.dtype, (name, key)
+
+
+def test_config_expert_cross_knob():
+    """K5 cross-term precision knob (config.expert_cross): 'f16' (default, f16x3) or
+    'f8' (f16x8, e4m3 cross terms); anything else is refused."""
+    import pytest
+    from modulatedgps_amd import config
+    old = config.expert_cross()
+    try:
+        for v in ("f8", "f16"):
+            config.set_expert_cross(v)
+            assert config.expert_cross() == v
+        with pytest.raises(ValueError):
+            config.set_expert_cross("bf16")
+    finally:
+        config.set_expert_cross(old)
