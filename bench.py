@@ -10,10 +10,15 @@ MixtureGPs/models.py:69-79: both SVGP layers, S = 25 Monte-Carlo samples,
 both KLs) over one batch of synthetic input already resident in HBM, with
 fresh in-kernel Philox noise per step.  Workload (N = 1): BASELINE config 3,
 N = 65536, M = 1024, K = 8, D = 8, fp32, per GPU.  Multi-GPU: data-parallel
-over N with weak scaling (every rank holds its own 65536-point shard of the
-global batch; Kuu/Cholesky/KL replicated; ONE RCCL all-reduce of the data-term
-scalar per step).  `value` = ELBO steps/s in units of config-3 evaluations,
-i.e. world_size * steps / max-over-ranks wall time.
+over N, one process per GPU (`--gpus N` without torchrun starts the N ranks
+itself).  `--scaling weak` (default): every rank holds its own 65536-point
+shard of the global batch; `--scaling strong`: BASELINE config c4, c3's
+N = 65536 split over the ranks.  Kuu/Cholesky/KL are replicated; ONE RCCL
+all-reduce of the data-term scalar per step.  `--layout expert`: the
+north_star layout (experts sharded, one all_to_all).  Timing: W warmup steps,
+then the K timed steps as `--repeats` blocks (default 5 x 50), each bracketed by
+barrier + synchronize, max over ranks; `value` = the median block rate in
+units of whole-config evaluations (weak: world_size evaluations per step).
 
 Rank 0 prints ONE JSON line (see README/DESIGN for the fields).
 """
@@ -45,8 +50,15 @@ PEAK_HBM = 8.0e12             # HBM3E spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=250,
+                    help="timed steps in total, run as --repeats contiguous blocks (default 5 x 50)")
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="the timed steps are split into this many blocks, each bracketed by barrier + "
+                         "synchronize; value = the median block rate (SURVEY §8d: median of 5 repeats)")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="multi-GPU data layout: 'weak' = N points per GPU (the default); 'strong' = BASELINE "
+                         "config c4, the config's N sharded over the ranks (N / world per GPU)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--planes", type=int, default=3, choices=(1, 2, 3),
                     help="bf16 planes per operand in K5 (3: f32-accurate x6, the default; 2 / 1: the "
@@ -67,6 +79,59 @@ def parse():
                     help="two N sizes of the CPU oracle sample (linear fit in N; the full N "
                          "is timed directly when it is one of them)")
     return ap.parse_args()
+
+
+def timed_blocks(step, steps, repeats, barrier, world, device, timing=None):
+    """Run `steps` timed steps as `repeats` contiguous blocks, each bracketed by a
+    barrier + torch.cuda.synchronize() on both sides; every block's wall time is the
+    max over ranks.  Returns (per-block (steps, seconds) list, last step's result)."""
+    repeats = max(1, min(repeats, steps))
+    sizes = [steps // repeats + (1 if r < steps % repeats else 0) for r in range(repeats)]
+    blocks, out = [], None
+    for n in sizes:
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            out = step(timing)
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        blocks.append((n, el))
+    return blocks, out
+
+
+def median_rate(blocks, world):
+    """Median over blocks of world * steps / seconds, and its ms per step."""
+    rates = sorted(world * n / el for n, el in blocks)
+    med = float(np.median(rates))
+    return med, world / med * 1e3, [round(r, 2) for r in rates]
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` without torchrun: start N ranks as child processes
+    (torch.distributed.run, 127.0.0.1 rendezvous, one GPU per rank) before anything
+    touches the GPU, and exit with their status.  Fails if fewer than N devices are
+    visible (device_count() does not initialise the GPU on this image), unless the
+    MGP_BENCH_SHARE_GPU=1 rehearsal puts every rank on cuda:0."""
+    import socket
+    import subprocess
+    share = os.environ.get("MGP_BENCH_SHARE_GPU") == "1"
+    have = torch.cuda.device_count()
+    if not share and have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {have} device(s) visible", file=sys.stderr)
+        sys.exit(2)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 def synthetic(cfg, rank, device):
@@ -245,7 +310,7 @@ def k5_modes_leg(elbo_step, args, fmt, steps=10):
     return out
 
 
-def train_leg(model, X, Y, kw, args, barrier, world, device):
+def train_leg(model, X, Y, kw, args, barrier, world, device, units):
     """Secondary line: the run_adam optimisation step (utils/training_utils.py:10-13:
     ELBO, its gradient w.r.t. every trainable parameter, one TF-legacy Adam update),
     same workload and timing protocol as the forward leg."""
@@ -263,26 +328,20 @@ def train_leg(model, X, Y, kw, args, barrier, world, device):
     for _ in range(max(1, args.warmup)):
         step()
     timing = {}
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        e = step(timing)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    steps = max(args.repeats, min(args.steps, 50))   # ~1 s of training steps at c3
+    blocks, e = timed_blocks(step, steps, args.repeats, barrier, world, device, timing)
+    value, ms, rates = median_rate(blocks, units)
     st = stage_stats(timing)
-    return {"metric": "training steps/sec (forward + full gradient + Adam)", "value": world * args.steps / elapsed,
-            "unit": "train steps/s", "ms_per_step": elapsed / args.steps * 1e3, "elbo_last": float(e.item()),
-            "stages_us_per_step": {k: round(v[0] * v[1] / args.steps * 1e3, 1) for k, v in st.items()}}
+    return {"metric": "training steps/sec (forward + full gradient + Adam)", "value": value,
+            "unit": "train steps/s", "ms_per_step": ms, "steps": steps, "block_rates": rates,
+            "elbo_last": float(e.item()),
+            "stages_us_per_step": {k: round(v[0] * v[1] / steps * 1e3, 1) for k, v in st.items()}}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(args)
     from modulatedgps_amd.config import (conditional_mode, expert_cross, expert_format, set_expert_cross,
                                          set_expert_format, set_expert_planes)
     x6 = conditional_mode() == "x6"
@@ -306,14 +365,22 @@ def main():
     group = torch.distributed.group.WORLD if world > 1 else None
     device = torch.device("cuda", local if world > 1 else 0)
     cfg = CONFIGS[args.config]
-    N, M, K, D, ls, S = cfg
     expert = args.layout == "expert" and world > 1
+    strong = args.scaling == "strong" and not expert and world > 1
+    if strong:  # c4: the config's N split over the ranks (balanced shards)
+        from modulatedgps_amd.distributed import shard_rows
+        lo, hi = shard_rows(cfg[0], rank, world)
+        cfg = (hi - lo,) + tuple(cfg[1:])
+    N, M, K, D, ls, S = cfg
     X_np, Y_np, layers = synthetic(cfg, 0 if expert else rank, device)
-    n_total = N if expert else N * world
+    if strong:
+        n_total, n_offset = CONFIGS[args.config][0], lo
+    else:
+        n_total, n_offset = (N if expert else N * world), rank * N
     model = build_model(cfg, layers, device, num_data=n_total)
     X = torch.from_numpy(X_np).to(device)
     Y = torch.from_numpy(Y_np).to(device)
-    kw = dict(n_offset=rank * N, n_total=n_total, process_group=group)
+    kw = dict(n_offset=n_offset, n_total=n_total, process_group=group)
     if expert:
         from modulatedgps_amd.distributed import expert_parallel_elbo
 
@@ -332,18 +399,7 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        elbo = elbo_step(timing)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    blocks, elbo = timed_blocks(elbo_step, args.steps, args.repeats, barrier, world, device, timing)
     elbo_val = float(elbo.item())
     info = model.last_info.cpu().tolist() if model.last_info is not None else None
     st = stage_stats(timing)
@@ -401,9 +457,11 @@ def main():
                               f"split-bf16: each f32 product is {k5_products} bf16 MFMA products, peak = "
                               f"2.5 PF bf16 dense / {k5_products}" if x6 else "f32 MFMA dense peak")}
 
-    ms_per_step = elapsed / args.steps * 1e3
-    value = (1 if expert else world) * args.steps / elapsed
-    train = None if (args.no_train or expert) else train_leg(model, X, Y, kw, args, barrier, world, device)
+    # ELBO steps/s in units of whole-config evaluations: weak = world evaluations of
+    # N points per step; strong / expert = one evaluation of the config's N per step
+    units = 1 if (expert or strong) else world
+    value, ms_per_step, block_rates = median_rate(blocks, units)
+    train = None if (args.no_train or expert) else train_leg(model, X, Y, kw, args, barrier, world, device, units)
     modes = None
     if world == 1 and x6 and args.planes == 3 and not args.no_modes:
         modes = k5_modes_leg(elbo_step, args, fmt)
@@ -416,8 +474,11 @@ def main():
             "metric": "ELBO steps/sec (N=65536, M=1024, K=8); Kuf HBM GB/s vs roofline",
             "value": value, "unit": "ELBO steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong" if expert else "weak", "vs_baseline": None,
-            "dtype": {3: "f32", 2: "f32/bf16x3 mixed", 1: "f32/bf16 mixed"}[args.planes] if x6 else "f32",
+            "scaling": "strong" if (expert or strong) else "weak", "vs_baseline": None,
+            "repeats": len(blocks), "steps_per_repeat": [n for n, _ in blocks], "block_rates": block_rates,
+            "dtype": (("f32 (split-f16 + e4m3 cross terms)" if f16x8 else "f32 (split-f16, 22-bit operands)")
+                      if f16 else {3: "f32 (split-bf16 x6, f32-exact operands)", 2: "f32/bf16x3 mixed",
+                                   1: "f32/bf16 mixed"}[args.planes]) if x6 else "f32",
             "data": "synthetic",
             "dtype_note": (("f32 operands and accumulation; K1/K4 products on bf16 MFMA via an exact 3-plane "
                             "split (6 products) in training; the forward chain K1 -> K4 -> K5 on f16 MFMA via "
@@ -430,8 +491,9 @@ def main():
                            (f"K1-K4 f32-accurate (x6 split-bf16), K5 on the leading {args.planes} bf16 plane(s) "
                             f"({k5_products} product(s), f32 accumulation); K3 in f64") if x6 else
                            "f32 MFMA (exact f32); K3 in f64"),
-            "config": {"workload": f"{args.config}: SMGP ELBO forward, N={N}/GPU, M={M}, K={K}, "
-                                   f"D={D}, S={S}, lengthscale={ls}",
+            "config": {"workload": (f"c4 ({args.config} N={n_total} sharded over {world} GPUs): " if strong else
+                                     f"{args.config}: ") + f"SMGP ELBO forward, N={N}/GPU, M={M}, K={K}, "
+                                    f"D={D}, S={S}, lengthscale={ls}",
                        "global_batch": n_total, "N_per_gpu": N, "M": M, "K": K, "D": D, "S": S,
                        "parallelism": (f"ep{world} (K experts sharded over ranks on N={N}, one RCCL all_to_all of "
                                        f"the conditionals + one scalar all-reduce)" if expert else

@@ -350,7 +350,8 @@ int mgp_gauss_kl_white(const float* q_mu, int64_t ldq, const float* q_sqrt, int6
 /* ---------------------------------------------------------------- K6
  * Monte-Carlo data term of the SMGP ELBO for the local data points:
  *   data_sum = sum_n [ logsumexp_s( sum_k W[s,n,k] ve[n,k] ) - log S ]
- *   logits = mu_a + z * sqrt(var_a + 1e-6)              (models.py:57-58, utils.py:26-27)
+ *   logits = mu_a + z * sqrt(var_a + jitter)            (models.py:57-58, utils.py:26-27;
+ *            jitter = gpflow.config.default_jitter(), 1e-6 unless set)
  *   W = softmax_k((-log(-log u) + logits) / tau)         (models.py:59-60,73-74; TFP 0.18)
  *   ve = -0.5 log 2pi - 0.5 log s2_k - 0.5((y - mu_f)^2 + var_f)/s2_k  (likelihoods.py:39-41)
  * Replaces SMGP.W_dist / E_log_p_Y / the batch sum of models.py:55-76.
@@ -361,7 +362,7 @@ int mgp_gauss_kl_white(const float* q_mu, int64_t ldq, const float* q_sqrt, int6
 size_t mgp_elbo_workspace_bytes(int64_t N);
 int mgp_elbo_terms(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
                    int64_t ldf, const float* Y, const float* lik_var, int64_t N, int32_t K,
-                   int32_t S, float tau, const float* noise_z, const float* noise_u,
+                   int32_t S, float tau, float jitter, const float* noise_z, const float* noise_u,
                    uint64_t seed, int64_t n_offset, double* data_sum, void* workspace,
                    size_t workspace_bytes, mgp_stream_t stream);
 
@@ -371,7 +372,7 @@ int mgp_elbo_terms(const float* mu_f, const float* var_f, const float* mu_a, con
  *   data_sum = sum_n [lse_s(sum_k W ve_a) - log S + lse_s(sum_k W ve_f) - log S]. */
 int mgp_elbo_terms_modified(const float* mu_f, const float* var_f, const float* mu_a,
                             const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
-                            const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                            const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau, float jitter,
                             const float* noise_z, const float* noise_u, uint64_t seed,
                             int64_t n_offset, double* data_sum, void* workspace,
                             size_t workspace_bytes, mgp_stream_t stream);
@@ -388,7 +389,7 @@ int mgp_elbo_terms_modified(const float* mu_f, const float* var_f, const float* 
 size_t mgp_elbo_backward_workspace_bytes(int64_t N, int32_t K);
 int mgp_elbo_terms_backward(const float* mu_f, const float* var_f, const float* mu_a,
                             const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
-                            const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                            const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau, float jitter,
                             const float* noise_z, const float* noise_u, uint64_t seed,
                             int64_t n_offset, float scale, float* G, int64_t ldg, double* g_lik_var,
                             double* g_assign_lik_var, void* workspace, size_t workspace_bytes,
@@ -411,12 +412,13 @@ int mgp_predict_epilogue(const float* fmean, const float* fvar, const float* ame
 
 /* SMGP.predict_samples (models.py:91-103): a fresh assignment sample W (as in
  * mgp_elbo_terms) and one normal draw z shared by the y- and f-samples:
- *   samples_y[s][n] = sum_k W (mu_f + z sqrt(var_f + lik_var_k + 1e-6))
- *   samples_f[s][n] = sum_k W (mu_f + z sqrt(var_f + 1e-6))
+ *   samples_y[s][n] = sum_k W (mu_f + z sqrt(var_f + lik_var_k + jitter))
+ *   samples_f[s][n] = sum_k W (mu_f + z sqrt(var_f + jitter))
+ * (jitter: default_jitter(), the reparameterize of utils.py:26-27)
  * Explicit noise (all three [S][N][K], parity mode) or Philox (streams 0/1 for
  * W, stream 2 for z).  Outputs [S][N]; either may be NULL. */
 int mgp_predict_samples(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
-                        int64_t ldf, const float* lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                        int64_t ldf, const float* lik_var, int64_t N, int32_t K, int32_t S, float tau, float jitter,
                         const float* noise_zw, const float* noise_uw, const float* noise_zy,
                         uint64_t seed, int64_t n_offset, float* samples_y, float* samples_f,
                         mgp_stream_t stream);
@@ -440,12 +442,12 @@ int mgp_philox_noise(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int3
  * parameter; RobustMax.epsilon is trainable=False). */
 int mgp_elbo_terms_multiclass(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
                               int64_t ldf, const float* Y, float epsilon, const float* assign_lik_var,
-                              int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
+                              int64_t N, int32_t K, int32_t S, float tau, float jitter, const float* noise_z,
                               const float* noise_u, uint64_t seed, int64_t n_offset, double* data_sum,
                               void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 int mgp_elbo_terms_multiclass_backward(const float* mu_f, const float* var_f, const float* mu_a,
                                        const float* var_a, int64_t ldf, const float* Y, float epsilon,
-                                       const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
+                                       const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau, float jitter,
                                        const float* noise_z, const float* noise_u, uint64_t seed,
                                        int64_t n_offset, float scale, float* G, int64_t ldg,
                                        double* g_assign_lik_var, void* workspace, size_t workspace_bytes,
@@ -457,7 +459,7 @@ int mgp_multiclass_predict(const float* fmean, const float* fvar, int64_t ldf, i
 /* SMGP.predict_samples with the MultiClass predictive mean / variance for samples_y. */
 int mgp_predict_samples_multiclass(const float* mu_f, const float* var_f, const float* mu_a,
                                    const float* var_a, int64_t ldf, float epsilon, int64_t N, int32_t K,
-                                   int32_t S, float tau, const float* noise_zw, const float* noise_uw,
+                                   int32_t S, float tau, float jitter, const float* noise_zw, const float* noise_uw,
                                    const float* noise_zy, uint64_t seed, int64_t n_offset, float* samples_y,
                                    float* samples_f, mgp_stream_t stream);
 

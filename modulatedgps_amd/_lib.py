@@ -126,39 +126,31 @@ SIGNATURES = {
     "mgp_gauss_kl_white": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr,
                                           c_ptr, c_size, c_ptr]),
     "mgp_elbo_workspace_bytes": (c_size, [c_i64]),
-    "mgp_elbo_terms": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32,
-                                      c_i32, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64, c_ptr, c_ptr,
-                                      c_size, c_ptr]),
-    "mgp_elbo_terms_modified": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64,
-                                               c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64,
-                                               c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_elbo_terms": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_i32, ctypes.c_float,
+                                 ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_elbo_terms_modified": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i32, c_i32,
+                                          ctypes.c_float, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
     "mgp_elbo_backward_workspace_bytes": (c_size, [c_i64, c_i32]),
-    "mgp_elbo_terms_backward": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64,
-                                               c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64,
-                                               ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size,
-                                               c_ptr]),
+    "mgp_elbo_terms_backward": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i32, c_i32,
+                                          ctypes.c_float, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64, ctypes.c_float, c_ptr, c_i64,
+                                          c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
     "mgp_elbo_combine": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, ctypes.c_double, ctypes.c_double, c_ptr,
                                         c_ptr, c_ptr]),
     "mgp_predict_epilogue": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr,
                                             c_ptr, c_ptr, c_ptr]),
     "mgp_philox_noise": (ctypes.c_int, [c_u64, c_i64, c_i64, c_i32, c_i32, c_ptr, c_ptr, c_ptr]),
     "mgp_philox_normal2": (ctypes.c_int, [c_u64, c_i64, c_i64, c_i32, c_i32, c_ptr, c_ptr]),
-    "mgp_predict_samples": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i32,
-                                           c_i32, ctypes.c_float, c_ptr, c_ptr, c_ptr, c_u64, c_i64,
-                                           c_ptr, c_ptr, c_ptr]),
-    "mgp_elbo_terms_multiclass": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, ctypes.c_float,
-                                                 c_ptr, c_i64, c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_u64,
-                                                 c_i64, c_ptr, c_ptr, c_size, c_ptr]),
-    "mgp_elbo_terms_multiclass_backward": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr,
-                                                          ctypes.c_float, c_ptr, c_i64, c_i32, c_i32,
-                                                          ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64,
-                                                          ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size,
-                                                          c_ptr]),
+    "mgp_predict_samples": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_i32, ctypes.c_float,
+                                      ctypes.c_float, c_ptr, c_ptr, c_ptr, c_u64, c_i64, c_ptr, c_ptr, c_ptr]),
+    "mgp_elbo_terms_multiclass": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, ctypes.c_float, c_ptr, c_i64, c_i32, c_i32,
+                                            ctypes.c_float, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_elbo_terms_multiclass_backward": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, ctypes.c_float, c_ptr, c_i64, c_i32, c_i32,
+                                                     ctypes.c_float, ctypes.c_float, c_ptr, c_ptr, c_u64, c_i64, ctypes.c_float, c_ptr, c_i64,
+                                                     c_ptr, c_ptr, c_size, c_ptr]),
     "mgp_multiclass_predict": (ctypes.c_int, [c_ptr, c_ptr, c_i64, c_i64, c_i32, ctypes.c_float, c_ptr, c_ptr,
                                               c_ptr]),
-    "mgp_predict_samples_multiclass": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, ctypes.c_float, c_i64,
-                                                      c_i32, c_i32, ctypes.c_float, c_ptr, c_ptr, c_ptr, c_u64,
-                                                      c_i64, c_ptr, c_ptr, c_ptr]),
+    "mgp_predict_samples_multiclass": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, ctypes.c_float, c_i64, c_i32, c_i32, ctypes.c_float,
+                                                 ctypes.c_float, c_ptr, c_ptr, c_ptr, c_u64, c_i64, c_ptr, c_ptr, c_ptr]),
 }
 
 _lib = None

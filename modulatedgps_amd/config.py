@@ -20,10 +20,8 @@ import torch
 #              at c3 shapes -- the f32 inputs' own rounding); f16 is half the MFMA
 #              work.  The training step follows it (A's image, S_k A in the
 #              backward); the reduced-plane modes use "x6".
-_CFG = {"jitter": 1e-6, "device": None, "conditional": os.environ.get("MGP_CONDITIONAL", "x6"),
-        "expert_planes": int(os.environ.get("MGP_K5_PLANES", "3")),
-        "expert_format": os.environ.get("MGP_K5_FORMAT", "f16"),
-        "expert_cross": os.environ.get("MGP_K5_CROSS", "f16")}
+_CFG = {"jitter": 1e-6, "device": None, "conditional": "x6", "expert_planes": 3, "expert_format": "f16",
+        "expert_cross": "f16"}
 # expert_cross (f16 images): the precision of K5's two cross-term products
 #              a_hi b_lo + a_lo b_hi -- "f16" (three f16 products) or "f8" (one
 #              e4m3 MFMA per two k-steps for both, mgp_expert_conditional_f16x8:
@@ -101,3 +99,23 @@ def forward_image_format(train=False):
     if expert_planes() != 3:
         return "x6"
     return expert_format()
+
+
+def _from_env():
+    """Environment overrides, validated by the setters (a bad value raises at import)."""
+    env = os.environ
+    if "MGP_CONDITIONAL" in env:
+        set_conditional_mode(env["MGP_CONDITIONAL"])
+    if "MGP_K5_PLANES" in env:
+        try:
+            planes = int(env["MGP_K5_PLANES"])
+        except ValueError:
+            raise ValueError(f"MGP_K5_PLANES={env['MGP_K5_PLANES']!r} is not 1, 2 or 3") from None
+        set_expert_planes(planes)
+    if "MGP_K5_FORMAT" in env:
+        set_expert_format(env["MGP_K5_FORMAT"])
+    if "MGP_K5_CROSS" in env:
+        set_expert_cross(env["MGP_K5_CROSS"])
+
+
+_from_env()

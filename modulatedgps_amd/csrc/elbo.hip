@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
     const float* __restrict__ lik_var, const float* __restrict__ lik_var_a, int64_t N, int K, int S,
-    float inv_tau,
+    float inv_tau, float jitter,
     const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
     uint32_t key1, int64_t n_offset, double* __restrict__ partials, float mc_a, float mc_b) {
   __shared__ double scratch[16];
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
         }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
-        sa[k] = sqrtf(va + 1e-6f);
+        sa[k] = sqrtf(va + jitter);
         if constexpr (MOD) {
           const float s2a = lik_var_a[k];
           const float da = y - ma[k];
@@ -250,11 +250,11 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
 // ------------------------------------------------------------------ K6 backward
 // Gradient of the data term of one point, DT_n = lse_s(l_s) - log S with
 // l_s = sum_k W_sk ve_k (MOD: + lse_s(la_s) - log S, la_s = sum_k W_sk ve^a_k),
-// W_s = softmax_k(x_s), x_sk = (g_sk + mu_a,k + z_sk sqrt(v_a,k + 1e-6)) / tau:
+// W_s = softmax_k(x_s), x_sk = (g_sk + mu_a,k + z_sk sqrt(v_a,k + jitter)) / tau:
 //   dDT/dve_k   = om_k = sum_s pi_s W_sk,            pi_s = exp(l_s - lse)
 //   dDT/dx_sk   = pi_s W_sk (ve_k - l_s)             (softmax Jacobian)
 //   dDT/dmu_f   = om_k (y - mu_f,k) / s2_k,  dDT/dvar_f = -om_k / (2 s2_k)
-//   dDT/dmu_a   = sum_s dDT/dx_sk / tau,     dDT/dvar_a = sum_s dDT/dx_sk z_sk / (2 tau sqrt(v_a,k + 1e-6))
+//   dDT/dmu_a   = sum_s dDT/dx_sk / tau,     dDT/dvar_a = sum_s dDT/dx_sk z_sk / (2 tau sqrt(v_a,k + jitter))
 //   dDT/ds2_k   = om_k (-1/(2 s2_k) + ((y - mu_f,k)^2 + var_f,k) / (2 s2_k^2))
 // (MOD adds the same terms of the assignment var-exp to the mu_a / var_a / s2^a
 // gradients).  Two passes over the samples with the noise redrawn (Philox is
@@ -267,8 +267,8 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
     const float* __restrict__ lik_var, const float* __restrict__ lik_var_a, int64_t N, int K, int S,
-    float inv_tau, const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
-    uint32_t key1, int64_t n_offset, float scale, float* __restrict__ G, int64_t ldg,
+    float inv_tau, float jitter, const float* __restrict__ noise_z, const float* __restrict__ noise_u,
+    uint32_t key0, uint32_t key1, int64_t n_offset, float scale, float* __restrict__ G, int64_t ldg,
     double* __restrict__ partials, float mc_a, float mc_b) {
   __shared__ double scratch[16];
   const int64_t n = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
         }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
-        sa[k] = sqrtf(va + 1e-6f);
+        sa[k] = sqrtf(va + jitter);
         if constexpr (MOD) {
           const float s2a = lik_var_a[k];
           const float da = y - ma[k];
@@ -600,7 +600,7 @@ template <int KMAX, bool MC = false>
 __global__ __launch_bounds__(256) void predict_samples_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ lik_var, int64_t N, int K,
-    int S, float inv_tau, const float* __restrict__ zw_in, const float* __restrict__ uw_in,
+    int S, float inv_tau, float jitter, const float* __restrict__ zw_in, const float* __restrict__ uw_in,
     const float* __restrict__ zy_in, uint32_t key0, uint32_t key1, int64_t n_offset,
     float* __restrict__ sy, float* __restrict__ sf, float mc_keep = 0.f, float mc_other = 0.f) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
     if (k < K) {
-      const float logit = fmaf(zw[k], sqrtf(var_a[(int64_t)k * ldf + n] + 1e-6f), mu_a[(int64_t)k * ldf + n]);
+      const float logit = fmaf(zw[k], sqrtf(var_a[(int64_t)k * ldf + n] + jitter), mu_a[(int64_t)k * ldf + n]);
       x[k] = (-logf(-logf(uw[k])) + logit) * inv_tau;
       xm = fmaxf(xm, x[k]);
     }
@@ -659,10 +659,10 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
       const float m = mu_f[(int64_t)k * ldf + n], v = var_f[(int64_t)k * ldf + n];
       den += e;
       if constexpr (MC)
-        ay = fmaf(e, fmaf(zy[k], sqrtf(ps[k] - ps[k] * ps[k] + 1e-6f), ps[k]), ay);
+        ay = fmaf(e, fmaf(zy[k], sqrtf(ps[k] - ps[k] * ps[k] + jitter), ps[k]), ay);
       else
-        ay = fmaf(e, fmaf(zy[k], sqrtf(v + lik_var[k] + 1e-6f), m), ay);
-      af = fmaf(e, fmaf(zy[k], sqrtf(v + 1e-6f), m), af);
+        ay = fmaf(e, fmaf(zy[k], sqrtf(v + lik_var[k] + jitter), m), ay);
+      af = fmaf(e, fmaf(zy[k], sqrtf(v + jitter), m), af);
     }
   if (sy) sy[(int64_t)s * N + n] = ay / den;
   if (sf) sf[(int64_t)s * N + n] = af / den;
@@ -689,7 +689,7 @@ using namespace mgp;
 
 static int predict_samples_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
                                int64_t ldf, const float* lik_var, int64_t N, int32_t K, int32_t S, float tau,
-                               const float* noise_zw, const float* noise_uw, const float* noise_zy, uint64_t seed,
+                               float jitter, const float* noise_zw, const float* noise_uw, const float* noise_zy, uint64_t seed,
                                int64_t n_offset, float* samples_y, float* samples_f, hipStream_t s, bool mc,
                                float keep, float other) {
   if (N == 0) return MGP_OK;
@@ -700,11 +700,11 @@ static int predict_samples_run(const float* mu_f, const float* var_f, const floa
   if (K <= KM) {                                                                                              \
     if (mc)                                                                                                   \
       hipLaunchKernelGGL((predict_samples_kernel<KM, true>), grid, block, 0, s, mu_f, var_f, mu_a, var_a, ldf, \
-                         lik_var, N, K, S, 1.f / tau, noise_zw, noise_uw, noise_zy, k0, k1, n_offset, samples_y, \
+                         lik_var, N, K, S, 1.f / tau, jitter, noise_zw, noise_uw, noise_zy, k0, k1, n_offset, samples_y, \
                          samples_f, keep, other);                                                              \
     else                                                                                                      \
       hipLaunchKernelGGL((predict_samples_kernel<KM, false>), grid, block, 0, s, mu_f, var_f, mu_a, var_a,     \
-                         ldf, lik_var, N, K, S, 1.f / tau, noise_zw, noise_uw, noise_zy, k0, k1, n_offset,     \
+                         ldf, lik_var, N, K, S, 1.f / tau, jitter, noise_zw, noise_uw, noise_zy, k0, k1, n_offset,     \
                          samples_y, samples_f, 0.f, 0.f);                                                      \
   } else
   MGP_PS_CASE(4) MGP_PS_CASE(8) MGP_PS_CASE(16) MGP_PS_CASE(32) {}
@@ -714,7 +714,7 @@ static int predict_samples_run(const float* mu_f, const float* var_f, const floa
 
 extern "C" int mgp_predict_samples(const float* mu_f, const float* var_f, const float* mu_a,
                                    const float* var_a, int64_t ldf, const float* lik_var, int64_t N,
-                                   int32_t K, int32_t S, float tau, const float* noise_zw,
+                                   int32_t K, int32_t S, float tau, float jitter, const float* noise_zw,
                                    const float* noise_uw, const float* noise_zy, uint64_t seed,
                                    int64_t n_offset, float* samples_y, float* samples_f,
                                    mgp_stream_t stream) {
@@ -729,16 +729,17 @@ extern "C" int mgp_predict_samples(const float* mu_f, const float* var_f, const 
   if (K > 32) return MGP_ERR_UNSUPPORTED;
   if (S < 1) return -9;
   if (!(tau > 0.f)) return -10;
+  if (!(jitter >= 0.f)) return -16;
   const bool any = noise_zw || noise_uw || noise_zy, all = noise_zw && noise_uw && noise_zy;
   if (any && !all) return -11;
   if (n_offset < 0) return -15;
-  return predict_samples_run(mu_f, var_f, mu_a, var_a, ldf, lik_var, N, K, S, tau, noise_zw, noise_uw, noise_zy,
+  return predict_samples_run(mu_f, var_f, mu_a, var_a, ldf, lik_var, N, K, S, tau, jitter, noise_zw, noise_uw, noise_zy,
                              seed, n_offset, samples_y, samples_f, (hipStream_t)stream, false, 0.f, 0.f);
 }
 
 extern "C" int mgp_predict_samples_multiclass(const float* mu_f, const float* var_f, const float* mu_a,
                                               const float* var_a, int64_t ldf, float epsilon, int64_t N,
-                                              int32_t K, int32_t S, float tau, const float* noise_zw,
+                                              int32_t K, int32_t S, float tau, float jitter, const float* noise_zw,
                                               const float* noise_uw, const float* noise_zy, uint64_t seed,
                                               int64_t n_offset, float* samples_y, float* samples_f,
                                               mgp_stream_t stream) {
@@ -753,11 +754,12 @@ extern "C" int mgp_predict_samples_multiclass(const float* mu_f, const float* va
   if (K > 32) return MGP_ERR_UNSUPPORTED;
   if (S < 1) return -9;
   if (!(tau > 0.f)) return -10;
+  if (!(jitter >= 0.f)) return -16;
   const bool any = noise_zw || noise_uw || noise_zy, all = noise_zw && noise_uw && noise_zy;
   if (any && !all) return -11;
   if (n_offset < 0) return -15;
   const float keep = 1.f - epsilon, other = (float)((double)epsilon / (double)(K - 1));
-  return predict_samples_run(mu_f, var_f, mu_a, var_a, ldf, nullptr, N, K, S, tau, noise_zw, noise_uw, noise_zy,
+  return predict_samples_run(mu_f, var_f, mu_a, var_a, ldf, nullptr, N, K, S, tau, jitter, noise_zw, noise_uw, noise_zy,
                              seed, n_offset, samples_y, samples_f, (hipStream_t)stream, true, keep, other);
 }
 
@@ -809,19 +811,19 @@ extern "C" size_t mgp_elbo_workspace_bytes(int64_t N) {
 template <int KM, bool MOD, bool MC>
 static void launch_elbo_terms(int nb, hipStream_t s, const float* mu_f, const float* var_f, const float* mu_a,
                               const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
-                              const float* lik_var_a, int64_t N, int K, int S, float inv_tau,
+                              const float* lik_var_a, int64_t N, int K, int S, float inv_tau, float jitter,
                               const float* noise_z, const float* noise_u, uint32_t k0, uint32_t k1,
                               int64_t n_offset, double* partials, float mc_a, float mc_b) {
   hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a, var_a,
-                     ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, noise_z, noise_u, k0, k1, n_offset, partials,
-                     mc_a, mc_b);
+                     ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1, n_offset,
+                     partials, mc_a, mc_b);
 }
 
 // mc: the pred likelihood is MultiClass(K)/RobustMax(eps) with mc_a = log(1 - eps),
 // mc_b = log(eps / (K - 1)) (lik_var unused); lik_var_a != NULL: SMGPModified.
 static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
                           int64_t ldf, const float* Y, const float* lik_var, const float* lik_var_a,
-                          int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
+                          int64_t N, int32_t K, int32_t S, float tau, float jitter, const float* noise_z,
                           const float* noise_u, uint64_t seed, int64_t n_offset, double* data_sum,
                           void* workspace, size_t workspace_bytes, hipStream_t s, bool mc = false,
                           float mc_a = 0.f, float mc_b = 0.f) {
@@ -834,8 +836,8 @@ static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu
   if (K <= KM) {                                                                                         \
     auto f = lik_var_a ? (mc ? launch_elbo_terms<KM, true, true> : launch_elbo_terms<KM, true, false>)   \
                        : (mc ? launch_elbo_terms<KM, false, true> : launch_elbo_terms<KM, false, false>); \
-    f(nb, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, noise_z, noise_u, \
-      k0, k1, n_offset, partials, mc_a, mc_b);                                                           \
+    f(nb, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, jitter, noise_z,  \
+      noise_u, k0, k1, n_offset, partials, mc_a, mc_b);                                                  \
   } else
     MGP_ELBO_CASE(1) MGP_ELBO_CASE(2) MGP_ELBO_CASE(4) MGP_ELBO_CASE(8) MGP_ELBO_CASE(16)
     MGP_ELBO_CASE(32) {}
@@ -849,7 +851,8 @@ static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu
 
 extern "C" int mgp_elbo_terms(const float* mu_f, const float* var_f, const float* mu_a,
                               const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
-                              int64_t N, int32_t K, int32_t S, float tau, const float* noise_z,
+                              int64_t N, int32_t K, int32_t S, float tau, float jitter,
+                              const float* noise_z,
                               const float* noise_u, uint64_t seed, int64_t n_offset,
                               double* data_sum, void* workspace, size_t workspace_bytes,
                               mgp_stream_t stream) {
@@ -865,17 +868,19 @@ extern "C" int mgp_elbo_terms(const float* mu_f, const float* var_f, const float
   if (K > 32) return MGP_ERR_UNSUPPORTED;
   if (S < 1) return -10;
   if (!(tau > 0.f)) return -11;
+  if (!(jitter >= 0.f)) return -14;
   if ((noise_z == nullptr) != (noise_u == nullptr)) return -12;
   if (n_offset < 0) return -15;
   if (!data_sum) return -16;
-  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, nullptr, N, K, S, tau, noise_z, noise_u,
+  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, nullptr, N, K, S, tau, jitter, noise_z, noise_u,
                         seed, n_offset, data_sum, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 extern "C" int mgp_elbo_terms_modified(const float* mu_f, const float* var_f, const float* mu_a,
                                        const float* var_a, int64_t ldf, const float* Y,
                                        const float* lik_var, const float* assign_lik_var, int64_t N,
-                                       int32_t K, int32_t S, float tau, const float* noise_z,
+                                       int32_t K, int32_t S, float tau, float jitter,
+                                       const float* noise_z,
                                        const float* noise_u, uint64_t seed, int64_t n_offset,
                                        double* data_sum, void* workspace, size_t workspace_bytes,
                                        mgp_stream_t stream) {
@@ -892,10 +897,11 @@ extern "C" int mgp_elbo_terms_modified(const float* mu_f, const float* var_f, co
   if (K > 32) return MGP_ERR_UNSUPPORTED;
   if (S < 1) return -11;
   if (!(tau > 0.f)) return -12;
+  if (!(jitter >= 0.f)) return -15;
   if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
   if (n_offset < 0) return -16;
   if (!data_sum) return -17;
-  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, tau, noise_z,
+  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, tau, jitter, noise_z,
                         noise_u, seed, n_offset, data_sum, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
@@ -996,17 +1002,17 @@ extern "C" size_t mgp_elbo_backward_workspace_bytes(int64_t N, int32_t K) {
 template <int KM, bool MOD, bool MC>
 static void launch_elbo_bwd(int nb, hipStream_t s, const float* mu_f, const float* var_f, const float* mu_a,
                             const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
-                            const float* lik_var_a, int64_t N, int K, int S, float inv_tau, const float* noise_z,
-                            const float* noise_u, uint32_t k0, uint32_t k1, int64_t n_offset, float scale,
+                            const float* lik_var_a, int64_t N, int K, int S, float inv_tau, float jitter,
+                            const float* noise_z, const float* noise_u, uint32_t k0, uint32_t k1, int64_t n_offset, float scale,
                             float* G, int64_t ldg, double* partials, float mc_a, float mc_b) {
   hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, MOD, MC>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
-                     var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, noise_z, noise_u, k0, k1, n_offset,
+                     var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1, n_offset,
                      scale, G, ldg, partials, mc_a, mc_b);
 }
 
 static int elbo_bwd_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a, int64_t ldf,
                         const float* Y, const float* lik_var, const float* assign_lik_var, int64_t N, int32_t K,
-                        int32_t S, float tau, const float* noise_z, const float* noise_u, uint64_t seed,
+                        int32_t S, float tau, float jitter, const float* noise_z, const float* noise_u, uint64_t seed,
                         int64_t n_offset, float scale, float* G, int64_t ldg, double* g_lik_var,
                         double* g_assign_lik_var, void* workspace, size_t workspace_bytes, hipStream_t s, bool mc,
                         float mc_a, float mc_b) {
@@ -1024,7 +1030,7 @@ static int elbo_bwd_run(const float* mu_f, const float* var_f, const float* mu_a
   if (km == KM) {                                                                                         \
     auto f = assign_lik_var ? (mc ? launch_elbo_bwd<KM, true, true> : launch_elbo_bwd<KM, true, false>)  \
                             : (mc ? launch_elbo_bwd<KM, false, true> : launch_elbo_bwd<KM, false, false>); \
-    f(nb, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, 1.f / tau, noise_z,       \
+    f(nb, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, 1.f / tau, jitter, noise_z, \
       noise_u, k0, k1, n_offset, scale, G, ldg, partials, mc_a, mc_b);                                    \
   } else
   MGP_ELBO_BWD_CASE(1) MGP_ELBO_BWD_CASE(2) MGP_ELBO_BWD_CASE(4) MGP_ELBO_BWD_CASE(8) MGP_ELBO_BWD_CASE(16)
@@ -1044,7 +1050,8 @@ static int elbo_bwd_run(const float* mu_f, const float* var_f, const float* mu_a
 extern "C" int mgp_elbo_terms_backward(const float* mu_f, const float* var_f, const float* mu_a,
                                        const float* var_a, int64_t ldf, const float* Y,
                                        const float* lik_var, const float* assign_lik_var, int64_t N,
-                                       int32_t K, int32_t S, float tau, const float* noise_z,
+                                       int32_t K, int32_t S, float tau, float jitter,
+                                       const float* noise_z,
                                        const float* noise_u, uint64_t seed, int64_t n_offset,
                                        float scale, float* G, int64_t ldg, double* g_lik_var,
                                        double* g_assign_lik_var, void* workspace,
@@ -1061,13 +1068,14 @@ extern "C" int mgp_elbo_terms_backward(const float* mu_f, const float* var_f, co
   if (K > 32) return MGP_ERR_UNSUPPORTED;
   if (S < 1) return -11;
   if (!(tau > 0.f)) return -12;
+  if (!(jitter >= 0.f)) return -15;
   if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
   if (n_offset < 0) return -16;
   if (!G) return -18;
   if (ldg < N) return -19;
   if (!g_lik_var) return -20;
   if (assign_lik_var && !g_assign_lik_var) return -21;
-  return elbo_bwd_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, tau, noise_z, noise_u,
+  return elbo_bwd_run(mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, assign_lik_var, N, K, S, tau, jitter, noise_z, noise_u,
                       seed, n_offset, scale, G, ldg, g_lik_var, g_assign_lik_var, workspace, workspace_bytes,
                       (hipStream_t)stream, false, 0.f, 0.f);
 }
@@ -1083,7 +1091,7 @@ static bool mc_consts(int K, float epsilon, float& a, float& b) {
 extern "C" int mgp_elbo_terms_multiclass(const float* mu_f, const float* var_f, const float* mu_a,
                                          const float* var_a, int64_t ldf, const float* Y, float epsilon,
                                          const float* assign_lik_var, int64_t N, int32_t K, int32_t S, float tau,
-                                         const float* noise_z, const float* noise_u, uint64_t seed,
+                                         float jitter, const float* noise_z, const float* noise_u, uint64_t seed,
                                          int64_t n_offset, double* data_sum, void* workspace,
                                          size_t workspace_bytes, mgp_stream_t stream) {
   float a, b;
@@ -1099,18 +1107,19 @@ extern "C" int mgp_elbo_terms_multiclass(const float* mu_f, const float* var_f, 
   if (K > 32) return MGP_ERR_UNSUPPORTED;
   if (S < 1) return -11;
   if (!(tau > 0.f)) return -12;
+  if (!(jitter >= 0.f)) return -15;
   if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
   if (n_offset < 0) return -16;
   if (!data_sum) return -17;
   mc_consts(K, epsilon, a, b);
-  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, nullptr, assign_lik_var, N, K, S, tau, noise_z, noise_u,
+  return elbo_terms_run(mu_f, var_f, mu_a, var_a, ldf, Y, nullptr, assign_lik_var, N, K, S, tau, jitter, noise_z, noise_u,
                         seed, n_offset, data_sum, workspace, workspace_bytes, (hipStream_t)stream, true, a, b);
 }
 
 extern "C" int mgp_elbo_terms_multiclass_backward(const float* mu_f, const float* var_f, const float* mu_a,
                                                   const float* var_a, int64_t ldf, const float* Y, float epsilon,
                                                   const float* assign_lik_var, int64_t N, int32_t K, int32_t S,
-                                                  float tau, const float* noise_z, const float* noise_u,
+                                                  float tau, float jitter, const float* noise_z, const float* noise_u,
                                                   uint64_t seed, int64_t n_offset, float scale, float* G,
                                                   int64_t ldg, double* g_assign_lik_var, void* workspace,
                                                   size_t workspace_bytes, mgp_stream_t stream) {
@@ -1127,13 +1136,14 @@ extern "C" int mgp_elbo_terms_multiclass_backward(const float* mu_f, const float
   if (K > 32) return MGP_ERR_UNSUPPORTED;
   if (S < 1) return -11;
   if (!(tau > 0.f)) return -12;
+  if (!(jitter >= 0.f)) return -15;
   if ((noise_z == nullptr) != (noise_u == nullptr)) return -13;
   if (n_offset < 0) return -16;
   if (!G) return -18;
   if (ldg < N) return -19;
   if (assign_lik_var && !g_assign_lik_var) return -20;
   mc_consts(K, epsilon, a, b);
-  return elbo_bwd_run(mu_f, var_f, mu_a, var_a, ldf, Y, nullptr, assign_lik_var, N, K, S, tau, noise_z, noise_u,
+  return elbo_bwd_run(mu_f, var_f, mu_a, var_a, ldf, Y, nullptr, assign_lik_var, N, K, S, tau, jitter, noise_z, noise_u,
                       seed, n_offset, scale, G, ldg, nullptr, g_assign_lik_var, workspace, workspace_bytes,
                       (hipStream_t)stream, true, a, b);
 }

@@ -52,11 +52,13 @@ class SquaredExponential:
         return self.K(X, X2)
 
     def _x(self, X):
+        """Inputs as float32 device rows with unit innermost stride (numpy views such
+        as linspace(...)[:, None] carry a 0 stride on the size-1 axis)."""
         X = torch.as_tensor(X)
-        if X.dtype != torch.float32 or X.device != self.device or X.stride(-1) != 1:
-            X = X.to(device=self.device, dtype=torch.float32).contiguous()
         if X.dim() == 1:
             X = X[:, None]
+        if X.dtype != torch.float32 or X.device != self.device or X.stride(-1) != 1:
+            X = torch.empty(X.shape, dtype=torch.float32, device=self.device).copy_(X)
         return X
 
     def parameters(self):

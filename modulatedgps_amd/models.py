@@ -75,6 +75,20 @@ class _Stage:
         return False
 
 
+class HostArray(np.ndarray):
+    """Host float64 array returned by the public predict_* methods: what the
+    reference's EagerTensors give the demos (numpy consumes it directly,
+    demos/demo_tf2.py:63-72,86-87,98-99, and `.numpy()` works as on a TF tensor)."""
+
+    def numpy(self):
+        return np.asarray(self)
+
+
+def _host(t):
+    """Device result -> HostArray (float64, the reference's default_float)."""
+    return t.detach().to(torch.float64).cpu().numpy().view(HostArray)
+
+
 def _to_dev(x, device, dtype=torch.float32):
     t = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x)
     return t.to(device=device, dtype=dtype)
@@ -106,6 +120,7 @@ class SVGPModified:
         if Z.dim() == 1:
             Z = Z[:, None]
         self.Z = Z.contiguous()
+        self._last_info = None
         M = self.Z.shape[0]
         self.num_latent_gps = int(num_latent_gps)
         K = self.num_latent_gps
@@ -273,9 +288,25 @@ class SGP:
         return lik.invlink.epsilon if isinstance(lik, MultiClass) else None
 
     def predict_y(self, Xnew, S=1):
-        """models.py:38-41 -> (mean, var) [S, N, K] (S broadcast copies); the
-        likelihood's _predict_mean_and_var through BroadcastingLikelihood
-        (broadcasting_lik.py:44-46): Gaussian (mu, var + sigma^2) or MultiClass (ps, ps - ps^2)."""
+        """models.py:38-41 -> (mean, var) [S, N, K] host arrays (HostArray, float64; S
+        copies); the likelihood's _predict_mean_and_var through BroadcastingLikelihood
+        (broadcasting_lik.py:44-46): Gaussian (mu, var + sigma^2) or MultiClass (ps, ps - ps^2).
+        predict_y_device returns the same as float32 device views."""
+        ym, yv = self.predict_y_device(Xnew, S)
+        self.check_linalg(self.pred_layer._last_info)
+        return _host(ym), _host(yv)
+
+    def check_linalg(self, info=None):
+        """Raise MGPLinAlgError if the last Cholesky of Kuu (both layers' for an SMGP
+        evaluation) found a non-positive pivot -- the reference's InvalidArgumentError
+        from base_conditional (models.py:141).  Reads K3's device `info` back (one host
+        sync): run_adam does it at its ELBO readback, predict_* before returning."""
+        info = getattr(self, "last_info", None) if info is None else info
+        if info is not None:
+            ops.check_info(info)
+
+    def predict_y_device(self, Xnew, S=1):
+        """predict_y as float32 device tensors [S, N, K] (broadcast views, no host copy)."""
         lik = self.likelihood.likelihood
         X = self.pred_layer.kernel._x(Xnew)
         fm, fv = self.pred_layer.conditional_kn(X)
@@ -488,7 +519,9 @@ class SMGP(SGP):
         num_data = self.num_data if self.num_data is not None else n_batch
         ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"],
                          out64=b["elbo64"])
-        return b["elbo64"] if return64 else b["elbo"]
+        # a fresh tensor per call (the reference returns a new value each time); the
+        # buffers are reused by the next evaluation
+        return (b["elbo64"] if return64 else b["elbo"]).clone()
 
     # ------------------------------------------------------------------ training
     def trainable_parameters(self):
@@ -566,7 +599,7 @@ class SMGP(SGP):
         for name, layer in (("pred", self.pred_layer), ("assign", self.assign_layer)):
             ops.kl_grad(layer.q_mu, layer.q_sqrt, num_data, grads[name + ".q_mu"], grads[name + ".q_sqrt"])
         ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"], out64=b["elbo64"])
-        return b["elbo"], grads
+        return b["elbo"].clone(), grads
 
     def training_loss_closure(self, data_iter, compile=True):
         """GPflow ExternalDataTrainingLossMixin.training_loss_closure: () -> -ELBO on the next batch."""
@@ -589,14 +622,26 @@ class SMGP(SGP):
 
     # ------------------------------------------------------------------ predictions
     def predict_assign(self, Xnew, S=1):
-        """models.py:85-89: softmax_K(mean_S mu_a) -> [N, K]."""
+        """models.py:85-89: softmax_K(mean_S mu_a) -> [N, K] host array (HostArray, float64)."""
+        asg = self.predict_assign_device(Xnew, S)
+        self.check_linalg(self.assign_layer._last_info)
+        return _host(asg)
+
+    def predict_assign_device(self, Xnew, S=1):
+        """predict_assign as a float32 device tensor [N, K]."""
         X = self.assign_layer.kernel._x(Xnew)
         am, _ = self.assign_layer.conditional_kn(X)
         _, _, asg = ops.predict_epilogue(None, None, am, None, want_y=False, want_assign=True)
         return asg
 
     def predict_samples(self, Xnew, S=1, noise=None, seed=None):
-        """models.py:91-103 -> samples_y, samples_f [S, N, 1]."""
+        """models.py:91-103 -> samples_y, samples_f [S, N, 1] host arrays (HostArray, float64)."""
+        sy, sf = self.predict_samples_device(Xnew, S, noise=noise, seed=seed)
+        self.check_linalg()
+        return _host(sy), _host(sf)
+
+    def predict_samples_device(self, Xnew, S=1, noise=None, seed=None):
+        """predict_samples as float32 device tensors [S, N, 1]."""
         X = self.pred_layer.kernel._x(Xnew)
         mu_f, var_f, mu_a, var_a = self.conditionals(X)
         if seed is None and noise is None:

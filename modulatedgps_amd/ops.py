@@ -12,6 +12,7 @@ outputs are [K][N] views.
 import torch
 
 from . import _lib
+from .config import default_jitter
 
 F32 = torch.float32
 
@@ -361,10 +362,12 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
 
 
 def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0,
-                        n_offset=0, scale=1.0, assign_lik_var=None, G=None, workspace=None, multiclass_eps=None):
+                        n_offset=0, scale=1.0, assign_lik_var=None, G=None, workspace=None, multiclass_eps=None,
+                        jitter=None):
     """Gradient of the data term: G [4, K, N] = scale * d/d(mu_f, var_f, mu_a, var_a) and the
     likelihood-variance gradients (float64 [K]; second one for SMGPModified, else None).
     multiclass_eps: MultiClass / RobustMax pred likelihood (no likelihood-variance gradient: None)."""
+    jitter = default_jitter() if jitter is None else jitter
     for t, n in ((mu_f, "mu_f"), (var_f, "var_f"), (mu_a, "mu_a"), (var_a, "var_a")):
         _check(t, n, 2)
     ldf = _ld(mu_f)
@@ -391,14 +394,16 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
     if multiclass_eps is not None:
         _lib.call("mgp_elbo_terms_multiclass_backward", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
                   var_a.data_ptr(), ldf, Y.data_ptr(), float(multiclass_eps),
-                  assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau), zp, up,
+                  assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau),
+                  float(jitter), zp, up,
                   int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), G.stride(1),
                   glva.data_ptr() if glva is not None else None, workspace.data_ptr(), workspace.numel(),
                   _stream())
         return G, glv, glva
     _lib.call("mgp_elbo_terms_backward", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
               var_a.data_ptr(), ldf, Y.data_ptr(), lik_var.data_ptr(),
-              assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau), zp, up,
+              assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau),
+              float(jitter), zp, up,
               int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), G.stride(1),
               glv.data_ptr(), glva.data_ptr() if glva is not None else None, workspace.data_ptr(),
               workspace.numel(), _stream())
@@ -567,10 +572,11 @@ def gauss_kl_white(q_mu, q_sqrt, out=None, workspace=None):
 
 # --------------------------------------------------------------------------- K6
 def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0, n_offset=0,
-               out=None, workspace=None, assign_lik_var=None, multiclass_eps=None):
+               out=None, workspace=None, assign_lik_var=None, multiclass_eps=None, jitter=None):
     """Sum over local points of logsumexp_s(sum_k W ve) - log S (float64 [1]).
     With assign_lik_var: the SMGPModified data term (models.py:112-123).
     multiclass_eps: the pred likelihood is MultiClass(K) / RobustMax(eps) (lik_var unused)."""
+    jitter = default_jitter() if jitter is None else jitter
     for t, n in ((mu_f, "mu_f"), (var_f, "var_f"), (mu_a, "mu_a"), (var_a, "var_a")):
         _check(t, n, 2)
     ldf = _ld(mu_f)
@@ -602,7 +608,8 @@ def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, se
             _check(assign_lik_var, "assign_lik_var")
         _lib.call("mgp_elbo_terms_multiclass", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
                   var_a.data_ptr(), ldf, Y.data_ptr(), float(multiclass_eps),
-                  assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau), zp, up,
+                  assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau),
+                  float(jitter), zp, up,
                   int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(), workspace.data_ptr(),
                   workspace.numel(), _stream())
         return out
@@ -610,11 +617,11 @@ def elbo_terms(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, se
         _check(assign_lik_var, "assign_lik_var")
         _lib.call("mgp_elbo_terms_modified", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
                   var_a.data_ptr(), ldf, Y.data_ptr(), lik_var.data_ptr(), assign_lik_var.data_ptr(), N, K,
-                  S, float(tau), zp, up, int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(),
+                  S, float(tau), float(jitter), zp, up, int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(),
                   workspace.data_ptr(), workspace.numel(), _stream())
         return out
     _lib.call("mgp_elbo_terms", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(), var_a.data_ptr(),
-              ldf, Y.data_ptr(), lik_var.data_ptr(), N, K, S, float(tau), zp, up,
+              ldf, Y.data_ptr(), lik_var.data_ptr(), N, K, S, float(tau), float(jitter), zp, up,
               int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(), workspace.data_ptr(),
               workspace.numel(), _stream())
     return out
@@ -665,9 +672,10 @@ def philox_normal2(seed, n_offset, N, K, S, device):
 
 
 def predict_samples(mu_f, var_f, mu_a, var_a, lik_var, S, tau=1e-2, noise=None, seed=0,
-                    n_offset=0, multiclass_eps=None):
+                    n_offset=0, multiclass_eps=None, jitter=None):
     """samples_y, samples_f [S, N] (models.py:91-103); multiclass_eps: MultiClass / RobustMax
     predictive mean / variance for samples_y (lik_var unused)."""
+    jitter = default_jitter() if jitter is None else jitter
     K, N = mu_f.shape
     dev = mu_f.device
     sy = torch.empty(S, N, dtype=F32, device=dev)
@@ -682,11 +690,11 @@ def predict_samples(mu_f, var_f, mu_a, var_a, lik_var, S, tau=1e-2, noise=None, 
         ptrs = [t.data_ptr() for t in noise]
     if multiclass_eps is not None:
         _lib.call("mgp_predict_samples_multiclass", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
-                  var_a.data_ptr(), _ld(mu_f), float(multiclass_eps), N, K, S, float(tau), *ptrs,
+                  var_a.data_ptr(), _ld(mu_f), float(multiclass_eps), N, K, S, float(tau), float(jitter), *ptrs,
                   int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), sy.data_ptr(), sf.data_ptr(), _stream())
         return sy, sf
     _lib.call("mgp_predict_samples", mu_f.data_ptr(), var_f.data_ptr(), mu_a.data_ptr(),
-              var_a.data_ptr(), _ld(mu_f), lik_var.data_ptr(), N, K, S, float(tau), *ptrs,
+              var_a.data_ptr(), _ld(mu_f), lik_var.data_ptr(), N, K, S, float(tau), float(jitter), *ptrs,
               int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), sy.data_ptr(), sf.data_ptr(), _stream())
     return sy, sf
 

@@ -45,6 +45,8 @@ def normwise(a, b):
 
 
 def to_np(t):
+    if isinstance(t, np.ndarray):  # the public predict_* return host arrays
+        return np.asarray(t, np.float64)
     return t.detach().double().cpu().numpy()
 
 

@@ -203,3 +203,72 @@ def test_expert_parallel_elbo(device, world):
         assert pr.exitcode == 0
     assert e == pytest.approx(ref, rel=1e-6)
     assert e == pytest.approx(oracle, rel=1e-4)
+
+
+def test_cholesky_failure_raises(device):
+    """A non-SPD Kuu (duplicated inducing points, zero jitter) raises MGPLinAlgError
+    where the reference raises InvalidArgumentError from base_conditional
+    (models.py:141): at run_adam's ELBO readback and in the predict_* methods."""
+    from modulatedgps_amd import config
+    from modulatedgps_amd._lib import MGPLinAlgError
+    from utils.data import Dataset
+    from utils.training_utils import run_adam
+    X, Y, p = R.synthetic_problem(500, 20, 3, 1, 0.5, state="perturbed", S=5)
+    p.pred["Z"][7] = p.pred["Z"][3]                   # two identical rows: Kuu singular
+    old = config.default_jitter()
+    config.set_default_jitter(0.0)
+    try:
+        model = build_model(p, device)
+        Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+        model._build_likelihood(Xd, Y)                 # asynchronous: no raise here
+        assert int(model.last_info.cpu()[0]) > 0
+        with pytest.raises(MGPLinAlgError):
+            model.check_linalg()
+        with pytest.raises(MGPLinAlgError):
+            model.predict_y(Xd)
+        with pytest.raises(MGPLinAlgError):
+            model.predict_samples(Xd, S=2)
+        it = iter(Dataset.from_tensor_slices((X, Y)).shuffle(500, seed=0).batch(100).repeat())
+        with pytest.raises(MGPLinAlgError):
+            run_adam(model, 10, it, 0.01)
+    finally:
+        config.set_default_jitter(old)
+
+
+def test_default_jitter_reaches_sampling(device):
+    """set_default_jitter changes both Kuu's jitter and the reparameterisation
+    jitter of W_dist / predict_samples (utils.py:26-27 reads default_jitter())."""
+    from modulatedgps_amd import config
+    X, Y, p = R.synthetic_problem(700, 25, 3, 1, 0.5, state="perturbed", S=6)
+    z, u = R.explicit_noise(6, 700, 3, seed=5)
+    old, old_r = config.default_jitter(), R.JITTER
+    try:
+        config.set_default_jitter(1e-3)
+        R.JITTER = 1e-3
+        ref = R.smgp_elbo(X, Y, p, z, u)
+        model = build_model(p, device)
+        Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+        e = float(model._build_likelihood(Xd, Y, noise=dev_noise(z, u, device)).cpu())
+        assert e == pytest.approx(ref, rel=1e-4)
+        rng = np.random.default_rng(9)
+        zw, uw, zy = rng.standard_normal((4, 700, 3)), rng.uniform(1e-6, 1 - 1e-6, (4, 700, 3)), \
+            rng.standard_normal((4, 700, 3))
+        sy_r, sf_r = R.predict_samples(X, p, 4, zw, uw, zy)
+        noise = [torch.as_tensor(a, dtype=torch.float32, device=device) for a in (zw, uw, zy)]
+        sy, sf = model.predict_samples(Xd, 4, noise=noise)
+        assert normwise(sf, sf_r) < 1e-4 and normwise(sy, sy_r) < 1e-4
+    finally:
+        config.set_default_jitter(old)
+        R.JITTER = old_r
+
+
+def test_elbo_returns_fresh_tensors(device):
+    """Each evaluation returns its own tensor (kept values do not alias the buffers)."""
+    X, Y, p = R.synthetic_problem(600, 20, 3, 1, 0.5, state="perturbed", S=5)
+    model = build_model(p, device)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    vals = [model.elbo((Xd, Y)) for _ in range(3)]     # fresh Philox noise per call
+    host = [float(v.cpu()) for v in vals]
+    assert len(set(host)) == 3
+    e, _ = model.elbo_and_grad(Xd, Y)
+    assert float(vals[0].cpu()) == host[0] and e.data_ptr() != vals[-1].data_ptr()

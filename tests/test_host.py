@@ -70,3 +70,45 @@ def test_config_expert_cross_knob():
             config.set_expert_cross("bf16")
     finally:
         config.set_expert_cross(old)
+
+
+def test_host_arrays_feed_the_demo_post_processing():
+    """predict_* return HostArray (float64 numpy); the demo's numpy lines
+    (demos/demo_tf2.py, reference demo_tf2.py:63-72,98-99) and `.numpy()` work."""
+    import numpy as np
+    from modulatedgps_amd.models import HostArray
+    sy = np.random.default_rng(0).standard_normal((100, 50, 1)).view(HostArray)
+    samples_y = np.hstack([sy, sy])
+    assert samples_y.shape == (100, 100, 1)
+    assert np.mean(samples_y, 0).shape == (100, 1)
+    assert np.reshape(samples_y, (100 * 100, -1)).shape == (10000, 1)
+    assert isinstance(sy.numpy(), np.ndarray) and sy.numpy().dtype == np.float64
+
+
+def test_env_config_is_validated():
+    """MGP_* environment overrides go through the setters (a bad value raises at import)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import modulatedgps_amd.config as c; print(c.expert_format(), c.expert_planes())"
+    ok = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                        env={**os.environ, "MGP_K5_FORMAT": "x6", "MGP_K5_PLANES": "2"})
+    assert ok.returncode == 0 and ok.stdout.split() == ["x6", "2"]
+    for k, v in (("MGP_K5_FORMAT", "bf8"), ("MGP_K5_PLANES", "4"), ("MGP_K5_CROSS", "x"),
+                 ("MGP_CONDITIONAL", "f64")):
+        bad = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                             env={**os.environ, k: v})
+        assert bad.returncode != 0 and "ValueError" in bad.stderr, (k, v)
+
+
+def test_bench_refuses_missing_gpus():
+    """`bench.py --gpus N` with fewer than N visible devices exits non-zero (here: none)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "MGP_BENCH_SHARE_GPU")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=root, capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 2 and "device(s) visible" in r.stderr

@@ -40,3 +40,24 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(_lib.MGPLibraryError):
         _lib.load()
+
+
+def test_binding_arities_match_header():
+    """Each ctypes prototype has as many arguments as the header declaration."""
+    import re
+    text = re.sub(r"/\*.*?\*/", "", open(_lib.HEADER_PATH).read(), flags=re.S)
+    for name, (_, args) in _lib.SIGNATURES.items():
+        m = re.search(r"\b" + name + r"\s*\(([^;]*?)\)\s*;", text, re.S)
+        assert m, name
+        decl = m.group(1).strip()
+        n = 0 if decl in ("", "void") else decl.count(",") + 1
+        assert n == len(args), (name, n, len(args))
+
+
+def test_jitter_argument_is_validated():
+    """The reparameterisation jitter (default_jitter(), utils.py:26-27) is an ABI
+    argument of K6 and the sampler; a negative value is rejected before any HIP call."""
+    lib = _lib.load()
+    c = ctypes.c_void_p(8)
+    rc = lib.mgp_elbo_terms(c, c, c, c, 4, c, c, 4, 2, 3, 0.01, -1.0, None, None, 0, 0, c, c, 64, None)
+    assert rc == -14
