@@ -257,11 +257,14 @@ __device__ __forceinline__ void blk_store(double* __restrict__ s, const doublex4
 }
 
 // Panel P (columns 16P..16P+15) of the diagonal tile, wave 0: lane r keeps the
-// 16 panel entries of row r; square-root-free right-looking sweep whose column
-// broadcasts are readlanes from the owning lane (no LDS round trip on the
-// critical path).  Writes L's panel (zeros above the diagonal) and
-// col[16P + c] = 1 / L[16P + c][16P + c].  (A division-free Bareiss-scaled
-// sweep was measured 18 % slower: the wave is issue-bound, not latency-bound.)
+// 16 panel entries of row r; right-looking sweep whose column broadcasts are
+// readlanes from the owning lanes (no LDS round trip on the critical path).
+// Per column c the 15 - c broadcasts are read before the pivot chain (they are
+// final once column c - 1 is applied), so the only serial work per column is
+// rsq + two Newton steps (1/piv = rs^2, no second reciprocal chain) and one
+// multiply before the next column's FMA; the remaining FMAs of column c overlap
+// the next pivot's chain.  Writes L's panel (zeros above the diagonal) and
+// col[16P + c] = 1 / L[16P + c][16P + c].
 template <int P>
 __device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __restrict__ col, int r, int& bad) {
   constexpr int C0 = 16 * P;
@@ -269,14 +272,25 @@ __device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __
 #pragma unroll
   for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + C0 + j];
   double rs[16];
+  // software pipeline: column c's pivot chain is issued before column c - 1's
+  // remaining FMAs (only a[c] had to be updated first)
+  double piv = read_lane_f64(a[0], C0);
+  if (!(piv > 0.0) && bad == 0) bad = C0 + 1;
+  rs[0] = rsqrt_f64(piv);
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
-    const double piv = read_lane_f64(a[c], C0 + c);
-    if (!(piv > 0.0) && bad == 0) bad = C0 + c + 1;
-    const double t = a[c] * rcp_f64(piv);
-    rs[c] = rsqrt_f64(piv);
+    double v[16];
 #pragma unroll
-    for (int s2 = c + 1; s2 < 16; ++s2) a[s2] = fma(-t, read_lane_f64(a[c], C0 + s2), a[s2]);
+    for (int s2 = c + 1; s2 < 16; ++s2) v[s2] = read_lane_f64(a[c], C0 + s2);  // column c, rows C0 + s2
+    const double t = a[c] * (rs[c] * rs[c]);                                // a[r][c] / piv_c
+    if (c + 1 < 16) {
+      a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+      piv = read_lane_f64(a[c + 1], C0 + c + 1);
+      if (!(piv > 0.0) && bad == 0) bad = C0 + c + 2;
+      rs[c + 1] = rsqrt_f64(piv);
+    }
+#pragma unroll
+    for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
   }
 #pragma unroll
   for (int c = 0; c < 16; ++c) sF[r * LDT + C0 + c] = (r >= C0 + c) ? a[c] * rs[c] : 0.0;

@@ -7,7 +7,7 @@ set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   tail -2 gpurun_out/pytest_gpu.log
 fi
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
