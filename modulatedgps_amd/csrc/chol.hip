@@ -193,6 +193,82 @@ __device__ __forceinline__ void quad_to_global(double* __restrict__ g, int64_t l
   quad_foreach([&](int ti, int tj, int r, int row, int col) { g[(int64_t)row * ld + col] = q.c[ti][tj][r]; });
 }
 
+// Wave-striped 64x64 products that skip the zero blocks of a triangular
+// operand and give every wave the same MFMA count.  RowBlk: wave w owns the
+// 16-row stripe w (blocks (w, tj)); ColBlk: wave w owns the 16-column stripe w
+// (blocks (ti, w)).  Lane / register layout per 16x16 block as blk_mma.
+struct Blk4 {
+  doublex4 c[4];
+};
+__device__ __forceinline__ Blk4 blk4_zero() {
+  Blk4 r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) r.c[t] = doublex4{0.0, 0.0, 0.0, 0.0};
+  return r;
+}
+
+// Row stripe: C[16w + i][16tj + j] += sign * sum_k A(i, k) B(k, j), A = sa[16w + i][k],
+// B(k, j) = TB ? sb[16tj + j][k] : sb[k][16tj + j].  TRI = 0: every k; TRI = 1:
+// k < 16 (tj + 1) (B = D^T, D lower triangular: 40 of 64 MFMAs); TRI = 2:
+// k >= 16 tj (B = D, lower triangular).
+template <bool TB, int TRI>
+__device__ __forceinline__ void row_mma(Blk4& r, const double* __restrict__ sa, const double* __restrict__ sb,
+                                        double sign) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+    const int k = k0 + kq;
+    const double av = sign * sa[(16 * w + l16) * LDT + k];
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) {
+      if (TRI == 1 && k0 >= 16 * (tj + 1)) continue;
+      if (TRI == 2 && k0 < 16 * tj) continue;
+      const double bv = TB ? sb[(16 * tj + l16) * LDT + k] : sb[k * LDT + 16 * tj + l16];
+      r.c[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, r.c[tj], 0, 0, 0);
+    }
+  }
+}
+
+// Column stripe: C[16ti + i][16w + j] += sum_k D[16ti + i][k] sb[k][16w + j] with
+// D lower triangular (k < 16 (ti + 1)): X_jc = D_j B_jc.
+__device__ __forceinline__ void col_mma_lower(Blk4& r, const double* __restrict__ sD, const double* __restrict__ sb) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+    const int k = k0 + kq;
+    const double bv = sb[k * LDT + 16 * w + l16];
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti) {
+      if (k0 >= 16 * (ti + 1)) continue;
+      const double av = sD[(16 * ti + l16) * LDT + k];
+      r.c[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, r.c[ti], 0, 0, 0);
+    }
+  }
+}
+
+template <bool ROW, typename F>
+__device__ __forceinline__ void blk4_foreach(F f) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = (lane >> 4) + 4 * q, cc = lane & 15;
+      if (ROW) f(t, q, 16 * w + rr, 16 * t + cc);
+      else f(t, q, 16 * t + rr, 16 * w + cc);
+    }
+}
+template <bool ROW>
+__device__ __forceinline__ void blk4_to_lds(double* __restrict__ s, const Blk4& r) {
+  blk4_foreach<ROW>([&](int t, int q, int row, int col) { s[row * LDT + col] = r.c[t][q]; });
+}
+__device__ __forceinline__ void row_from_global(Blk4& r, const double* __restrict__ g, int64_t ld) {
+  blk4_foreach<true>([&](int t, int q, int row, int col) { r.c[t][q] = g[(int64_t)row * ld + col]; });
+}
+__device__ __forceinline__ void row_to_global(double* __restrict__ g, int64_t ld, const Blk4& r) {
+  blk4_foreach<true>([&](int t, int q, int row, int col) { g[(int64_t)row * ld + col] = r.c[t][q]; });
+}
+
 // Uniform double from lane `lane` (compile-time) of a VGPR pair.
 __device__ __forceinline__ double read_lane_f64(double v, int lane) {
   const uint64_t u = (uint64_t)__double_as_longlong(v);
@@ -256,6 +332,26 @@ __device__ __forceinline__ void blk_store(double* __restrict__ s, const doublex4
   for (int r = 0; r < 4; ++r) s[((lane >> 4) + 4 * r) * LDT + (lane & 15)] = v[r];
 }
 
+// Lower 16x16 blocks (bi >= bj) of the diagonal tile s -= P P^T, in place in LDS;
+// the 10 blocks dealt 3/3/2/2 over the waves (48 MFMAs at most per wave).
+__device__ __forceinline__ void diag_lower_update(double* __restrict__ s, const double* __restrict__ sP) {
+  const int w = threadIdx.x >> 6;
+  for (int q = w; q < 10; q += 4) {
+    int bi = 0;
+    while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+    const int bj = q - bi * (bi + 1) / 2;
+    doublex4 acc = blk_load(s + 16 * bi * LDT + 16 * bj);
+    const int lane = threadIdx.x & 63, l16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int k0 = 0; k0 < CB; k0 += 4) {
+      const double av = -sP[(16 * bi + l16) * LDT + k0 + kq];
+      const double bv = sP[(16 * bj + l16) * LDT + k0 + kq];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+    blk_store(s + 16 * bi * LDT + 16 * bj, acc);
+  }
+}
+
 // Panel P (columns 16P..16P+15) of the diagonal tile, wave 0: lane r keeps the
 // 16 panel entries of row r; right-looking sweep whose column broadcasts are
 // readlanes from the owning lanes (no LDS round trip on the critical path).
@@ -317,35 +413,32 @@ __device__ __forceinline__ void panel_update(double* __restrict__ sF, int w, int
   }
 }
 
-// X_pp = L_pp^-1 of diagonal block p (one wave; quad layout: lane = column
-// cc x row group g, DPP broadcast of the pivot row); needs col[16p ..].
+// X_pp = L_pp^-1 of diagonal block p (one wave; needs col[16p ..] = 1 / L_rr).
+// Lane cc (of 16; the other lanes duplicate) owns column cc of X and runs the
+// right-looking forward substitution in registers: x_k = acc_k / L_kk, then
+// acc_r -= L_rk x_k for r > k, with the L_rk wave-uniform LDS broadcasts.  The
+// serial chain is one multiply and one FMA per row (the quad-layout version
+// broadcast every pivot through DPP: ~5 K cycles, this one ~1 K).
 __device__ __forceinline__ void inv_diag_block(const double* __restrict__ sF, double* __restrict__ sX,
                                                const double* __restrict__ col, int p, int lane) {
-  const int cc = lane >> 2, g = lane & 3;
+  const int cc = lane & 15;
   const double* L = sF + 16 * p * LDT + 16 * p;
-  double x[4];
+  double acc[16], rs[16];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) x[k] = (4 * g + k == cc) ? 1.0 : 0.0;
-#pragma unroll
-  for (int I = 0; I < 16; ++I) {
-    const int GI = I >> 2, KI = I & 3;
-    double xi = x[KI] * col[16 * p + I];
-    switch (GI) {  // compile-time after unrolling
-      case 0: xi = quad_bcast_f64<0>(xi); break;
-      case 1: xi = quad_bcast_f64<1>(xi); break;
-      case 2: xi = quad_bcast_f64<2>(xi); break;
-      default: xi = quad_bcast_f64<3>(xi); break;
-    }
-    if (g == GI) x[KI] = xi;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int row = 4 * g + k;
-      const double l = L[row * LDT + I];
-      x[k] = (row > I) ? fma(-l, xi, x[k]) : x[k];
-    }
+  for (int r = 0; r < 16; ++r) {
+    acc[r] = (r == cc) ? 1.0 : 0.0;
+    rs[r] = col[16 * p + r];
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) sX[(16 * p + 4 * g + k) * LDT + 16 * p + cc] = x[k];
+  for (int k = 0; k < 16; ++k) {
+    acc[k] *= rs[k];                      // x_k (final)
+#pragma unroll
+    for (int r = k + 1; r < 16; ++r) acc[r] = fma(-L[r * LDT + k], acc[k], acc[r]);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sX[(16 * p + r) * LDT + 16 * p + cc] = acc[r];
+  }
 }
 
 // X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj (one wave, f64 MFMA; the product's
@@ -386,12 +479,16 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int bad = 0;
+  const int js = (int)(gcol0 / CB) - 1;
   if (w == 0) panel_factor<0>(sF, col, lane, bad);
+  STAMP(js, 8);
   __syncthreads();
   panel_update<0>(sF, w);
   __syncthreads();
+  STAMP(js, 9);
   if (w == 0) panel_factor<1>(sF, col, lane, bad);
   else if (w == 1) inv_diag_block(sF, sX, col, 0, lane);
+  STAMP(js, 10);
   __syncthreads();
   if (w < 3) {
     panel_update<1>(sF, w, 3);
@@ -402,8 +499,10 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     }
   }
   __syncthreads();
+  STAMP(js, 11);
   if (w == 0) panel_factor<2>(sF, col, lane, bad);
   else if (w == 1) inv_diag_block(sF, sX, col, 1, lane);
+  STAMP(js, 12);
   __syncthreads();
   if (w == 0) panel_update<2>(sF, 0, 1);
   else if (w == 1) inv_offdiag_block(sF, sX, 1, 0, lane);
@@ -415,11 +514,12 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     inv_diag_block(sF, sX, col, 2, lane);
   }
   __syncthreads();
-  STAMP((int)(gcol0 / CB) - 1, 5);
+  STAMP(js, 5);
   if (w == 0) inv_diag_block(sF, sX, col, 3, lane);
   else if (w == 1) inv_offdiag_block(sF, sX, 2, 1, lane);
   else if (w == 2) inv_offdiag_block(sF, sX, 2, 0, lane);
   __syncthreads();
+  STAMP(js, 13);
   if (w < 3) inv_offdiag_block(sF, sX, 3, 2 - w, lane);
   __syncthreads();
 }
@@ -493,10 +593,10 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     if (c < j) tile_load(s1, Bt(j, c), Mp);
     __syncthreads();
     if (c < j) {
-      Quad x = quad_zero();
-      tile_mma<false, false>(x, sD, s1, 1.0);
+      Blk4 x = blk4_zero();
+      col_mma_lower(x, sD, s1);
       __syncthreads();
-      quad_to_lds(s1, x);
+      blk4_to_lds<false>(s1, x);
       __syncthreads();
       store_linvT(c, s1);
     } else {
@@ -513,22 +613,22 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     const bool la = (ai == 0 && bl_ == 0);
     if (la) STAMP(j, 0);
     TileRegs r1, rD, r2;
-    Quad u;
+    Blk4 u;
     tile_fetch(r1, Wt(i, j), Mp);
     tile_fetch(rD, ws_D(a, b, j), CB);
-    if (l != i) tile_fetch(r2, Wt(l, j), Mp);
-    quad_from_global(u, Wt(i, l), Mp);  // the updated tile, in flight with the operands
+    tile_fetch(r2, (l != i) ? Wt(l, j) : Wt(i, l), Mp);  // P_l's operand, or the diagonal tile itself
+    if (l != i) row_from_global(u, Wt(i, l), Mp);      // the updated tile, in flight with the operands
     tile_put(s1, r1);
     tile_put(sD, rD);
-    if (l != i) tile_put(s2, r2);
+    tile_put(s2, r2);
     __syncthreads();
     if (la) STAMP(j, 1);
-    Quad pi = quad_zero(), pl = quad_zero();
-    tile_mma<false, true>(pi, s1, sD, 1.0);                 // P_i = W_ij D_j^T
-    if (l != i) tile_mma<false, true>(pl, s2, sD, 1.0);     // P_l
+    Blk4 pi = blk4_zero(), pl = blk4_zero();
+    row_mma<true, 1>(pi, s1, sD, 1.0);                 // P_i = W_ij D_j^T (D lower: 40 MFMAs/wave)
+    if (l != i) row_mma<true, 1>(pl, s2, sD, 1.0);     // P_l
     __syncthreads();
-    quad_to_lds(s1, pi);
-    if (l != i) quad_to_lds(s2, pl);
+    blk4_to_lds<true>(s1, pi);
+    if (l != i) blk4_to_lds<true>(s2, pl);
     __syncthreads();
     if (la) STAMP(j, 2);
     if (l == i && a.L) {
@@ -536,21 +636,26 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
       tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
                      (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
     }
-    tile_mma<false, true>(u, s1, (l == i) ? s1 : s2, -1.0);  // W_il -= P_i P_l^T
-    if (ai == 0 && bl_ == 0) {  // look-ahead: factor the next diagonal tile
+    if (l != i) {
+      row_mma<true, 0>(u, s1, s2, -1.0);               // W_il -= P_i P_l^T
+      row_to_global(Wt(i, l), Mp, u);
+      return;
+    }
+    // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T in place in LDS (s2)
+    diag_lower_update(s2, s1);
+    if (la) {  // look-ahead: factor the next diagonal tile
       __syncthreads();
       STAMP(j, 3);
-      quad_to_lds(s1, u);
-      __syncthreads();
       STAMP(j, 4);
-      factor_diag_tile(s1, s2, col, a.info + b, (int64_t)(j + 1) * CB);
+      factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB);
       STAMP(j, 6);
       __syncthreads();
-      write_diag(a, b, j + 1, s1, s2);
+      write_diag(a, b, j + 1, s2, s1);
       __syncthreads();
       STAMP(j, 7);
     } else {
-      quad_to_global(Wt(i, l), Mp, u);
+      __syncthreads();
+      tile_store_f64(Wt(i, l), Mp, s2);
     }
     return;
   }
@@ -559,28 +664,32 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   const int x = idx - nU;
   const int i = j + 1 + x / (j + 1), c = x % (j + 1);
   TileRegs r1, rD, r2;
-  Quad u = quad_zero();
+  Blk4 u = blk4_zero();
   tile_fetch(r1, Wt(i, j), Mp);
   tile_fetch(rD, ws_D(a, b, j), CB);
   if (c < j) {
     tile_fetch(r2, Bt(j, c), Mp);
-    quad_from_global(u, Bt(i, c), Mp);
+    row_from_global(u, Bt(i, c), Mp);
   }
   tile_put(s1, r1);
   tile_put(sD, rD);
   if (c < j) tile_put(s2, r2);
   __syncthreads();
-  Quad pi = quad_zero(), xq = quad_zero();
-  tile_mma<false, true>(pi, s1, sD, 1.0);                   // P_i
-  if (c < j) tile_mma<false, false>(xq, sD, s2, 1.0);       // X_jc = D_j B_jc
+  Blk4 pi = blk4_zero(), xq = blk4_zero();
+  row_mma<true, 1>(pi, s1, sD, 1.0);                   // P_i
+  if (c < j) col_mma_lower(xq, sD, s2);                // X_jc = D_j B_jc
   __syncthreads();
-  quad_to_lds(s1, pi);
-  if (c < j) quad_to_lds(s2, xq);
+  blk4_to_lds<true>(s1, pi);
+  if (c < j) blk4_to_lds<false>(s2, xq);
   __syncthreads();
-  const double* sx = (c < j) ? s2 : sD;                     // X_jj = D_j
-  if (i == j + 1) store_linvT(c, sx);
-  tile_mma<false, false>(u, s1, sx, -1.0);                  // B_ic -= P_i X_jc
-  quad_to_global(Bt(i, c), Mp, u);
+  if (c < j) {
+    if (i == j + 1) store_linvT(c, s2);
+    row_mma<false, 0>(u, s1, s2, -1.0);                // B_ic -= P_i X_jc
+  } else {                                             // X_jj = D_j (lower triangular)
+    if (i == j + 1) store_linvT(c, sD);
+    row_mma<false, 2>(u, s1, sD, -1.0);
+  }
+  row_to_global(Bt(i, c), Mp, u);
 }
 
 // ------------------------------------------------------------------ Cholesky backward

@@ -29,9 +29,11 @@ buf = (ctypes.c_ulonglong * (64 * 16))()
 lib.mgp_dbg_chol_stamps(buf)
 st = [[buf[j * 16 + k] for k in range(16)] for j in range(64)]
 steps = M // 64 - 1
-print("step  load  P_i  update  stage  panels  inverse  write  | next-step gap")
+print("step  load  P_i  update  stage  panels  inverse  write  | next-step gap  || panel0 upd0 panel1 upd1 panel2 upd2+panel3 | inv-a inv-b")
 for j in range(steps):
     s = st[j]
     d = [s[k + 1] - s[k] if s[k + 1] and s[k] else 0 for k in range(7)]
     gap = (st[j + 1][0] - s[7]) if j + 1 < steps and st[j + 1][0] else 0
-    print(j, d[0], d[1], d[2], d[3], s[5] - s[4], s[6] - s[5], s[7] - s[6], "|", gap)
+    sub = [s[8] - s[4], s[9] - s[8], s[10] - s[9], s[11] - s[10], s[12] - s[11], s[5] - s[12], "|",
+           s[13] - s[5], s[6] - s[13]] if s[8] else []
+    print(j, d[0], d[1], d[2], d[3], s[5] - s[4], s[6] - s[5], s[7] - s[6], "|", gap, "||", *sub)
