@@ -457,6 +457,17 @@ __device__ __forceinline__ void inv_offdiag_block(const double* __restrict__ sF,
   blk_store(sX + 16 * i * LDT + 16 * j, xv);
 }
 
+// -X_ii Y for Y in accumulator layout (the registers are the B operand as they stand).
+__device__ __forceinline__ doublex4 neg_x_times(const double* __restrict__ Xii, const doublex4& y, int lane) {
+  doublex4 xv = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const double av = -Xii[(lane & 15) * LDT + 4 * s4 + (lane >> 4)];
+    xv = __builtin_amdgcn_mfma_f64_16x16x4f64(av, y[s4], xv, 0, 0, 0);
+  }
+  return xv;
+}
+
 // Factor the symmetric 64x64 tile in sF (lower part used) in place: sF <- L
 // (zeros above), sX <- L^-1 (zeros above).  Called by all 256 threads.
 //
@@ -471,9 +482,12 @@ __device__ __forceinline__ void inv_offdiag_block(const double* __restrict__ sF,
 //   U1  update 1 (w0..w2)   | w3 zero the upper blocks of X
 //   S2  w0 panel 2          | w1 X_11
 //   U2  update 2 (w0)       | w1 X_10
-//   S3  w0 panel 3          | w1 X_22
-//   I1  w0 X_33             | w1 X_21 | w2 X_20
-//   I2  w0 X_32             | w1 X_31 | w2 X_30
+//   S3  w0 panel 3          | w1 X_22, X_21 | w2 T_20 = L_20 X_00 + L_21 X_10,
+//                                             T_30 = L_30 X_00 + L_31 X_10 | w3 T_31 = L_31 X_11
+//   I1  w0 X_33             | w1 Y_32 = L_32 X_22 | w2 X_20 = -X_22 T_20 | w3 Y_31 = T_31 + L_32 X_21
+//   I2  w0 X_32 = -X_33 Y_32 | w1 X_31 = -X_33 Y_31 | w2 X_30 = -X_33 (T_30 + L_32 X_20)
+// (the sums over the already final blocks run beside panel 3; T / Y live in
+// four of X's upper blocks, zeroed again by the wave that reads them last).
 // Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0) {
@@ -507,20 +521,67 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
   if (w == 0) panel_update<2>(sF, 0, 1);
   else if (w == 1) inv_offdiag_block(sF, sX, 1, 0, lane);
   __syncthreads();
+  auto L_ = [&](int bi, int bj) { return sF + 16 * bi * LDT + 16 * bj; };
+  auto X_ = [&](int bi, int bj) { return sX + 16 * bi * LDT + 16 * bj; };
+  // scratch: T_20 -> X(0,1), T_30 -> X(0,2), T_31 / Y_31 -> X(0,3), Y_32 -> X(1,2)
+  auto S_ = [&](int bi, int bj) {
+    const int q = (bi == 2) ? 1 : (bj == 0 ? 2 : (bj == 1 ? 3 : 6));
+    return sX + 16 * (q >> 2) * LDT + 16 * (q & 3);
+  };
+  const doublex4 zero4 = {0.0, 0.0, 0.0, 0.0};
   if (w == 0) {
     panel_factor<3>(sF, col, lane, bad);
     if (bad && lane == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
   } else if (w == 1) {
     inv_diag_block(sF, sX, col, 2, lane);
+    inv_offdiag_block(sF, sX, 2, 1, lane);
+  } else if (w == 2) {
+    doublex4 t = {0.0, 0.0, 0.0, 0.0};
+    blk_mma<false>(t, L_(2, 0), X_(0, 0), 1.0);
+    blk_mma<false>(t, L_(2, 1), X_(1, 0), 1.0);
+    blk_store(S_(2, 0), t);
+    t = doublex4{0.0, 0.0, 0.0, 0.0};
+    blk_mma<false>(t, L_(3, 0), X_(0, 0), 1.0);
+    blk_mma<false>(t, L_(3, 1), X_(1, 0), 1.0);
+    blk_store(S_(3, 0), t);
+  } else {
+    doublex4 t = {0.0, 0.0, 0.0, 0.0};
+    blk_mma<false>(t, L_(3, 1), X_(1, 1), 1.0);
+    blk_store(S_(3, 1), t);
   }
   __syncthreads();
   STAMP(js, 5);
-  if (w == 0) inv_diag_block(sF, sX, col, 3, lane);
-  else if (w == 1) inv_offdiag_block(sF, sX, 2, 1, lane);
-  else if (w == 2) inv_offdiag_block(sF, sX, 2, 0, lane);
+  if (w == 0) {
+    inv_diag_block(sF, sX, col, 3, lane);
+  } else if (w == 1) {
+    doublex4 y = {0.0, 0.0, 0.0, 0.0};
+    blk_mma<false>(y, L_(3, 2), X_(2, 2), 1.0);
+    blk_store(S_(3, 2), y);
+  } else if (w == 2) {
+    const doublex4 t = blk_load(S_(2, 0));
+    blk_store(S_(2, 0), zero4);
+    blk_store(X_(2, 0), neg_x_times(X_(2, 2), t, lane));
+  } else {
+    doublex4 y = blk_load(S_(3, 1));
+    blk_mma<false>(y, L_(3, 2), X_(2, 1), 1.0);
+    blk_store(S_(3, 1), y);
+  }
   __syncthreads();
   STAMP(js, 13);
-  if (w < 3) inv_offdiag_block(sF, sX, 3, 2 - w, lane);
+  if (w == 0) {
+    const doublex4 y = blk_load(S_(3, 2));
+    blk_store(S_(3, 2), zero4);
+    blk_store(X_(3, 2), neg_x_times(X_(3, 3), y, lane));
+  } else if (w == 1) {
+    const doublex4 y = blk_load(S_(3, 1));
+    blk_store(S_(3, 1), zero4);
+    blk_store(X_(3, 1), neg_x_times(X_(3, 3), y, lane));
+  } else if (w == 2) {
+    doublex4 y = blk_load(S_(3, 0));
+    blk_store(S_(3, 0), zero4);
+    blk_mma<false>(y, L_(3, 2), X_(2, 0), 1.0);
+    blk_store(X_(3, 0), neg_x_times(X_(3, 3), y, lane));
+  }
   __syncthreads();
 }
 
