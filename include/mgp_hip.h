@@ -93,6 +93,16 @@ int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M, int32_t D
                         const int32_t* n_ls, float jitter, int32_t batch, float* L,
                         float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                         void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+/* Same; prep_done (a hipEvent_t, nullable) is recorded on the stream once Kuu
+ * is built and its first diagonal tile factored, so a caller can start work
+ * that is independent of the factorisation (K1, the q_sqrt images) on another
+ * stream then rather than beside the build (which it would starve). */
+int mgp_kuu_potrf_trtri_ev(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                           const float* const* variance, const float* const* lengthscales,
+                           const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                           float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                           void* workspace, size_t workspace_bytes, void* prep_done,
+                           mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K4
  * Whitened projection A = L^-1 Kuf (as the triangular GEMM LinvT^T . Kuf) plus

@@ -86,6 +86,21 @@ __device__ __forceinline__ double input_elem(const CholArgs& a, int b, int64_t g
   return v;
 }
 
+// Kuu element (gr, gc) of batch entry b from Z with the inverse lengthscales sil
+// (float64, precomputed once per workgroup: no division per element).
+__device__ __forceinline__ double kuu_elem(const CholArgs& a, const float* __restrict__ Z,
+                                           const double* __restrict__ sil, double var, int64_t gr, int64_t gc) {
+  if (gr >= a.M || gc >= a.M) return gr == gc ? 1.0 : 0.0;
+  double s = 0.0;
+  for (int d = 0; d < a.D; ++d) {
+    const double diff = ((double)Z[gr * a.ldz + d] - (double)Z[gc * a.ldz + d]) * sil[d];
+    s = fma(diff, diff, s);
+  }
+  double v = var * exp(-0.5 * s);
+  if (gr == gc) v += a.jitter;
+  return v;
+}
+
 // 64x64 f64 tile (row-major, ld) staged through registers: fetch issues all
 // eight 16-B loads per thread before any LDS store, so several tiles' loads
 // can be in flight together (fetch, fetch, ..., put, put).
@@ -596,12 +611,28 @@ __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, cons
 // ------------------------------------------------------------------ prep launch
 __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   __shared__ double s1[CB * LDT], s2[CB * LDT], col[CB];
+  __shared__ double sil[32];
   const int b = blockIdx.y;
+  const float* Zb = a.Z[0];
+  double varb = 0.0;
+  if (!a.A) {  // Kuu from Z: select this batch entry (no dynamic indexing of the argument arrays)
+    const float *ls = a.ls[0], *var = a.var[0];
+    int nls = a.n_ls[0];
+#pragma unroll
+    for (int i = 1; i < kMaxBatch; ++i)
+      if (b == i) { Zb = a.Z[i]; ls = a.ls[i]; var = a.var[i]; nls = a.n_ls[i]; }
+    if (threadIdx.x < a.D) sil[threadIdx.x] = 1.0 / (double)ls[nls == 1 ? 0 : threadIdx.x];
+    varb = (double)var[0];
+    __syncthreads();
+  }
+  auto elem = [&](int64_t gr, int64_t gc) {
+    return a.A ? input_elem(a, b, gr, gc) : kuu_elem(a, Zb, sil, varb, gr, gc);
+  };
   if (blockIdx.x == 0) {  // factor tile (0, 0) straight from the input (dispatched first)
     if (threadIdx.x == 0) a.info[b] = 0;
     for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
       const int r = idx >> 6, c = idx & 63;
-      s1[r * LDT + c] = input_elem(a, b, r, c);
+      s1[r * LDT + c] = elem(r, c);
     }
     __syncthreads();
     factor_diag_tile(s1, s2, col, a.info + b, 0);
@@ -615,7 +646,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     double* W = ws_W(a, b) + r0 * a.Mp + c0;
     for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
       const int r = idx >> 6, c = idx & 63;
-      W[(int64_t)r * a.Mp + c] = input_elem(a, b, r0 + r, c0 + c);
+      W[(int64_t)r * a.Mp + c] = elem(r0 + r, c0 + c);
     }
   }
   // zero L above / LinvT below the block diagonal (within M x M)
@@ -863,7 +894,8 @@ extern "C" size_t mgp_chol_workspace_bytes(int64_t M, int32_t batch) {
   return (size_t)chol_ws_doubles_per_batch(M) * (size_t)batch * sizeof(double);
 }
 
-static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s) {
+static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s,
+                    hipEvent_t prep_done = nullptr) {
   if (!workspace || workspace_bytes < mgp_chol_workspace_bytes(a.M, batch)) return MGP_ERR_WORKSPACE;
   if (!aligned16(workspace)) return MGP_ERR_ALIGN;
   a.Mp = chol_mp(a.M);
@@ -874,6 +906,10 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
   hipLaunchKernelGGL(chol_prep, dim3(a.nb * a.nb + 1, batch), block, 0, s, a);
   int st = launch_status();
   if (st) return st;
+  if (prep_done) {
+    st = hip_status(hipEventRecord(prep_done, s));
+    if (st) return st;
+  }
   for (int j = 0; j < a.nb; ++j) {
     const int T = a.nb - j - 1;
     const int n = (T == 0) ? a.nb : T * (T + 1) / 2 + T * (j + 1);
@@ -904,11 +940,12 @@ extern "C" int mgp_potrf_trtri(const float* A, int64_t lda, int64_t strideA, int
   return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
-extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+static int kuu_potrf_trtri_impl(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
                                    const float* const* variance, const float* const* lengthscales,
                                    const int32_t* n_ls, float jitter, int32_t batch, float* L,
                                    float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
-                                   void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+                                   void* workspace, size_t workspace_bytes, hipEvent_t prep_done,
+                                mgp_stream_t stream) {
   if (!Z) return -1;
   if (ldz < D) return -2;
   if (M < 0) return -3;
@@ -932,7 +969,26 @@ extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M
   a.ldz = ldz; a.D = D; a.jitter = (double)jitter;
   a.L = L; a.LinvT = LinvT; a.ldl = ldl; a.strideL = strideL;
   a.info = info; a.M = M;
-  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream);
+  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream, prep_done);
+}
+
+extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                                   const float* const* variance, const float* const* lengthscales,
+                                   const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                                   float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                                   void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
+                              info, workspace, workspace_bytes, nullptr, stream);
+}
+
+extern "C" int mgp_kuu_potrf_trtri_ev(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                                      const float* const* variance, const float* const* lengthscales,
+                                      const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                                      float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                                      void* workspace, size_t workspace_bytes, void* prep_done,
+                                      mgp_stream_t stream) {
+  return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
+                              info, workspace, workspace_bytes, (hipEvent_t)prep_done, stream);
 }
 
 extern "C" size_t mgp_chol_backward_workspace_bytes(int64_t M) {

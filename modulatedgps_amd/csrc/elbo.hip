@@ -462,6 +462,9 @@ __global__ __launch_bounds__(256) void kl_partials_kernel(const float* __restric
                                                           int64_t ldqs, int64_t strideq, int64_t M,
                                                           int K, int nRowBlocks,
                                                           double* __restrict__ partials) {
+  // one block: kKlRows rows of one L_k; each thread owns 4 consecutive columns
+  // of every row (float4 loads of all the block's rows issued before any use:
+  // the rows were a serial chain of load latencies), masked to the lower triangle
   __shared__ double scratch[16];
   const int blk = blockIdx.x;
   float tr = 0.f, ld = 0.f, mh = 0.f;
@@ -469,19 +472,32 @@ __global__ __launch_bounds__(256) void kl_partials_kernel(const float* __restric
     const int k = blk / nRowBlocks;
     const int64_t r0 = (int64_t)(blk % nRowBlocks) * kKlRows;
     const float* L = q_sqrt + (int64_t)k * strideq;
-    for (int64_t i = r0; i < r0 + kKlRows && i < M; ++i) {
-      const float* row = L + i * ldqs;
-      for (int64_t j = threadIdx.x; j <= i; j += blockDim.x) {
-        const float v = row[j];
-        tr = fmaf(v, v, tr);
-        if (j == i) ld += logf(v * v);
+    const int64_t rmax = min<int64_t>(r0 + kKlRows, M) - 1;  // last row of the block
+    for (int64_t c0 = 4 * (int64_t)threadIdx.x; c0 <= rmax; c0 += 4 * (int64_t)blockDim.x) {
+      floatx4 v[kKlRows];
+#pragma unroll
+      for (int r = 0; r < kKlRows; ++r) {
+        const int64_t i = r0 + r;
+        v[r] = (i <= rmax && c0 <= i) ? *reinterpret_cast<const floatx4*>(L + i * ldqs + c0)
+                                      : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int r = 0; r < kKlRows; ++r) {
+        const int64_t i = r0 + r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = (c0 + e <= i) ? v[r][e] : 0.f;
+          tr = fmaf(x, x, tr);
+          if (c0 + e == i && i <= rmax) ld += logf(x * x);
+        }
       }
     }
   } else {  // the last block: Mahalanobis term sum q_mu^2
-    for (int64_t idx = threadIdx.x; idx < M * K; idx += blockDim.x) {
-      const float v = q_mu[(idx / K) * ldq + (idx % K)];
-      mh = fmaf(v, v, mh);
-    }
+    for (int64_t m = threadIdx.x; m < M; m += blockDim.x)
+      for (int k = 0; k < K; ++k) {
+        const float v = q_mu[m * ldq + k];
+        mh = fmaf(v, v, mh);
+      }
   }
   const double a = block_sum<double>((double)tr, scratch);
   const double b = block_sum<double>((double)ld, scratch);
@@ -936,6 +952,7 @@ extern "C" int mgp_gauss_kl_white(const float* q_mu, int64_t ldq, const float* q
   if (M < 1) return -6;
   if (K < 1) return -7;
   if (!kl_out) return -8;
+  if ((ldqs & 3) || (strideq & 3) || !aligned16(q_sqrt)) return MGP_ERR_ALIGN;  // float4 rows
   if (!workspace || workspace_bytes < mgp_kl_workspace_bytes(M, K)) return MGP_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   const int nrb = kl_row_blocks(M);

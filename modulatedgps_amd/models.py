@@ -210,11 +210,12 @@ class SVGPModified:
         Afr, stats = self.x6_trsm(X.shape[0], LinvT, Kfr, bufs, timing, fmt)
         return self.x6_expert(X.shape[0], Afr, Lfr, stats, bufs, timing, fmt)
 
-    def x6_trsm(self, N, LinvT, Kfr, bufs, timing=None, fmt="x6"):
+    def x6_trsm(self, N, LinvT, Kfr, bufs, timing=None, fmt="x6", Tfr=None):
         """K4 on images: A's image (split-f16 when fmt == "f16") and the column
-        statistics (x6 mode)."""
-        with _Stage(timing, "split_tri"):
-            Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"), fmt=fmt)
+        statistics (x6 mode).  Tfr: L^-T's image if already split."""
+        if Tfr is None:
+            with _Stage(timing, "split_tri"):
+                Tfr = ops.split_upper_x6(LinvT, out=bufs.get("Tfr"), fmt=fmt)
         with _Stage(timing, "trsm_stats"):
             return ops.trsm_stats_x6(Tfr, Kfr, self.q_mu, self.num_inducing, N, Afr=bufs.get("Afr"),
                                      stats=bufs.get("stats"), A=bufs.get("A32"),
@@ -390,9 +391,10 @@ class SMGP(SGP):
         self._bufs[key] = b
         return b
 
-    def _factorise(self, b):
+    def _factorise(self, b, prep_event=None):
         """Kuu of both layers and their batched Cholesky + inverse (one K3 sweep).
-        Training buffers also keep L (b["L_f"], b["L_a"]) for the backward pass."""
+        Training buffers also keep L (b["L_f"], b["L_a"]) for the backward pass.
+        prep_event: recorded once Kuu is built (batched path only; else after K3)."""
         pf, pa = self.pred_layer, self.assign_layer
         train = b.get("train", False)
         if "LinvT2" in b:
@@ -402,7 +404,7 @@ class SMGP(SGP):
             Lo, LinvT, info = ops.kuu_potrf_trtri(
                 [pf.Z, pa.Z], [pf.kernel.variance, pa.kernel.variance],
                 [pf.kernel.lengthscales, pa.kernel.lengthscales], default_jitter(), LinvT=b["LinvT2"],
-                L=b.get("L2"), want_L=train)
+                L=b.get("L2"), want_L=train, prep_event=prep_event)
             self.last_info = info
             if train:
                 b["L_f"], b["L_a"] = Lo[0], Lo[1]
@@ -418,7 +420,16 @@ class SMGP(SGP):
                 b["L_" + name] = Lo[0]
             b["LinvT_" + name] = LinvT[0]
         self.last_info = torch.cat(infos)
+        if prep_event is not None:
+            prep_event.record()
         return outs[0], outs[1]
+
+    def _prep_event(self):
+        """The K3 prep-done event (created once: its handle is passed to the C-ABI)."""
+        if getattr(self, "_prep_ev", None) is None:
+            self._prep_ev = torch.cuda.Event()
+            self._prep_ev.record()   # creates the underlying hipEvent_t
+        return self._prep_ev
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
@@ -430,17 +441,30 @@ class SMGP(SGP):
 
         x6 mode: K1 and the tril(q_sqrt) images of both layers (and, when kl_out
         is given, both KL terms) run on a side stream concurrently with the
-        latency-bound K3 sweep, which occupies only a few CUs."""
+        latency-bound K3 sweep, which occupies only a few CUs.  They start once
+        K3 has built Kuu (its prep event): launched beside the build, K1's 4096
+        workgroups starve it (101 us instead of ~20)."""
         X = self.pred_layer.kernel._x(X)
         N = X.shape[0]
         b = self._buffers(N, train)
         layers = (("f", self.pred_layer), ("a", self.assign_layer))
         images = {}
         fmt = forward_image_format(train)
+        prep = None
         if b["x6"]:
             main = torch.cuda.current_stream(self.device)
             side = self._side_stream()
-            side.wait_stream(main)
+            prep = self._prep_event()
+        with _Stage(timing, "kuu_chol"):
+            LinvT_f, LinvT_a = self._factorise(b, prep_event=prep)
+        Tfr = {}
+        if b["x6"] and "Tfr_a" in b:
+            # L^-T images straight after K3 on its stream (no cross-stream wait in front)
+            with _Stage(timing, "split_tri"):
+                for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
+                    Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt)
+        if b["x6"]:
+            side.wait_event(prep)   # after Kuu's build (and so after everything before K3 on main)
             with torch.cuda.stream(side):
                 for L, layer in layers:
                     images[L] = layer.operand_images(X, {"Kfr": b["Kfr_" + L], "Lfr": b["Lfr_" + L]},
@@ -449,9 +473,6 @@ class SMGP(SGP):
                     with _Stage(timing, "gauss_kl"):
                         self.pred_layer.prior_kl(out=kl_out[0:1])
                         self.assign_layer.prior_kl(out=kl_out[1:2])
-        with _Stage(timing, "kuu_chol"):
-            LinvT_f, LinvT_a = self._factorise(b)
-        if b["x6"]:
             main.wait_stream(side)
         LinvT = {"f": LinvT_f, "a": LinvT_a}
         bufs = {L: {"Kuf": b["Kuf_" + L], "A": b["A_" + L], "stats": b["stats_" + L],
@@ -464,8 +485,8 @@ class SMGP(SGP):
             pf, pa = self.pred_layer, self.assign_layer
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt)
-            Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing, fmt)
+                Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt, Tfr=Tfr["a"])
+            Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing, fmt, Tfr=Tfr["f"])
             pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
             main.wait_stream(side)
             pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)

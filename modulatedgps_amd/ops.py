@@ -123,10 +123,11 @@ def potrf_trtri(A, L=None, LinvT=None, info=None, workspace=None):
 
 
 def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, info=None,
-                    workspace=None, want_L=False):
+                    workspace=None, want_L=False, prep_event=None):
     """Kuu (float64, from Z) + Cholesky + inverse for a batch of layers sharing M, D.
     Zs / variances / lengthscales: lists of device tensors.  Returns L (or None),
-    LinvT [B, M, M] and info int32 [B]."""
+    LinvT [B, M, M] and info int32 [B].  prep_event: a torch.cuda.Event (already
+    created) recorded once Kuu is built (mgp_kuu_potrf_trtri_ev)."""
     import ctypes
     Bt = len(Zs)
     M, D = Zs[0].shape
@@ -150,9 +151,15 @@ def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, inf
     vp = P(*[v.data_ptr() for v in variances])
     lp = P(*[l.data_ptr() for l in lengthscales])
     nl = (ctypes.c_int32 * Bt)(*[l.numel() for l in lengthscales])
-    _lib.call("mgp_kuu_potrf_trtri", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
-              L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
-              LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(), _stream())
+    if prep_event is not None:
+        _lib.call("mgp_kuu_potrf_trtri_ev", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
+                  L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
+                  LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(),
+                  prep_event.cuda_event, _stream())
+    else:
+        _lib.call("mgp_kuu_potrf_trtri", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
+                  L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
+                  LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(), _stream())
     return L, LinvT, info
 
 
@@ -557,6 +564,7 @@ def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None
 def gauss_kl_white(q_mu, q_sqrt, out=None, workspace=None):
     """Whitened KL (models.py:79) as a float64 device tensor of shape [1]."""
     _check(q_mu, "q_mu", 2), _check(q_sqrt, "q_sqrt", 3)
+    q_sqrt = as_padded(q_sqrt)  # float4 rows (no copy for the layers' padded storage)
     M, K = q_mu.shape
     dev = q_mu.device
     if out is None:
