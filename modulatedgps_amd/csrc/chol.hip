@@ -367,6 +367,17 @@ __device__ __forceinline__ void diag_lower_update(double* __restrict__ s, const 
   }
 }
 
+// s[R0 .. R0+15][C1 .. C1+15] -= sum over 16 NK columns k of sa[R0 + i][k] sb[C1 + j][k]
+// (one wave, f64 MFMA; rows of sa / sb at leading dimension LDT).
+template <int NK>
+__device__ __forceinline__ void sub_outer_blk(double* __restrict__ s, int R0, int C1, const double* __restrict__ sa,
+                                              const double* __restrict__ sb) {
+  doublex4 acc = blk_load(s + R0 * LDT + C1);
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) blk_mma<true>(acc, sa + R0 * LDT + 16 * kk, sb + C1 * LDT + 16 * kk, -1.0);
+  blk_store(s + R0 * LDT + C1, acc);
+}
+
 // Panel P (columns 16P..16P+15) of the diagonal tile, wave 0: lane r keeps the
 // 16 panel entries of row r; right-looking sweep whose column broadcasts are
 // readlanes from the owning lanes (no LDS round trip on the critical path).
@@ -491,12 +502,15 @@ __device__ __forceinline__ doublex4 neg_x_times(const double* __restrict__ Xii, 
 // update to the trailing blocks on the f64 MFMA.  The inverse is built by the
 // idle waves while wave 0 runs the next panel: X_pp = L_pp^-1 as soon as panel
 // p is final, X_ij (i > j) = -X_ii sum_k L_ik X_kj as soon as its operands are:
-//   S0  w0 panel 0
-//   U0  update 0 (6 blocks, 4 waves)
-//   S1  w0 panel 1          | w1 X_00
-//   U1  update 1 (w0..w2)   | w3 zero the upper blocks of X
-//   S2  w0 panel 2          | w1 X_11
+//   S0  w0 panel 0          | w1..w3 the caller's pending P P^T update of the
+//                             blocks right of column block 0 (sPend, look-ahead)
+//   U0  update 0 of column block 1 (w0..w2) | w3 zero the upper blocks of X
+//   S1  w0 panel 1          | w1 X_00 | w2, w3 update 0 of blocks (2,2), (3,2), (3,3)
+//   U1  update 1 of column block 2 (w0, w1)
+//   S2  w0 panel 2          | w1 X_11 | w2 update 1 of block (3,3)
 //   U2  update 2 (w0)       | w1 X_10
+// (a trailing update runs on the critical path only for the column block the
+// next panel sweeps; the rest runs beside that sweep)
 //   S3  w0 panel 3          | w1 X_22, X_21 | w2 T_20 = L_20 X_00 + L_21 X_10,
 //                                             T_30 = L_30 X_00 + L_31 X_10 | w3 T_31 = L_31 X_11
 //   I1  w0 X_33             | w1 Y_32 = L_32 X_22 | w2 X_20 = -X_22 T_20 | w3 Y_31 = T_31 + L_32 X_21
@@ -504,23 +518,27 @@ __device__ __forceinline__ doublex4 neg_x_times(const double* __restrict__ Xii, 
 // (the sums over the already final blocks run beside panel 3; T / Y live in
 // four of X's upper blocks, zeroed again by the wave that reads them last).
 // Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
-__device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* __restrict__ sX,
-                                                 double* __restrict__ col, int32_t* info, int64_t gcol0) {
+// sPend (optional, may alias sX): the caller's pending update sF -= sPend sPend^T
+// of the lower blocks right of column block 0 (column block 0 already applied).
+__device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* sX,
+                                                 double* __restrict__ col, int32_t* info, int64_t gcol0,
+                                                 const double* sPend = nullptr) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int bad = 0;
   const int js = (int)(gcol0 / CB) - 1;
-  if (w == 0) panel_factor<0>(sF, col, lane, bad);
+  if (w == 0) {
+    panel_factor<0>(sF, col, lane, bad);
+  } else if (sPend) {  // blocks (1,1), (2,1) | (3,1), (2,2) | (3,2), (3,3)
+    const int bi0 = (w == 1) ? 1 : 3, bj0 = (w == 3) ? 2 : 1;
+    const int bi1 = (w == 3) ? 3 : 2, bj1 = (w == 1) ? 1 : (w == 2 ? 2 : 3);
+    sub_outer_blk<4>(sF, 16 * bi0, 16 * bj0, sPend, sPend);
+    sub_outer_blk<4>(sF, 16 * bi1, 16 * bj1, sPend, sPend);
+  }
   STAMP(js, 8);
   __syncthreads();
-  panel_update<0>(sF, w);
-  __syncthreads();
-  STAMP(js, 9);
-  if (w == 0) panel_factor<1>(sF, col, lane, bad);
-  else if (w == 1) inv_diag_block(sF, sX, col, 0, lane);
-  STAMP(js, 10);
-  __syncthreads();
+  const double* P0 = sF;  // panel p's L columns: sF + 16 p
   if (w < 3) {
-    panel_update<1>(sF, w, 3);
+    sub_outer_blk<1>(sF, 16 * (w + 1), 16, P0, P0);  // update 0 of (1,1), (2,1), (3,1)
   } else {
     for (int q = 0; q < 6; ++q) {  // upper blocks (i < j) of X are zero
       const int i = q < 3 ? 0 : (q < 5 ? 1 : 2), j = q < 3 ? q + 1 : (q < 5 ? q - 1 : 3);
@@ -528,9 +546,25 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     }
   }
   __syncthreads();
+  STAMP(js, 9);
+  if (w == 0) {
+    panel_factor<1>(sF, col, lane, bad);
+  } else if (w == 1) {
+    inv_diag_block(sF, sX, col, 0, lane);
+  } else if (w == 2) {
+    sub_outer_blk<1>(sF, 32, 32, P0, P0);  // update 0 of (2,2), (3,2)
+    sub_outer_blk<1>(sF, 48, 32, P0, P0);
+  } else {
+    sub_outer_blk<1>(sF, 48, 48, P0, P0);  // update 0 of (3,3)
+  }
+  STAMP(js, 10);
+  __syncthreads();
+  if (w < 2) sub_outer_blk<1>(sF, 32 + 16 * w, 32, sF + 16, sF + 16);  // update 1 of (2,2), (3,2)
+  __syncthreads();
   STAMP(js, 11);
   if (w == 0) panel_factor<2>(sF, col, lane, bad);
   else if (w == 1) inv_diag_block(sF, sX, col, 1, lane);
+  else if (w == 2) sub_outer_blk<1>(sF, 48, 48, sF + 16, sF + 16);  // update 1 of (3,3)
   STAMP(js, 12);
   __syncthreads();
   if (w == 0) panel_update<2>(sF, 0, 1);
@@ -601,11 +635,30 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
 }
 
 // Write the factored diagonal tile j: L block (f32, guarded to M; optional) and D_j (f64).
+// Full tiles with 16-B stores (ld of L is a multiple of 4, tile origins 64-aligned).
 __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, const double* sF, const double* sX) {
   const int64_t g0 = (int64_t)j * CB;
   const int nr = (int)min<int64_t>(CB, a.M - g0);
-  if (a.L) tile_store_f32(a.L + (int64_t)b * a.strideL + g0 * a.ldl + g0, a.ldl, sF, false, nr, nr);
-  tile_store_f64(ws_D(a, b, j), CB, sX);
+  if (a.L) {
+    float* g = a.L + (int64_t)b * a.strideL + g0 * a.ldl + g0;
+    if (nr == CB) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int idx = threadIdx.x + kCholThreads * it, r = idx >> 4, c = (idx & 15) * 4;
+        const double* sr = sF + r * LDT + c;
+        *reinterpret_cast<float4*>(g + (int64_t)r * a.ldl + c) =
+            make_float4((float)sr[0], (float)sr[1], (float)sr[2], (float)sr[3]);
+      }
+    } else {
+      tile_store_f32(g, a.ldl, sF, false, nr, nr);
+    }
+  }
+  double* d = ws_D(a, b, j);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
+    *reinterpret_cast<double2*>(d + r * CB + c) = make_double2(sX[r * LDT + c], sX[r * LDT + c + 1]);
+  }
 }
 
 // ------------------------------------------------------------------ prep launch
@@ -723,7 +776,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     if (l != i) blk4_to_lds<true>(s2, pl);
     __syncthreads();
     if (la) STAMP(j, 2);
-    if (l == i && a.L) {
+    if (l == i && !la && a.L) {  // L_ij (the look-ahead's L_{j+1,j}: by forward-substitution tile (j+1, j))
       const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
       tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
                      (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
@@ -733,19 +786,22 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
       row_to_global(Wt(i, l), Mp, u);
       return;
     }
-    // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T in place in LDS (s2)
-    diag_lower_update(s2, s1);
     if (la) {  // look-ahead: factor the next diagonal tile
+      // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
+      // lower blocks are applied beside the first panel sweep
+      sub_outer_blk<4>(s2, 16 * (threadIdx.x >> 6), 0, s1, s1);
       __syncthreads();
       STAMP(j, 3);
       STAMP(j, 4);
-      factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB);
+      factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1);
       STAMP(j, 6);
       __syncthreads();
       write_diag(a, b, j + 1, s2, s1);
       __syncthreads();
       STAMP(j, 7);
     } else {
+      // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T in place in LDS (s2)
+      diag_lower_update(s2, s1);
       __syncthreads();
       tile_store_f64(Wt(i, l), Mp, s2);
     }
@@ -774,6 +830,11 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   blk4_to_lds<true>(s1, pi);
   if (c < j) blk4_to_lds<false>(s2, xq);
   __syncthreads();
+  if (i == j + 1 && c == j && a.L) {                   // L_{j+1,j} (off the look-ahead's chain)
+    const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
+    tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
+                   (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
+  }
   if (c < j) {
     if (i == j + 1) store_linvT(c, s2);
     row_mma<false, 0>(u, s1, s2, -1.0);                // B_ic -= P_i X_jc

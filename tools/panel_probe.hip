@@ -1,0 +1,342 @@
+// K3 panel-sweep probe: cycles of one 64 x 16 panel factorisation (wave 0 of a
+// 64-thread workgroup) for variants of the sweep, stamped with sched-barrier
+// fenced s_memtime.  Build and run on the GPU box:
+//   hipcc -O3 --offload-arch=gfx950 -I include -I modulatedgps_amd/csrc -o tools/panel_probe tools/panel_probe.hip
+//   tools/panel_probe
+#include "../modulatedgps_amd/csrc/chol.hip"
+
+namespace probe {
+using namespace mgp;
+
+__device__ __forceinline__ double rcp_f64_chain(double p) {
+  const double r = __builtin_amdgcn_rcp(p);
+  return fma(r, fma(-p, r, 1.0), r);
+}
+__device__ __forceinline__ double rsqrt1_f64(double p) {
+  const double r = __builtin_amdgcn_rsq(p);
+  return r * fma(-0.5 * p * r, r, 1.5);
+}
+
+// LDS-broadcast sweep with an rcp pivot chain (measured slower than the kernel's readlane sweep)
+__device__ void lds_sweep(double* sF, double* col, double* sb, int r, int& bad) {
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  double rs[16], pv[16];
+  double vcur[16], vnext[16];
+  int zb;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zb));
+  const double* sbz = sb + zb;
+  sb[r] = a[0];
+#pragma unroll
+  for (int s2 = 2; s2 < 16; ++s2) vcur[s2] = sbz[s2];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double piv = read_lane_f64(a[c], c);
+    pv[c] = piv;
+    rs[c] = rsqrt1_f64(piv);
+    if (c + 1 < 16) {
+      const double v1 = read_lane_f64(a[c], c + 1);
+      const double t = a[c] * rcp_f64_chain(piv);
+      a[c + 1] = fma(-t, v1, a[c + 1]);
+      if (c + 2 < 16) {
+        sb[((c + 1) & 1) * CB + r] = a[c + 1];
+#pragma unroll
+        for (int s2 = c + 3; s2 < 16; ++s2) vnext[s2] = sbz[((c + 1) & 1) * CB + s2];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, vcur[s2], a[s2]);
+#pragma unroll
+      for (int s2 = c + 3; s2 < 16; ++s2) vcur[s2] = vnext[s2];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) if (!(pv[c] > 0.0) && bad == 0) bad = c + 1;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+}
+
+__device__ __forceinline__ unsigned long long stamp() {
+  __builtin_amdgcn_sched_barrier(0);
+  unsigned long long t;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// chain only: the pivot recurrence without the off-chain trailing updates
+__device__ void chain_only(double* sF, double* col, int r, int& bad) {
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+#pragma unroll
+  for (int c = 0; c < 15; ++c) {
+    const double piv = read_lane_f64(a[c], c);
+    const double v1 = read_lane_f64(a[c], c + 1);
+    const double t = a[c] * rcp_f64_chain(piv);
+    a[c + 1] = fma(-t, v1, a[c + 1]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = a[c];
+}
+
+// trailing updates only: fixed t, LDS broadcast as in panel_factor
+__device__ void updates_only(double* sF, double* sb, int r) {
+  double a[16], vcur[16], vnext[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  int zb;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zb));
+  const double* sbz = sb + zb;
+  sb[r] = a[0];
+#pragma unroll
+  for (int s2 = 2; s2 < 16; ++s2) vcur[s2] = sbz[s2];
+#pragma unroll
+  for (int c = 0; c < 15; ++c) {
+    const double t = a[c] * 0.01;
+    if (c + 2 < 16) {
+      sb[((c + 1) & 1) * CB + r] = a[c + 1];
+#pragma unroll
+      for (int s2 = c + 3; s2 < 16; ++s2) vnext[s2] = sbz[((c + 1) & 1) * CB + s2];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, vcur[s2], a[s2]);
+#pragma unroll
+    for (int s2 = c + 3; s2 < 16; ++s2) vcur[s2] = vnext[s2];
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = a[c];
+}
+
+// previous sweep: all broadcasts by readlane, rsq + two Newton steps on the chain
+__device__ void readlane_sweep(double* sF, double* col, int r, int& bad) {
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  double rs[16];
+  double piv = read_lane_f64(a[0], 0);
+  rs[0] = rsqrt_f64(piv);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    double v[16];
+#pragma unroll
+    for (int s2 = c + 1; s2 < 16; ++s2) v[s2] = read_lane_f64(a[c], s2);
+    const double t = a[c] * (rs[c] * rs[c]);
+    if (c + 1 < 16) {
+      a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+      piv = read_lane_f64(a[c + 1], c + 1);
+      rs[c + 1] = rsqrt_f64(piv);
+    }
+#pragma unroll
+    for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+}
+
+
+// V2: readlane broadcasts, rcp chain, rs (one Newton) per column, bad deferred
+__device__ void rl_rcp(double* sF, double* col, int r, int& bad) {
+  double a[16], rs[16], pv[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double piv = read_lane_f64(a[c], c);
+    pv[c] = piv;
+    rs[c] = rsqrt1_f64(piv);
+    if (c + 1 < 16) {
+      double v[16];
+#pragma unroll
+      for (int s2 = c + 1; s2 < 16; ++s2) v[s2] = read_lane_f64(a[c], s2);
+      const double t = a[c] * rcp_f64_chain(piv);
+      a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) if (!(pv[c] > 0.0) && bad == 0) bad = c + 1;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+}
+
+// V5/V6: pipelined -- column c-1's deferred trailing updates are issued inside
+// column c's pivot chain (PIN: sched barriers between the groups)
+template <bool PIN>
+__device__ void rl_pipe(double* sF, double* col, int r, int& bad) {
+  double a[16], rs[16], pv[16], vp[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  double tp = 0.0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double piv = read_lane_f64(a[c], c);
+    const double v1 = (c + 1 < 16) ? read_lane_f64(a[c], c + 1) : 0.0;
+    if (PIN) __builtin_amdgcn_sched_barrier(0);
+    if (c >= 1) {   // deferred updates of column c - 1 (s >= c + 1; s = c + 1 first: the chain needs it)
+#pragma unroll
+      for (int s2 = c + 1; s2 < 16; ++s2) a[s2] = fma(-tp, vp[s2], a[s2]);
+    }
+    if (PIN) __builtin_amdgcn_sched_barrier(0);
+    pv[c] = piv;
+    if (c + 1 < 16) {
+      const double t = a[c] * rcp_f64_chain(piv);
+      a[c + 1] = fma(-t, v1, a[c + 1]);
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) vp[s2] = read_lane_f64(a[c], s2);
+      tp = t;
+    }
+    if (PIN) __builtin_amdgcn_sched_barrier(0);
+    rs[c] = rsqrt1_f64(piv);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) if (!(pv[c] > 0.0) && bad == 0) bad = c + 1;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+}
+
+
+// V7: one rsq (one Newton) per column: L = a rs on the chain, t = L rs
+template <bool PIPE>
+__device__ void rs1(double* sF, double* col, int r, int& bad) {
+  double a[16], pv[16], vp[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  double tp = 0.0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double piv = read_lane_f64(a[c], c);
+    pv[c] = piv;
+    const double r0 = __builtin_amdgcn_rsq(piv);
+    const double hp = 0.5 * piv;
+    double v[16];
+    if (!PIPE) {
+#pragma unroll
+      for (int s2 = c + 1; s2 < 16; ++s2) v[s2] = read_lane_f64(a[c], s2);
+    } else {
+      if (c + 1 < 16) v[c + 1] = read_lane_f64(a[c], c + 1);
+      if (c >= 1) {
+#pragma unroll
+        for (int s2 = c + 1; s2 < 16; ++s2) a[s2] = fma(-tp, vp[s2], a[s2]);
+      }
+    }
+    const double rs = r0 * fma(-hp * r0, r0, 1.5);
+    if (r == 0) col[c] = rs;
+    const double L = a[c] * rs;
+    a[c] = (r >= c) ? L : 0.0;
+    if (c + 1 < 16) {
+      const double t = L * rs;
+      a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+      if (!PIPE) {
+#pragma unroll
+        for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
+      } else {
+#pragma unroll
+        for (int s2 = c + 2; s2 < 16; ++s2) vp[s2] = read_lane_f64(a[c] * 0.0 + L / rs, s2);
+        tp = t;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) if (!(pv[c] > 0.0) && bad == 0) bad = c + 1;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = a[c];
+}
+
+
+// V8-V10: the previous readlane sweep with a cheaper pivot chain.
+// MODE 0: v_rsq_f64 + 1 Newton; 1: f32 rsq + 2 Newton (f64); 2: f32 rsq + 1 Newton
+template <int MODE>
+__device__ __forceinline__ double rsq_mode(double p) {
+  double r;
+  if (MODE == 0) r = __builtin_amdgcn_rsq(p);
+  else r = (double)__builtin_amdgcn_rsqf((float)p);
+  const double h = 0.5 * p;
+  r = r * fma(-h * r, r, 1.5);
+  if (MODE == 1) r = r * fma(-h * r, r, 1.5);
+  return r;
+}
+template <int MODE>
+__device__ void rl_mode(double* sF, double* col, int r, int& bad) {
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  double rs[16];
+  double piv = read_lane_f64(a[0], 0);
+  rs[0] = rsq_mode<MODE>(piv);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    double v[16];
+#pragma unroll
+    for (int s2 = c + 1; s2 < 16; ++s2) v[s2] = read_lane_f64(a[c], s2);
+    const double t = a[c] * (rs[c] * rs[c]);
+    if (c + 1 < 16) {
+      a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+      piv = read_lane_f64(a[c + 1], c + 1);
+      rs[c + 1] = rsq_mode<MODE>(piv);
+    }
+#pragma unroll
+    for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+}
+
+__global__ void run(const double* src, double* dst, unsigned long long* t, int variant) {
+  __shared__ double sF[CB * LDT], col[3 * CB];
+  const int r = threadIdx.x;
+  for (int j = 0; j < 64; ++j) sF[r * LDT + j] = src[r * 64 + j];
+  __syncthreads();
+  int bad = 0;
+  unsigned long long t0 = stamp();
+  if (variant == 0) lds_sweep(sF, col, col + CB, r, bad);
+  else if (variant == 1) readlane_sweep(sF, col, r, bad);
+  else if (variant == 2) chain_only(sF, col, r, bad);
+  else if (variant == 3) updates_only(sF, col + CB, r);
+  else if (variant == 4) rl_rcp(sF, col, r, bad);
+  else if (variant == 5) rl_pipe<true>(sF, col, r, bad);
+  else if (variant == 6) rl_pipe<false>(sF, col, r, bad);
+  else if (variant == 7) rs1<false>(sF, col, r, bad);
+  else if (variant == 8) rl_mode<0>(sF, col, r, bad);
+  else if (variant == 9) rl_mode<1>(sF, col, r, bad);
+  else rl_mode<2>(sF, col, r, bad);
+  unsigned long long t1 = stamp();
+  if (r == 0) t[variant] = t1 - t0;
+  __syncthreads();
+  for (int j = 0; j < 64; ++j) dst[r * 64 + j] = sF[r * LDT + j] + bad;
+}
+}  // namespace probe
+
+int main() {
+  double h[64 * 64];
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 64; ++j) h[i * 64 + j] = (i == j ? 64.0 : 0.0) + 1.0 / (1.0 + i + j);
+  double *src, *dst;
+  unsigned long long* t;
+  (void)hipMalloc(&src, sizeof(h));
+  (void)hipMalloc(&dst, sizeof(h));
+  (void)hipMalloc(&t, 16 * sizeof(unsigned long long));
+  (void)hipMemcpy(src, h, sizeof(h), hipMemcpyHostToDevice);
+  unsigned long long ht[16] = {0};
+  const char* names[11] = {"panel_factor (LDS broadcast, rcp chain)", "readlane sweep (kernel)", "chain only",
+                          "trailing updates only", "readlane + rcp chain", "pipelined, pinned", "pipelined", "rsq1 chain", "readlane, rsq f64 + 1 Newton", "readlane, rsq f32 + 2 Newton", "readlane, rsq f32 + 1 Newton"};
+  for (int rep = 0; rep < 3; ++rep)
+    for (int v = 0; v < 11; ++v) hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
+  (void)hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
+  // agreement of the variants' L panels
+  double ref[64 * 64], out[64 * 64];
+  for (int v = 0; v < 11; ++v) {
+    if (v == 2 || v == 3) continue;
+    hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
+    (void)hipMemcpy(v == 0 ? ref : out, dst, sizeof(ref), hipMemcpyDeviceToHost);
+    if (v == 0) continue;
+    double e = 0;
+    for (int i = 0; i < 64; ++i) for (int j = 0; j < 16; ++j) e = fmax(e, fabs(out[i * 64 + j] - ref[i * 64 + j]));
+    printf("variant %d max |diff| vs 0: %.3e\n", v, e);
+  }
+  for (int v = 0; v < 11; ++v) printf("%-42s %6llu cycles (%.0f per column)\n", names[v], ht[v], ht[v] / 16.0);
+  return 0;
+}
