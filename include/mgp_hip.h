@@ -103,6 +103,17 @@ int mgp_kuu_potrf_trtri_ev(const float* const* Z, int64_t ldz, int64_t M, int32_
                            float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                            void* workspace, size_t workspace_bytes, void* prep_done,
                            mgp_stream_t stream);
+/* Same; linvt_absmax (nullable host array of `batch` device floats, each
+ * nullable) receives max |(L^-1)^T| of that matrix, folded in while K3 writes
+ * the inverse (zeroed by the launch itself) -- the scale bound of the L^-T
+ * split-f16 image, so mgp_split_upper_f16_bounded needs no reduction pass
+ * (pass mgp_x6_bound_ptr(Tfr, M, 0, 1) to write it straight into the image). */
+int mgp_kuu_potrf_trtri_ex(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                           const float* const* variance, const float* const* lengthscales,
+                           const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                           float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                           void* workspace, size_t workspace_bytes, void* prep_done,
+                           float* const* linvt_absmax, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K4
  * Whitened projection A = L^-1 Kuf (as the triangular GEMM LinvT^T . Kuf) plus
@@ -215,6 +226,14 @@ int mgp_rbf_kuf_f16(const float* X, int64_t ldx, const float* Z, int64_t ldz, in
                     void* Kfr, size_t kfr_bytes, mgp_stream_t stream);
 int mgp_split_upper_f16(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, size_t tfr_bytes,
                         mgp_stream_t stream);
+/* mgp_split_upper_f16 whose image trailer already holds max |LinvT| (from
+ * mgp_kuu_potrf_trtri_ex): the split alone, no reduction launches. */
+int mgp_split_upper_f16_bounded(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, size_t tfr_bytes,
+                                mgp_stream_t stream);
+/* Device address of the split-f16 scale bound in an image's trailer: lower /
+ * upper triangular images of K matrices (K >= 1), or a column image (K = 0,
+ * N columns).  NULL for a NULL image or M <= 0. */
+float* mgp_x6_bound_ptr(void* img, int64_t M, int64_t N, int32_t K);
 int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,
                        int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
                        void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A, int64_t lda,

@@ -54,6 +54,9 @@ SIGNATURES = {
     "mgp_kuu_potrf_trtri_ev": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_ptr,
                                            ctypes.c_float, c_i32, c_ptr, c_ptr, c_i64, c_i64, c_ptr,
                                            c_ptr, c_size, c_ptr, c_ptr]),
+    "mgp_kuu_potrf_trtri_ex": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_ptr,
+                                           ctypes.c_float, c_i32, c_ptr, c_ptr, c_i64, c_i64, c_ptr,
+                                           c_ptr, c_size, c_ptr, c_ptr, c_ptr]),
     "mgp_stats_tiles": (ctypes.c_int, [c_i64]),
     "mgp_trsm_stats": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                       c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
@@ -117,6 +120,8 @@ SIGNATURES = {
     "mgp_rbf_kuf_f16": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i32,
                                        c_ptr, c_size, c_ptr]),
     "mgp_split_upper_f16": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_split_upper_f16_bounded": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_x6_bound_ptr": (ctypes.c_void_p, [c_ptr, c_i64, c_i64, c_i32]),
     "mgp_trsm_stats_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                           c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "mgp_trsm_stats_f16x8": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,

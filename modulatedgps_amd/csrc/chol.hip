@@ -54,6 +54,7 @@ struct CholArgs {
   int n_ls[kMaxBatch]; int64_t ldz; int D; double jitter;
   float* L; float* LinvT; int64_t ldl, strideL;   // L may be NULL
   int32_t* info;
+  float* lt_absmax[kMaxBatch];                    // optional per batch: max |L^-T| (float bits, atomicMax)
   double* ws; int64_t strideWS;                   // per batch: W, B [Mp][Mp], D [nb][64][64]
   int64_t M, Mp; int nb;
 };
@@ -136,6 +137,29 @@ __device__ __forceinline__ void tile_store_f32(float* __restrict__ g, int64_t ld
     const int r = idx >> 6, c = idx & 63;
     if (r < nr && c < nc) g[(int64_t)r * ld + c] = (float)(transpose ? s[c * LDT + r] : s[r * LDT + c]);
   }
+}
+
+// tile_store_f32 that also returns this thread's max |stored value|.
+__device__ __forceinline__ float tile_store_f32_max(float* __restrict__ g, int64_t ld, const double* __restrict__ s,
+                                                    bool transpose, int nr, int nc) {
+  float m = 0.f;
+  for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+    const int r = idx >> 6, c = idx & 63;
+    if (r < nr && c < nc) {
+      const float v = (float)(transpose ? s[c * LDT + r] : s[r * LDT + c]);
+      g[(int64_t)r * ld + c] = v;
+      m = fmaxf(m, fabsf(v));
+    }
+  }
+  return m;
+}
+
+// Wave maximum of a non-negative float, folded into *out by one atomic per wave
+// (non-negative floats order as their bit patterns).
+__device__ __forceinline__ void wave_absmax_atomic(float m, float* out) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
 }
 
 __device__ __forceinline__ void tile_store_f64(double* __restrict__ g, int64_t ld, const double* __restrict__ s) {
@@ -682,7 +706,14 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     return a.A ? input_elem(a, b, gr, gc) : kuu_elem(a, Zb, sil, varb, gr, gc);
   };
   if (blockIdx.x == 0) {  // factor tile (0, 0) straight from the input (dispatched first)
-    if (threadIdx.x == 0) a.info[b] = 0;
+    if (threadIdx.x == 0) {
+      a.info[b] = 0;
+      float* lt = a.lt_absmax[0];
+#pragma unroll
+      for (int i = 1; i < kMaxBatch; ++i)
+        if (b == i) lt = a.lt_absmax[i];
+      if (lt) *lt = 0.f;
+    }
     for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
       const int r = idx >> 6, c = idx & 63;
       s1[r * LDT + c] = elem(r, c);
@@ -726,10 +757,15 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   const int64_t Mp = a.Mp;
   auto Wt = [&](int bi, int bl) { return W + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
   auto Bt = [&](int bi, int bl) { return Bm + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
+  float* lt_max = a.lt_absmax[0];  // this batch entry's max |L^-T| (no dynamic indexing of the arguments)
+#pragma unroll
+  for (int q = 1; q < kMaxBatch; ++q)
+    if (b == q) lt_max = a.lt_absmax[q];
   auto store_linvT = [&](int c, const double* sx) {  // X_jc -> LinvT block (c, j)
     const int64_t gr = (int64_t)c * CB, gc = (int64_t)j * CB;
-    tile_store_f32(LinvT + gr * a.ldl + gc, a.ldl, sx, true, (int)min<int64_t>(CB, a.M - gr),
-                   (int)min<int64_t>(CB, a.M - gc));
+    const float m = tile_store_f32_max(LinvT + gr * a.ldl + gc, a.ldl, sx, true, (int)min<int64_t>(CB, a.M - gr),
+                                       (int)min<int64_t>(CB, a.M - gc));
+    if (lt_max) wave_absmax_atomic(m, lt_max);
   };
 
   if (T == 0) {  // last step: row block j of X only
@@ -1006,7 +1042,7 @@ static int kuu_potrf_trtri_impl(const float* const* Z, int64_t ldz, int64_t M, i
                                    const int32_t* n_ls, float jitter, int32_t batch, float* L,
                                    float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                                    void* workspace, size_t workspace_bytes, hipEvent_t prep_done,
-                                mgp_stream_t stream) {
+                                   float* const* lt_absmax, mgp_stream_t stream) {
   if (!Z) return -1;
   if (ldz < D) return -2;
   if (M < 0) return -3;
@@ -1026,6 +1062,7 @@ static int kuu_potrf_trtri_impl(const float* const* Z, int64_t ldz, int64_t M, i
     if (!Z[b] || !variance[b] || !lengthscales[b]) return -1;
     if (n_ls[b] != 1 && n_ls[b] != D) return -7;
     a.Z[b] = Z[b]; a.var[b] = variance[b]; a.ls[b] = lengthscales[b]; a.n_ls[b] = n_ls[b];
+    a.lt_absmax[b] = lt_absmax ? lt_absmax[b] : nullptr;
   }
   a.ldz = ldz; a.D = D; a.jitter = (double)jitter;
   a.L = L; a.LinvT = LinvT; a.ldl = ldl; a.strideL = strideL;
@@ -1039,7 +1076,7 @@ extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M
                                    float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                                    void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
   return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
-                              info, workspace, workspace_bytes, nullptr, stream);
+                              info, workspace, workspace_bytes, nullptr, nullptr, stream);
 }
 
 extern "C" int mgp_kuu_potrf_trtri_ev(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
@@ -1049,7 +1086,17 @@ extern "C" int mgp_kuu_potrf_trtri_ev(const float* const* Z, int64_t ldz, int64_
                                       void* workspace, size_t workspace_bytes, void* prep_done,
                                       mgp_stream_t stream) {
   return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
-                              info, workspace, workspace_bytes, (hipEvent_t)prep_done, stream);
+                              info, workspace, workspace_bytes, (hipEvent_t)prep_done, nullptr, stream);
+}
+
+extern "C" int mgp_kuu_potrf_trtri_ex(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                                      const float* const* variance, const float* const* lengthscales,
+                                      const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                                      float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                                      void* workspace, size_t workspace_bytes, void* prep_done,
+                                      float* const* linvt_absmax, mgp_stream_t stream) {
+  return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
+                              info, workspace, workspace_bytes, (hipEvent_t)prep_done, linvt_absmax, stream);
 }
 
 extern "C" size_t mgp_chol_backward_workspace_bytes(int64_t M) {

@@ -1053,6 +1053,33 @@ extern "C" int mgp_split_upper_f16(const float* LinvT, int64_t ldl, int64_t M, v
   return launch_status();
 }
 
+// mgp_split_upper_f16 whose trailer already holds max |LinvT| (written by
+// mgp_kuu_potrf_trtri_ex into mgp_x6_bound_ptr(Tfr)): the split alone.
+extern "C" int mgp_split_upper_f16_bounded(const float* LinvT, int64_t ldl, int64_t M, void* Tfr, size_t tfr_bytes,
+                                           mgp_stream_t stream) {
+  if (!LinvT) return -1;
+  if (ldl < M) return -2;
+  if (M < 0) return -3;
+  if (!Tfr) return -4;
+  if (M == 0) return MGP_OK;
+  if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(Tfr)) return MGP_ERR_ALIGN;
+  const int64_t Mp = x6_mp(M);
+  const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
+  const int64_t nfrag = (int64_t)nmb * nmk;
+  const float* bound = trailer(Tfr, lower_planes(M, 1));
+  hipLaunchKernelGGL(split_tri_kernel<false>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     LinvT, ldl, (int64_t)0, M, nmb, nmk, nfrag, (bf16x8*)Tfr, bound);
+  return launch_status();
+}
+
+// Device address of the split-f16 scale bound in an image's trailer (lower /
+// upper images: K = matrices in the batch; column images: K = 0, N columns).
+extern "C" float* mgp_x6_bound_ptr(void* img, int64_t M, int64_t N, int32_t K) {
+  if (!img || M <= 0) return nullptr;
+  return trailer(img, K > 0 ? lower_planes(M, K) : cols_planes(M, N));
+}
+
 extern "C" int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr,
                                   size_t afr_bytes, mgp_stream_t stream) {
   if (!A) return -1;

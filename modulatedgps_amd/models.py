@@ -391,10 +391,12 @@ class SMGP(SGP):
         self._bufs[key] = b
         return b
 
-    def _factorise(self, b, prep_event=None):
+    def _factorise(self, b, prep_event=None, tfr_bounds=False):
         """Kuu of both layers and their batched Cholesky + inverse (one K3 sweep).
         Training buffers also keep L (b["L_f"], b["L_a"]) for the backward pass.
-        prep_event: recorded once Kuu is built (batched path only; else after K3)."""
+        prep_event: recorded once Kuu is built (batched path only; else after K3).
+        tfr_bounds: K3 also writes max |LinvT| into the L^-T split-f16 images'
+        trailers (b["Tfr_f"], b["Tfr_a"]; batched path), for bounded splits."""
         pf, pa = self.pred_layer, self.assign_layer
         train = b.get("train", False)
         if "LinvT2" in b:
@@ -404,7 +406,8 @@ class SMGP(SGP):
             Lo, LinvT, info = ops.kuu_potrf_trtri(
                 [pf.Z, pa.Z], [pf.kernel.variance, pa.kernel.variance],
                 [pf.kernel.lengthscales, pa.kernel.lengthscales], default_jitter(), LinvT=b["LinvT2"],
-                L=b.get("L2"), want_L=train, prep_event=prep_event)
+                L=b.get("L2"), want_L=train, prep_event=prep_event,
+                tfr_bound_images=[b["Tfr_f"], b["Tfr_a"]] if tfr_bounds else None)
             self.last_info = info
             if train:
                 b["L_f"], b["L_a"] = Lo[0], Lo[1]
@@ -455,14 +458,17 @@ class SMGP(SGP):
             main = torch.cuda.current_stream(self.device)
             side = self._side_stream()
             prep = self._prep_event()
+        # split-f16 L^-T images: K3 folds their scale bound (max |LinvT|) into its
+        # writes of the inverse, so the split needs no reduction launches
+        bounded = b["x6"] and "Tfr_a" in b and "LinvT2" in b and fmt == "f16"
         with _Stage(timing, "kuu_chol"):
-            LinvT_f, LinvT_a = self._factorise(b, prep_event=prep)
+            LinvT_f, LinvT_a = self._factorise(b, prep_event=prep, tfr_bounds=bounded)
         Tfr = {}
         if b["x6"] and "Tfr_a" in b:
             # L^-T images straight after K3 on its stream (no cross-stream wait in front)
             with _Stage(timing, "split_tri"):
                 for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
-                    Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt)
+                    Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt, bounded=bounded)
         if b["x6"]:
             side.wait_event(prep)   # after Kuu's build (and so after everything before K3 on main)
             with torch.cuda.stream(side):
@@ -480,15 +486,13 @@ class SMGP(SGP):
                     "Afr": b.get("Afr_" + L, b.get("Afr")), "Tfr": b.get("Tfr_" + L, b.get("Tfr")),
                     "A32": b.get("A32_" + L)} for L, _ in layers}
         if b["x6"] and "Tfr_a" in b:
-            # K4 of the assign layer on the side stream, beside the pred layer's K4 and
-            # K5 (K4 leaves MFMA and memory slack that the other kernels fill)
+            # both layers' K4 then both K5 in stream order on the main stream: the
+            # matrix-core kernels fill the chip alone, and a cross-stream hand-off
+            # costs 10-25 us of idle GPU per wait (measured)
             pf, pa = self.pred_layer, self.assign_layer
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt, Tfr=Tfr["a"])
             Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing, fmt, Tfr=Tfr["f"])
+            Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt, Tfr=Tfr["a"])
             pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
-            main.wait_stream(side)
             pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)
         else:
             for L, layer in layers:

@@ -123,11 +123,14 @@ def potrf_trtri(A, L=None, LinvT=None, info=None, workspace=None):
 
 
 def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, info=None,
-                    workspace=None, want_L=False, prep_event=None):
+                    workspace=None, want_L=False, prep_event=None, tfr_bound_images=None):
     """Kuu (float64, from Z) + Cholesky + inverse for a batch of layers sharing M, D.
     Zs / variances / lengthscales: lists of device tensors.  Returns L (or None),
     LinvT [B, M, M] and info int32 [B].  prep_event: a torch.cuda.Event (already
-    created) recorded once Kuu is built (mgp_kuu_potrf_trtri_ev)."""
+    created) recorded once Kuu is built (mgp_kuu_potrf_trtri_ev).
+    tfr_bound_images: per layer, the L^-T split-f16 image buffer whose trailer
+    receives max |LinvT| (mgp_kuu_potrf_trtri_ex; then split_upper_x6(...,
+    bounded=True) skips its reduction)."""
     import ctypes
     Bt = len(Zs)
     M, D = Zs[0].shape
@@ -151,7 +154,14 @@ def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, inf
     vp = P(*[v.data_ptr() for v in variances])
     lp = P(*[l.data_ptr() for l in lengthscales])
     nl = (ctypes.c_int32 * Bt)(*[l.numel() for l in lengthscales])
-    if prep_event is not None:
+    if tfr_bound_images is not None:
+        lib = _lib.load()
+        bp = P(*[lib.mgp_x6_bound_ptr(t.data_ptr(), M, 0, 1) for t in tfr_bound_images])
+        _lib.call("mgp_kuu_potrf_trtri_ex", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
+                  L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
+                  LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(),
+                  prep_event.cuda_event if prep_event is not None else None, bp, _stream())
+    elif prep_event is not None:
         _lib.call("mgp_kuu_potrf_trtri_ev", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
                   L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
                   LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(),
@@ -208,15 +218,20 @@ def rbf_kuf_x6(X, Z, variance, lengthscales, out=None, fmt="x6"):
     return out
 
 
-def split_upper_x6(LinvT, out=None, fmt="x6"):
+def split_upper_x6(LinvT, out=None, fmt="x6", bounded=False):
     """Split-bf16 image of (L^-1)^T [M, M] (upper triangle) as K4's T operand
-    (fmt "f16": the split-f16 image, mgp_split_upper_f16)."""
+    (fmt "f16": the split-f16 image, mgp_split_upper_f16; bounded: `out`'s trailer
+    already holds max |LinvT| from kuu_potrf_trtri(..., tfr_bound_images=...),
+    mgp_split_upper_f16_bounded)."""
     _check(LinvT, "LinvT", 2)
     M = LinvT.shape[0]
     nbytes = _lib.load().mgp_x6_lower_bytes(M, 1)
+    if bounded and (fmt != "f16" or out is None):
+        raise ValueError("bounded splits are split-f16 into the image that received the bound")
     if out is None or out.numel() < nbytes:
         out = _ws(nbytes, LinvT.device)
-    _lib.call("mgp_split_upper_" + _fmt(fmt), LinvT.data_ptr(), _ld(LinvT), M, out.data_ptr(), out.numel(), _stream())
+    name = "mgp_split_upper_f16_bounded" if bounded else "mgp_split_upper_" + _fmt(fmt)
+    _lib.call(name, LinvT.data_ptr(), _ld(LinvT), M, out.data_ptr(), out.numel(), _stream())
     return out
 
 

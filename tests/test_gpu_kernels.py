@@ -116,6 +116,32 @@ def test_kuu_factorisation_matches_float64(device):
         assert normwise(to_np(LinvT[b]).T, Li) < 1e-6
 
 
+@pytest.mark.parametrize("M", [300, 1024])
+def test_kuu_linvt_bound_and_bounded_split(device, M):
+    """mgp_kuu_potrf_trtri_ex: K3 writes max |LinvT| into the L^-T images' trailers
+    (bit-exact vs the reduction of the written LinvT), and the bounded split then
+    gives the same split-f16 image as mgp_split_upper_f16's own reduction."""
+    from modulatedgps_amd import _lib, ops
+    rng = np.random.default_rng(3)
+    Zs = [_t(rng.standard_normal((M, 4)), device) for _ in range(2)]
+    var, ls = [_t([0.5], device), _t([0.1], device)], [_t([0.8], device), _t([1.3], device)]
+    nbytes = _lib.load().mgp_x6_lower_bytes(M, 1)
+    imgs = [torch.full((nbytes,), 7, dtype=torch.uint8, device=device) for _ in range(2)]
+    _, LinvT, info = ops.kuu_potrf_trtri(Zs, var, ls, 1e-6, tfr_bound_images=imgs)
+    assert (info.cpu() == 0).all()
+    for b in range(2):
+        bound = imgs[b][nbytes - 256:nbytes - 252].view(torch.float32).item()
+        ref = float(torch.triu(LinvT[b]).abs().max())
+        assert bound == ref
+        ops.split_upper_x6(LinvT[b], out=imgs[b], fmt="f16", bounded=True)
+        own = ops.split_upper_x6(LinvT[b], fmt="f16")
+        planes = (nbytes - 256) // 3072   # fragments x (f16 hi, f16 lo, unused) KiB planes
+        a = imgs[b][:planes * 3072].view(planes, 3, 1024)[:, :2]
+        o = own[:planes * 3072].view(planes, 3, 1024)[:, :2]
+        assert torch.equal(a, o)
+        assert torch.equal(imgs[b][nbytes - 256:nbytes - 252], own[nbytes - 256:nbytes - 252])
+
+
 @pytest.mark.parametrize("M,dup", [(1024, 0.0), (1024, 1e-3), (700, 1e-2)])
 def test_kuu_factorisation_ill_conditioned(device, M, dup):
     """K3 on badly conditioned Kuu (inducing points with near-duplicates, cond up
