@@ -42,8 +42,11 @@ constexpr int kMaxBatch = 8;
 #ifdef MGP_DBG_STAMPS
 __device__ unsigned long long g_stamps[64 * 16];
 #define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+// 100 MHz reference clock (one time base for every CU): slots 14 / 15
+#define RSTAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(j, k) do {} while (0)
+#define RSTAMP(j, k) do {} while (0)
 #endif
 
 struct CholArgs {
@@ -792,7 +795,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     const int bl_ = idx - ai * (ai + 1) / 2;
     const int i = j + 1 + ai, l = j + 1 + bl_;
     const bool la = (ai == 0 && bl_ == 0);
-    if (la) STAMP(j, 0);
+    if (la) { RSTAMP(j, 14); STAMP(j, 0); }
     TileRegs r1, rD, r2;
     Blk4 u;
     tile_fetch(r1, Wt(i, j), Mp);
@@ -835,6 +838,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
       write_diag(a, b, j + 1, s2, s1);
       __syncthreads();
       STAMP(j, 7);
+      RSTAMP(j, 15);
     } else {
       // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T in place in LDS (s2)
       diag_lower_update(s2, s1);

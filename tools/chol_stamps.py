@@ -16,13 +16,29 @@ import torch  # noqa: E402
 from modulatedgps_amd import _lib, ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
-M = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+M = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1024
 g = torch.Generator(device=dev).manual_seed(0)
 Z = torch.randn(M, 8, device=dev, generator=g)
 var = torch.tensor([0.5], device=dev)
 ls = torch.tensor([1.0], device=dev)
+with_k1 = "--with-k1" in sys.argv   # K1 x 2 on a side stream from the prep on, as in the step
+if with_k1:
+    N = 65536
+    X = torch.randn(N, 8, device=dev, generator=g)
+    side = torch.cuda.Stream(device=dev)
+    ev = torch.cuda.Event()
+    ev.record()
+    kfr = [ops.rbf_kuf_x6(X, Z, var, ls, fmt="f16") for _ in range(2)]
 for _ in range(3):
-    ops.kuu_potrf_trtri([Z, Z], [var, var], [ls, ls], 1e-6)
+    if with_k1:
+        torch.cuda.synchronize()
+        ops.kuu_potrf_trtri([Z, Z], [var, var], [ls, ls], 1e-6, prep_event=ev)
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            for k in kfr:
+                ops.rbf_kuf_x6(X, Z, var, ls, out=k, fmt="f16")
+    else:
+        ops.kuu_potrf_trtri([Z, Z], [var, var], [ls, ls], 1e-6)
 torch.cuda.synchronize()
 lib = _lib.load()
 buf = (ctypes.c_ulonglong * (64 * 16))()
@@ -37,3 +53,10 @@ for j in range(steps):
     sub = [s[8] - s[4], s[9] - s[8], s[10] - s[9], s[11] - s[10], s[12] - s[11], s[5] - s[12], "|",
            s[13] - s[5], s[6] - s[13]] if s[8] else []
     print(j, d[0], d[1], d[2], d[3], s[5] - s[4], s[6] - s[5], s[7] - s[6], "|", gap, "||", *sub)
+print("reference clock (100 MHz, one time base): step wall us, shader clock GHz, gap to the next step's look-ahead start us")
+for j in range(steps):
+    s, n = st[j], st[j + 1] if j + 1 < steps else None
+    wall = (s[15] - s[14]) * 1e-2
+    clk = (s[7] - s[0]) / max(1, s[15] - s[14]) / 10.0
+    gap = (n[14] - s[15]) * 1e-2 if n and n[14] else float("nan")
+    print(f"{j:2d} wall {wall:6.2f} us  clock {clk:5.2f} GHz  gap {gap:6.2f} us")
