@@ -298,6 +298,23 @@ int mgp_gram_f16(const float* X, int64_t ldx, int64_t sx, int64_t MI, const floa
                  int32_t mode, float* out, int64_t ldo, int64_t so, const float* x_bound,
                  const float* y_bound, const float* w_bound, void* workspace, size_t workspace_bytes,
                  mgp_stream_t stream);
+/* Row image of X (M x N f32, ldx % 4 == 0) for mgp_gram_f16_rows: fp16 hi / lo
+ * planes of X 2^e (e from the DEVICE bound *bound, as mgp_gram_f16 scales X) in
+ * the gram's fragment order, [32-row block][16-column k-step] blocks of 2 KiB,
+ * zero beyond M and N; mgp_rows_f16_ksteps(N) k-steps per row block. */
+int64_t mgp_rows_f16_ksteps(int64_t N);
+size_t mgp_rows_f16_bytes(int64_t M, int64_t N);
+int mgp_split_rows_f16(const float* X, int64_t ldx, int64_t M, int64_t N, const float* bound, void* img,
+                       size_t img_bytes, mgp_stream_t stream);
+/* mgp_gram_f16 (weighted: W required; X and the f32 Y 2-D, shared by the batch)
+ * with X given as its row image (mgp_split_rows_f16 of X with bound x_bound): X
+ * is split once instead of once per tile and batch entry, and one workgroup
+ * serves two batch entries.  Bit-identical to mgp_gram_f16.  The P_k =
+ * A diag(Gv_k) A^T grams of mgp_conditional_backward_f16 / _f16x8 run here. */
+int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI, const float* Y, int64_t ldy, int64_t MJ,
+                      const float* W, int64_t sw, int64_t N, int32_t batch, float alpha, int32_t mode, float* out,
+                      int64_t ldo, int64_t so, const float* x_bound, const float* y_bound, const float* w_bound,
+                      void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 
 /* Backward of one layer's whitened conditional (the GradientTape pass through
  * GPflow base_conditional, models.py:141-143, and SVGP's Knn = var,

@@ -87,6 +87,12 @@ SIGNATURES = {
     "mgp_gram_f16": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64,
                                     c_i32, ctypes.c_float, c_i32, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                                     c_size, c_ptr]),
+    "mgp_rows_f16_ksteps": (c_i64, [c_i64]),
+    "mgp_rows_f16_bytes": (c_size, [c_i64, c_i64]),
+    "mgp_split_rows_f16": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_gram_f16_rows": (ctypes.c_int, [c_ptr, c_size, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i32,
+                                         ctypes.c_float, c_i32, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
+                                         c_size, c_ptr]),
     "mgp_conditional_backward_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
     "mgp_conditional_backward_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
                                                    c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64,

@@ -348,27 +348,43 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
     }
   };
 
-  // chunk c lives in register set (c even: ra, odd: rb) and LDS buffer c % 2.
-  // The two roles run separate loops with the same barriers (one per chunk),
-  // so neither role's registers are live in the other's loop.
+  // chunk c lives in register set c % 4 and LDS buffer c % 2; the load of chunk
+  // c + 4 is issued as soon as chunk c is stashed (four chunk phases cover its
+  // latency).  The two roles run separate loops with the same barriers (one per
+  // chunk), so neither role's registers are live in the other's loop.
   if (producer) {
+    Regs r2, r3;
+    if (nch > 0) load(ra, 0);
+    if (nch > 1) load(rb, 1);
+    if (nch > 2) load(r2, 2);
+    if (nch > 3) load(r3, 3);
     if (nch > 0) {
-      load(ra, 0);
-      if (nch > 1) load(rb, 1);
       stash(ra, 0, 0);
-      if (nch > 2) load(ra, 2);
+      if (nch > 4) load(ra, 4);
     }
     __syncthreads();
-    for (int64_t i = 0; i < nch; i += 2) {
+    for (int64_t i = 0; i < nch; i += 4) {
       if (i + 1 < nch) {
         stash(rb, i + 1, 1);
-        if (i + 3 < nch) load(rb, i + 3);
+        if (i + 5 < nch) load(rb, i + 5);
       }
       __syncthreads();
       if (i + 1 >= nch) break;
       if (i + 2 < nch) {
-        stash(ra, i + 2, 0);
-        if (i + 4 < nch) load(ra, i + 4);
+        stash(r2, i + 2, 0);
+        if (i + 6 < nch) load(r2, i + 6);
+      }
+      __syncthreads();
+      if (i + 2 >= nch) break;
+      if (i + 3 < nch) {
+        stash(r3, i + 3, 1);
+        if (i + 7 < nch) load(r3, i + 7);
+      }
+      __syncthreads();
+      if (i + 3 >= nch) break;
+      if (i + 4 < nch) {
+        stash(ra, i + 4, 0);
+        if (i + 8 < nch) load(ra, i + 8);
       }
       __syncthreads();
     }
@@ -396,6 +412,210 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
     }
 }
 
+// ------------------------------------------------------------------ weighted gram on a row image, entry pairs
+// ws[z][b][i][j] = sum_n X[i][n] W_b[n] Y[j][n] over split z (the P_k grams of the
+// conditional backward): X (as its row image, split once) and the f32 Y are
+// shared by the batch, so one workgroup takes TWO batch entries of a tile: X's
+// fragments and Y's chunk are loaded once per chunk and Y is weighted and split
+// per entry (half the L2 -> CU traffic and a third less split work than one
+// entry per workgroup on gram_x6_kernel).  768 threads: consumer waves 0-7
+// (entry e = w / 4, 64 x 64 of the tile each, two per SIMD), producer waves 8-11.
+// Chunks of 32 n, double-buffered, one barrier each.
+constexpr int kXG2 = 2176;  // LDS bytes per (32-row block, k-step) group: 2 planes x 1 KiB + 128 B pad
+
+template <bool TRI>
+__global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restrict__ Ximg, int64_t nns, int64_t MI,
+                                                            const float* __restrict__ Y, int64_t ldy, int64_t MJ,
+                                                           const float* __restrict__ W, int64_t sw, int64_t N,
+                                                           int64_t nper, int nbj, int tiles, int pairs, int batch,
+                                                           int nsplit, float* __restrict__ ws, int64_t bstride,
+                                                           int64_t zstride, const float* __restrict__ xb,
+                                                           const float* __restrict__ yb,
+                                                           const float* __restrict__ wb) {
+  __shared__ __attribute__((aligned(16))) char sX[2][8 * kXG2], sY[2][2][8 * kXG2];
+  int q, pr, z;
+  {
+    const int id = blockIdx.x, items = tiles * pairs;
+    if (nsplit % 8 == 0) {
+      const int x = id & 7, j = id >> 3;
+      z = x + 8 * (j / items);
+      const int rem = j % items;
+      q = rem % tiles;
+      pr = rem / tiles;
+    } else {
+      q = id % tiles;
+      pr = (id / tiles) % pairs;
+      z = id / items;
+    }
+  }
+  int bi, bj;
+  if (TRI) {
+    bi = (int)((sqrtf(8.f * q + 1.f) - 1.f) * 0.5f);
+    while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+    while (bi * (bi + 1) / 2 > q) --bi;
+    bj = q - bi * (bi + 1) / 2;
+  } else {
+    bi = q / nbj;
+    bj = q % nbj;
+  }
+  const int b0 = 2 * pr;
+  const bool two = b0 + 1 < batch;
+  const int64_t i0 = (int64_t)bi * kGT, j0 = (int64_t)bj * kGT;
+  const int64_t nb = (int64_t)z * nper;
+  const int64_t ne = (nb + nper < N) ? nb + nper : N;
+  const int64_t nch = nb < ne ? (ne - nb + kXC - 1) / kXC : 0;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // X's image carries 2^ex; the weighted Y is split at 2^ey (bound |Y| |W|)
+  const int ex = img_exp(*xb), ey = img_exp(*yb * *wb);
+  const float ys = ldexpf(1.f, ey), unscale = ldexpf(1.f, -(ex + ey));
+
+  // ---- producer state.  Y: thread pt (0..255) of wave pw = pt / 64 loads 4
+  // consecutive n (column group cg) of rows 32 qq + rr, qq = 0..3, rr = 8 pw +
+  // (lane / 2) % 8, cg = 2 (lane / 16) + lane % 2 (gram_x6_kernel's lane pattern).
+  // X: 16-B image units u = pt + 256 s of the chunk's 8 blocks (row block u / 256,
+  // k-step (u / 128) % 2) -> LDS group u / 128, byte (u % 128) 16.
+  const int pt = tid - 512, pw = pt >> 6;
+  const int rr = 8 * pw + ((lane >> 1) & 7), cg = 2 * (lane >> 4) + (lane & 1);
+  const int soff = (cg >> 2) * kXG2 + (rr + 32 * ((cg >> 1) & 1)) * 16 + (cg & 1) * 8;
+  const int64_t rows_x = MI - i0 < kGT ? MI - i0 : kGT, rows_y = MJ - j0 < kGT ? MJ - j0 : kGT;
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Ximg + 4 * (int64_t)bi * nns * 2048), (short)0, (int)(uint32_t)((rows_x + 31) / 32 * nns * 2048),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t rY =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Y + j0 * ldy), (short)0, (int)(uint32_t)(rows_y * ldy * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(W + b0 * sw), (short)0, (int)(uint32_t)(N * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W + (two ? b0 + 1 : b0) * sw), (short)0, (int)(uint32_t)(N * 4), 0x00020000);
+  const uint32_t vy = (uint32_t)(rr * ldy + 4 * cg) * 4u, qy = (uint32_t)(32 * ldy * 4);
+  uint32_t vxi[4];
+  int dxi[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int u = pt + 256 * s, g = u >> 7;
+    vxi[s] = (uint32_t)(((g >> 1) * nns + (g & 1)) * 2048 + (u & 127) * 16);
+    dxi[s] = g * kXG2 + (u & 127) * 16;
+  }
+  struct Regs { u32x4v x[4]; floatx4 y[4], w0, w1; };
+  Regs ra, rb;
+  // loads are unconditional (past the data the resources read zeros or unused
+  // bytes): every path issues the same count, so the wait counts stay tight
+  auto load = [&](Regs& r, int64_t c) {
+    const int64_t n0 = nb + c * kXC;
+    const uint32_t so = (uint32_t)(n0 * 4), xso = (uint32_t)(n0 / 16 * 2048);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) r.x[s] = __builtin_amdgcn_raw_buffer_load_b128(rX, vxi[s], xso, 0);
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+      r.y[qq] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rY, vy + qq * qy, so, 0));
+    r.w0 = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rW0, 16u * cg, so, 0));
+    r.w1 = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rW1, 16u * cg, so, 0));
+  };
+  auto stash = [&](Regs& r, int64_t c, int buf) {
+    // Y's columns >= ne are zeroed (the last chunk; X's image is zero there) by
+    // selects, not branches: a branch here costs the loads' wait-count tracking
+    const int lim = (int)(ne - (nb + c * kXC)) - 4 * cg;
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) r.y[qq][e2] = e2 < lim ? r.y[qq][e2] : 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *reinterpret_cast<u32x4v*>(sX[buf] + dxi[s]) = r.x[s];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      stash4h(sY[buf][0] + 2 * qq * kXG2 + soff, r.y[qq] * r.w0, ys);
+      stash4h(sY[buf][1] + 2 * qq * kXG2 + soff, r.y[qq] * r.w1, ys);
+    }
+  };
+
+  // ---- consumer state: wave w (entry e) multiplies X blocks wb_, wb_ + 1 by the
+  // weighted Y blocks vb, vb + 1
+  const int e = w >> 2, wl = w & 3;
+  const int wb_ = (wl >> 1) * 2, vb = (wl & 1) * 2;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[a][c][k] = 0.f;
+  auto compute = [&](int buf) {
+    const char* sy_ = sY[buf][e];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 c[2][3];
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          c[t2][p] = *reinterpret_cast<const bf16x8*>(sy_ + (2 * (vb + t2) + ks) * kXG2 + p * 1024 + lane * 16);
+#pragma unroll
+      for (int ta = 0; ta < 2; ++ta) {
+        bf16x8 a[3];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          a[p] = *reinterpret_cast<const bf16x8*>(sX[buf] + (2 * (wb_ + ta) + ks) * kXG2 + p * 1024 + lane * 16);
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb) acc[ta][tb] = mfma_fmt<2, true>(a, c[tb], acc[ta][tb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // chunk c in register set c % 3 and LDS buffer c % 2; the load of chunk c + 3
+  // is issued as soon as chunk c is stashed (three chunk phases cover it)
+  if (w >= 8) {
+    Regs rc;
+    auto phase = [&](Regs& r, int64_t c, int buf) {
+      if (c < nch) stash(r, c, buf);
+      load(r, c + 3);
+      __syncthreads();
+    };
+    load(ra, 0);
+    load(rb, 1);
+    load(rc, 2);
+    if (nch > 0) stash(ra, 0, 0);
+    load(ra, 3);
+    __syncthreads();
+    for (int64_t i = 0; i < nch; i += 6) {
+      phase(rb, i + 1, 1);
+      if (i + 1 >= nch) break;
+      phase(rc, i + 2, 0);
+      if (i + 2 >= nch) break;
+      phase(ra, i + 3, 1);
+      if (i + 3 >= nch) break;
+      phase(rb, i + 4, 0);
+      if (i + 4 >= nch) break;
+      phase(rc, i + 5, 1);
+      if (i + 5 >= nch) break;
+      phase(ra, i + 6, 0);
+    }
+    return;
+  }
+  __syncthreads();
+  for (int64_t i = 0; i < nch; i += 2) {
+    compute(0);
+    __syncthreads();
+    if (i + 1 >= nch) break;
+    compute(1);
+    __syncthreads();
+  }
+  if (e == 1 && !two) return;
+  float* out = ws + (int64_t)z * zstride + (int64_t)(b0 + e) * bstride;
+#pragma unroll
+  for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+      const int64_t j = j0 + 32 * (vb + tb) + (lane & 31);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int64_t i = i0 + 32 * (wb_ + ta) + acc_row(k, lane);
+        if (i < MI && j < MJ) out[i * MJ + j] = acc[ta][tb][k] * unscale;
+      }
+    }
+}
+
 // out[b][i][j] = alpha * sum_z ws[z][b][i][j]; mode 0 full, 1 lower triangle
 // (zero above), 2 symmetric (the upper triangle mirrors the lower).
 __global__ __launch_bounds__(256) void gram_x6_reduce_kernel(const float* __restrict__ ws, int64_t bstride,
@@ -415,9 +635,67 @@ __global__ __launch_bounds__(256) void gram_x6_reduce_kernel(const float* __rest
   out[b * so + i * ldo + j] = v;
 }
 
+// Row image of X (M x N f32) for the gram's X side: [row block rb][k-step ns]
+// blocks of [plane][lane] 16-B units, lane (r, h) <- row 32 rb + r, element j <-
+// n = 16 ns + 8 h + j (the gram's lane -> n assignment), scaled by
+// 2^img_exp(*bound) and split into fp16 hi / lo (planes 0 / 1); zero beyond M, N.
+// Workgroup: one row block, 8 k-steps; thread: units u = tid + 256 s.
+__global__ __launch_bounds__(256) void split_rows_f16_kernel(const float* __restrict__ X, int64_t ldx, int64_t M,
+                                                             int64_t N, int nns, const float* __restrict__ bound,
+                                                             bf16x8* __restrict__ img) {
+  const int64_t rb = blockIdx.y;
+  const float scale = ldexpf(1.f, img_exp(*bound));
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int u = threadIdx.x + 256 * s, lane = u & 63;
+    const int64_t ns = 8 * (int64_t)blockIdx.x + (u >> 6);
+    if (ns >= nns) continue;
+    const int64_t row = 32 * rb + (lane & 31), n = 16 * ns + 8 * (lane >> 5);
+    float v[8];
+    if (row < M && n + 7 < N) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(X + row * ldx + n);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(X + row * ldx + n + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = a[j];
+        v[4 + j] = b[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (row < M && n + j < N) ? X[row * ldx + n + j] : 0.f;
+    }
+    store_split_f16(img + (rb * nns + ns) * 128 + lane, v, scale);
+  }
+}
+
 }  // namespace mgp
 
 using namespace mgp;
+
+extern "C" int64_t mgp_rows_f16_ksteps(int64_t N) { return N <= 0 ? 0 : (N + kXC - 1) / kXC * (kXC / 16); }
+
+extern "C" size_t mgp_rows_f16_bytes(int64_t M, int64_t N) {
+  if (M <= 0 || N <= 0) return 16;
+  return (size_t)((M + 31) / 32) * (size_t)mgp_rows_f16_ksteps(N) * 2048;
+}
+
+extern "C" int mgp_split_rows_f16(const float* X, int64_t ldx, int64_t M, int64_t N, const float* bound, void* img,
+                                  size_t img_bytes, mgp_stream_t stream) {
+  if (!X) return -1;
+  if (ldx < N || ldx % 4) return -2;
+  if (M < 0) return -3;
+  if (N < 0) return -4;
+  if (!bound) return -5;
+  if (!img) return -6;
+  if (M == 0 || N == 0) return MGP_OK;
+  if (img_bytes < mgp_rows_f16_bytes(M, N)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(X) || !aligned16(img)) return MGP_ERR_ALIGN;
+  const int64_t nns = mgp_rows_f16_ksteps(N);
+  if (nns >= ((int64_t)1 << 30) || (M + 31) / 32 > 65535) return MGP_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(split_rows_f16_kernel, dim3((unsigned)((nns + 7) / 8), (unsigned)((M + 31) / 32)), dim3(256), 0,
+                     (hipStream_t)stream, X, ldx, M, N, (int)nns, bound, (bf16x8*)img);
+  return launch_status();
+}
 
 static int gram_splits(int64_t N, int tiles) {
   // aim for >= 1024 workgroups, each with >= 1024 points
@@ -562,4 +840,58 @@ extern "C" int mgp_gram_f16(const float* X, int64_t ldx, int64_t sx, int64_t MI,
   if (W && !w_bound) return -20;
   return gram_x6_launch(X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, N, batch, alpha, mode, out, ldo, so, workspace,
                         workspace_bytes, stream, x_bound, y_bound, w_bound);
+}
+
+// mgp_gram_f16 (weighted) with X given as its row image (mgp_split_rows_f16 of X
+// with bound x_bound) and the f32 Y shared by the batch: X's split is done once,
+// and one workgroup serves two batch entries (gram_rows2_kernel).
+extern "C" int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI, const float* Y, int64_t ldy,
+                                 int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                                 int32_t mode, float* out, int64_t ldo, int64_t so, const float* x_bound,
+                                 const float* y_bound, const float* w_bound, void* workspace, size_t workspace_bytes,
+                                 mgp_stream_t stream) {
+  if (!ximg) return -1;
+  if (!Y) return -4;
+  if (ldy < N || ldy % 4) return -5;
+  if (!W) return -10;
+  if (!x_bound) return -18;
+  if (!y_bound) return -19;
+  if (!w_bound) return -20;
+  if (MI < 0 || MJ < 0 || N < 0 || batch < 0) return -3;
+  if (mode < 0 || mode > 2 || (mode && MI != MJ)) return -14;
+  if (batch > 1 && sw % 4) return -10;
+  if (MI > 0 && N > 0 && ximg_bytes < mgp_rows_f16_bytes(MI, N)) return MGP_ERR_WORKSPACE;
+  if (N * 4 >= ((int64_t)1 << 31) || (int64_t)kGT * ldy * 4 >= ((int64_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  const int64_t nns = mgp_rows_f16_ksteps(N);
+  if (4 * nns * 2048 >= ((int64_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  if (!out) return -15;
+  if (ldo < MJ) return -16;
+  if (batch > 1 && so < ldo * MI) return -17;
+  if (MI == 0 || MJ == 0 || batch == 0) return MGP_OK;
+  if (!aligned16(ximg) || !aligned16(Y) || !aligned16(W)) return MGP_ERR_ALIGN;
+  if (!workspace || workspace_bytes < mgp_gram_x6_workspace_bytes(MI, MJ, N, batch, mode)) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles = gram_x6_tiles(MI, MJ, mode != 0);
+  const int nbj = (int)((MJ + kGT - 1) / kGT);
+  const int nsplit = N > 0 ? gram_x6_splits(N, (int64_t)tiles * batch) : 1;  // the x6 gram's workspace
+  int64_t nper = (N + nsplit - 1) / nsplit;
+  nper = (nper + kXC - 1) / kXC * kXC;
+  float* ws = (float*)workspace;
+  const int64_t bstride = MI * MJ, zstride = (int64_t)batch * MI * MJ;
+  const int pairs = (batch + 1) / 2;
+  const dim3 grid((unsigned)(tiles * pairs * nsplit));
+  if (mode != 0)
+    hipLaunchKernelGGL(gram_rows2_kernel<true>, grid, dim3(768), 0, s, (const char*)ximg, nns, MI, Y, ldy, MJ, W, sw,
+                       N, nper, nbj, tiles, pairs, (int)batch, nsplit, ws, bstride, zstride, x_bound, y_bound,
+                       w_bound);
+  else
+    hipLaunchKernelGGL(gram_rows2_kernel<false>, grid, dim3(768), 0, s, (const char*)ximg, nns, MI, Y, ldy, MJ, W, sw,
+                       N, nper, nbj, tiles, pairs, (int)batch, nsplit, ws, bstride, zstride, x_bound, y_bound,
+                       w_bound);
+  int st = launch_status();
+  if (st) return st;
+  const int64_t total = (int64_t)batch * MI * MJ;
+  hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, bstride,
+                     zstride, nsplit, MI, MJ, total, alpha, (int)mode, out, ldo, so);
+  return launch_status();
 }

@@ -1124,6 +1124,14 @@ extern "C" int mgp_expert_conditional_f16x8(const void* Afr, size_t afr_bytes, c
 
 // ------------------------------------------------------------------ conditional backward (x6)
 extern "C" size_t mgp_gram_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t tri);
+extern "C" size_t mgp_rows_f16_bytes(int64_t M, int64_t N);
+extern "C" int mgp_split_rows_f16(const float* X, int64_t ldx, int64_t M, int64_t N, const float* bound, void* img,
+                                  size_t img_bytes, mgp_stream_t stream);
+extern "C" int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI, const float* Y, int64_t ldy,
+                                 int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
+                                 int32_t mode, float* out, int64_t ldo, int64_t so, const float* x_bound,
+                                 const float* y_bound, const float* w_bound, void* workspace, size_t workspace_bytes,
+                                 mgp_stream_t stream);
 extern "C" size_t mgp_gram_x6_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t batch, int32_t mode);
 
 extern "C" int mgp_gram_x6(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
@@ -1150,7 +1158,8 @@ CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
   size_t o = 0;
   const int64_t ldm = (M + 3) / 4 * 4;
   w.sfr = o;  o += al256(mgp_x6_lower_bytes(M, K));
-  w.ga0 = o;  o += al256((size_t)M * ldn * 4);
+  // gA0 (read last by step 3), then A's row image for the P_k gram (step 5)
+  w.ga0 = o;  o += al256(std::max((size_t)M * ldn * 4, mgp_rows_f16_bytes(M, N)));
   w.gafr = o; o += al256(mgp_x6_cols_bytes(M, N));
   w.lifr = o; o += al256(mgp_x6_lower_bytes(M, 1));
   w.P = o;    o += al256((size_t)K * M * ldm * 4);
@@ -1338,8 +1347,12 @@ static int conditional_backward(
     if ((st = hip_status(hipMemsetAsync(bnd, 0, sizeof(float), s)))) return st;
     launch_absmax<0>(Gv, ldg, (int64_t)0, (int64_t)K, N, (int64_t)K, bnd, s);
     if ((st = launch_status())) return st;
-    st = mgp_gram_f16(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, a_bound, a_bound, bnd, gws,
-                      gwsb, stream);
+    // A's row image (split once; gA0's space is free after step 3) as the grams'
+    // unweighted side
+    const size_t rimg = mgp_rows_f16_bytes(M, N);
+    if ((st = mgp_split_rows_f16(A, lda, M, N, a_bound, gA0, rimg, stream))) return st;
+    st = mgp_gram_f16_rows(gA0, rimg, M, A, lda, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, a_bound, a_bound, bnd,
+                           gws, gwsb, stream);
   } else {
     st = mgp_gram_x6(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, gws, gwsb, stream);
   }

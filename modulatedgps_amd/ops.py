@@ -505,12 +505,27 @@ def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):
     return out
 
 
-def gram_x6(X, Y, W=None, alpha=1.0, mode=0, N=None, out=None, workspace=None, bounds=None):
+def split_rows_f16(X, bound, N=None, out=None):
+    """X's row image for gram_x6(x_rows=...) (mgp_split_rows_f16): X [MI, >=N] f32, bound a float32
+    device tensor >= max |X| (the scale mgp_gram_f16 would use)."""
+    _check(X, "X", 2)
+    M = X.shape[0]
+    N = X.shape[1] if N is None else N
+    nbytes = _lib.load().mgp_rows_f16_bytes(M, N)
+    if out is None or out.numel() < nbytes:
+        out = _ws(nbytes, X.device)
+    _lib.call("mgp_split_rows_f16", X.data_ptr(), _ld(X), M, N, bound.data_ptr(), out.data_ptr(), out.numel(),
+              _stream())
+    return out
+
+
+def gram_x6(X, Y, W=None, alpha=1.0, mode=0, N=None, out=None, workspace=None, bounds=None, x_rows=None):
     """out[b][i][j] = alpha * sum_n X[b][i][n] W[b][n] Y[b][j][n] at f32 accuracy on the bf16 MFMA.
     X [B, MI, >=N] / [MI, >=N] (Y likewise; a 2-D operand is shared by the batch); W [B, >=N] or None;
     mode 0 full, 1 lower triangle, 2 symmetric.  bounds = (x_bound, y_bound, w_bound) float32
     device tensors of max |X|, |Y|, |W| (w_bound None without W): the split-f16 variant
-    (mgp_gram_f16)."""
+    (mgp_gram_f16).  x_rows: split_rows_f16(X, x_bound) of a 2-D X (with bounds, W and a 2-D Y):
+    the same products with X's split done once (mgp_gram_f16_rows)."""
     X3 = X if X.dim() == 3 else X.unsqueeze(0)
     Y3 = Y if Y.dim() == 3 else Y.unsqueeze(0)
     B = max(X3.shape[0], Y3.shape[0], W.shape[0] if W is not None and W.dim() == 2 else 1)
@@ -526,6 +541,12 @@ def gram_x6(X, Y, W=None, alpha=1.0, mode=0, N=None, out=None, workspace=None, b
     if workspace is None or workspace.numel() < nbytes:
         workspace = _ws(nbytes, dev)
     so = out.stride(0) if out.dim() == 3 else MI * _ld(out)
+    if x_rows is not None:
+        xb, yb, wb = bounds
+        _lib.call("mgp_gram_f16_rows", x_rows.data_ptr(), x_rows.numel(), MI, Y3.data_ptr(), Y3.stride(1), MJ,
+                  W.data_ptr(), sw, N, B, float(alpha), int(mode), out.data_ptr(), out.stride(-2), so,
+                  xb.data_ptr(), yb.data_ptr(), wb.data_ptr(), workspace.data_ptr(), workspace.numel(), _stream())
+        return out
     if bounds is not None:
         xb, yb, wb = bounds
         _lib.call("mgp_gram_f16", X3.data_ptr(), X3.stride(1), sx, MI, Y3.data_ptr(), Y3.stride(1), sy, MJ,

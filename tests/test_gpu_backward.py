@@ -195,3 +195,33 @@ def test_gram_x6(device, MI, MJ, N, B, mode, weighted):
     out16 = ops.gram_x6(Xd, Yd, Wd, alpha=-0.5, mode=mode, N=N, bounds=(bx, by, bw))
     got16 = to_np(out16).reshape(B, MI, -1)[:, :, :MJ]
     assert normwise(got16, ref.numpy()) < 4e-6
+
+@pytest.mark.parametrize("MI,MJ,N,B,mode", [(1024, 1024, 16384, 4, 2), (300, 300, 5000, 3, 2), (130, 70, 777, 2, 0),
+                                            (64, 64, 31, 1, 2), (256, 256, 4096, 8, 1)])
+def test_gram_f16_rows(device, MI, MJ, N, B, mode):
+    """The weighted gram with X as its row image (mgp_split_rows_f16 + mgp_gram_f16_rows,
+    two batch entries per workgroup) is bit-identical to mgp_gram_f16 splitting X on
+    the fly (same split, same fragment order, same split-K sums), and within the
+    split-f16 gram's accuracy of float64 (test_gram_x6's 4e-6)."""
+    from modulatedgps_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(7 * MI + N)
+    X = torch.randn(MI, N, generator=g)
+    Y = X[:MJ] if mode else torch.randn(MJ, N, generator=g)
+    W = torch.rand(B, N, generator=g) - 0.3
+    Xd = ops.padded(MI, N, device).copy_(X.to(device))
+    Yd = Xd[:MJ] if mode else ops.padded(MJ, N, device).copy_(Y.to(device))
+    Wd = ops.padded(B, N, device).copy_(W.to(device))
+    bx = torch.tensor([1.5 * float(X.abs().max())], device=device)
+    by = torch.tensor([float(Y.abs().max())], device=device)
+    bw = torch.tensor([float(W.abs().max())], device=device)
+    ref16 = ops.gram_x6(Xd, Yd, Wd, alpha=2.0, mode=mode, N=N, bounds=(bx, by, bw))
+    img = ops.split_rows_f16(Xd, bx, N=N)
+    got = ops.gram_x6(Xd, Yd, Wd, alpha=2.0, mode=mode, N=N, bounds=(bx, by, bw), x_rows=img)
+    assert torch.equal(got, ref16)
+    ref = 2.0 * torch.einsum("in,bn,jn->bij", X.double(), W.double(), Y.double())
+    if mode == 1:
+        ref = torch.tril(ref)
+    elif mode == 2:
+        ref = torch.tril(ref) + torch.tril(ref, -1).transpose(1, 2)
+    got = to_np(got).reshape(B, MI, -1)[:, :, :MJ]
+    assert normwise(got, ref.numpy()) < 4e-6

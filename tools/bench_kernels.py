@@ -77,6 +77,8 @@ def main():
     gLm = ops.padded(M, M, dev)
     wsg = torch.empty(max(ops._lib.load().mgp_gram_x6_workspace_bytes(M, M, N, K, 2),
                           ops._lib.load().mgp_gram_x6_workspace_bytes(M, M, N, 1, 1)), dtype=torch.uint8, device=dev)
+    gbnd = (A32[:, :N].abs().max().reshape(1), A32[:, :N].abs().max().reshape(1), Gv[:, :N].abs().max().reshape(1))
+    arows = ops.split_rows_f16(A32, gbnd[0], N=N)
     cb = ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N)
     wsc = torch.empty(ops.conditional_backward_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev)
     A32h = ops.padded(M, N, dev)   # the f16 chain's training K4: f16 A image + f32 A
@@ -114,6 +116,9 @@ def main():
                                                                fmt="f16", cross="f8"),
         "gram_x6_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg),
         "gram_x6_Lm": lambda: ops.gram_x6(gK, A32, None, mode=1, N=N, out=gLm, workspace=wsg),
+        "gram_f16_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg, bounds=gbnd),
+        "gram_f16_rows_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg, bounds=gbnd,
+                                               x_rows=arows),
         "rbf_bwd": lambda: ops.rbf_backward(X, Z, var, lsc, gK),
         "cond_bwd_x6": lambda: ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
                                                            out=cb, workspace=wsc),
@@ -141,7 +146,8 @@ def main():
     for name in ("trsm_stats_x6", "trsm_stats_x6f16", "trsm_stats_f16", "trsm_stats_f16x8"):
         if name in out:
             out[name]["tflops"] = M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
-    for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N),
+    for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N), ("gram_f16_P", K * M * M * N),
+                     ("gram_f16_rows_P", K * M * M * N),
                      ("cond_bwd_x6", (2 * K + 1) * M * M * N), ("cond_bwd_f16", (2 * K + 1) * M * M * N)):
         if name in out:
             out[name]["tflops"] = fl / (out[name]["median_ms"] * 1e-3) / 1e12
