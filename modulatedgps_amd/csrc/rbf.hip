@@ -214,9 +214,13 @@ static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, 
 // Kernel 1: 4 waves x 2 rows of Z per block, lanes stride over an n-chunk four
 // points at a time; each lane accumulates its <= 64 points in float32 (sums of
 // centred terms), the lane / chunk reduction is float64.  Kernel 2 folds the
-// chunks and writes the grads.
+// chunks (one thread per sum), kernel 3 writes the grads.
+// VEC (ldx % 4 == 0, ldx >= DMAX, X 16-byte aligned): a point's coordinates come
+// in DMAX / 4 dwordx4 loads instead of DMAX dword loads at a 4 ldx-byte lane
+// stride -- the strided dword loads cost the address unit 8x the cycles and
+// bounded this kernel.
 constexpr int kRbfRows = 2;  // rows of Z per wave
-template <int DMAX>
+template <int DMAX, bool VEC = false>
 __global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restrict__ X, int64_t ldx,
                                                            const float* __restrict__ Z, int64_t ldz, int64_t N,
                                                            int64_t M, int D, const float* __restrict__ variance,
@@ -246,8 +250,17 @@ __global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restri
     for (int j = 0; j < NS; ++j) acc[r][j] = 0.f;
   auto point = [&](int64_t n) {
     float x[DMAX], g[R];
+    if constexpr (VEC && DMAX >= 4) {
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[n * ldx + d] : 0.f;
+      for (int q4 = 0; q4 < DMAX / 4; ++q4) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(X + n * ldx + 4 * q4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[4 * q4 + j] = (4 * q4 + j < D) ? v[j] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[n * ldx + d] : 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) g[r] = (m0 + r < M) ? gK[(m0 + r) * ldg + n] : 0.f;
 #pragma unroll
@@ -285,6 +298,16 @@ __global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restri
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
       if (lane == 0 && m0 + r < M) part[((int64_t)blockIdx.y * M + m0 + r) * NS + j] = v;
     }
+}
+
+// part[0][m][j] = sum over the chunks of part[ch][m][j] (in place: each thread
+// reads only its own (m, j) of every chunk), one thread per (m, j), fixed order.
+__global__ __launch_bounds__(256) void rbf_bwd_fold_kernel(double* __restrict__ part, int nchunks, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  double v = part[idx];
+  for (int ch = 1; ch < nchunks; ++ch) v += part[(int64_t)ch * total + idx];
+  part[idx] = v;
 }
 
 template <int DMAX>
@@ -476,13 +499,20 @@ extern "C" int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int
   const dim3 grid((unsigned)((M + 4 * kRbfRows - 1) / (4 * kRbfRows)), (unsigned)(nch > 0 ? nch : 1));
 #define MGP_RBF_BWD_CASE(DM)                                                                                  \
   if (D <= DM) {                                                                                              \
-    if (nch > 0)                                                                                              \
+    const bool vec = DM >= 4 && ldx % 4 == 0 && ldx >= DM && aligned16(X);                                     \
+    if (nch > 0 && vec)                                                                                       \
+      hipLaunchKernelGGL((rbf_bwd_rows_kernel<DM, true>), grid, dim3(256), 0, s, X, ldx, Z, ldz, N, M, D,       \
+                         variance, lengthscales, n_ls, gK, ldg, chunk, part);                                 \
+    else if (nch > 0)                                                                                         \
       hipLaunchKernelGGL(rbf_bwd_rows_kernel<DM>, grid, dim3(256), 0, s, X, ldx, Z, ldz, N, M, D, variance,    \
                          lengthscales, n_ls, gK, ldg, chunk, part);                                           \
     else                                                                                                      \
       hipMemsetAsync(part, 0, mgp_rbf_backward_workspace_bytes(N, M, D), s);                                  \
-    hipLaunchKernelGGL(rbf_bwd_finish_kernel<DM>, dim3(1), dim3(256), 0, s, part, nch > 0 ? nch : 1, M, D, Z,  \
-                       ldz, variance, lengthscales, n_ls, zf, accumulate, gZ, ldgz, g_var, g_ls);             \
+    if (nch > 1)                                                                                              \
+      hipLaunchKernelGGL(rbf_bwd_fold_kernel, dim3((unsigned)((M * (1 + 2 * DM) + 255) / 256)), dim3(256), 0, s, \
+                         part, nch, M * (1 + 2 * DM));                                                        \
+    hipLaunchKernelGGL(rbf_bwd_finish_kernel<DM>, dim3(1), dim3(256), 0, s, part, 1, M, D, Z, ldz, variance,   \
+                       lengthscales, n_ls, zf, accumulate, gZ, ldgz, g_var, g_ls);                            \
     return launch_status();                                                                                   \
   }
   MGP_RBF_BWD_CASE(1)

@@ -135,11 +135,15 @@ def test_chol_backward(device, M, D, ls):
     assert normwise(to_np(g), ref) < 1e-4
 
 
-@pytest.mark.parametrize("N,M,D,ard,sym", [(3000, 64, 2, False, False), (5000, 200, 3, True, False),
-                                            (200, 200, 3, True, True), (1024, 1024, 8, False, True)])
-def test_rbf_backward(device, N, M, D, ard, sym):
+@pytest.mark.parametrize("N,M,D,ard,sym,ldx", [(3000, 64, 2, False, False, 0), (5000, 200, 3, True, False, 0),
+                                                (200, 200, 3, True, True, 0), (1024, 1024, 8, False, True, 0),
+                                                (4000, 96, 4, True, False, 0), (3001, 64, 16, True, False, 0),
+                                                (2500, 80, 5, True, False, 8), (2500, 80, 5, False, False, 0)])
+def test_rbf_backward(device, N, M, D, ard, sym, ldx):
     """Reverse mode of K(Z, X) (and of K(Z, Z) with a symmetric cotangent) w.r.t.
-    Z, the variance and the lengthscales against float64 autograd."""
+    Z, the variance and the lengthscales against float64 autograd; D = 4, 8, 16 with
+    ldx = D and D = 5 in rows of 8 take the dwordx4 point loads, the rest the dword
+    loads."""
     from modulatedgps_amd import ops
     rng = np.random.default_rng(12)
     Z = rng.standard_normal((M, D)).astype(np.float32)
@@ -150,7 +154,13 @@ def test_rbf_backward(device, N, M, D, ard, sym):
     if sym:
         gK = 0.5 * (gK + gK.T)
     dev = lambda a: torch.as_tensor(a, device=device)
-    gZ, gv, gl = ops.rbf_backward(dev(X), dev(Z), dev(np.float32([0.6])), dev(lsv), ops.as_padded(dev(gK)),
+    Xd = dev(X)
+    if ldx:  # X as the first D columns of rows of ldx floats
+        Xd = torch.zeros(N, ldx, device=device)
+        Xd[:, :D] = dev(X)
+        Xd[:, D:] = 7.0  # must not enter the result
+        Xd = Xd[:, :D]
+    gZ, gv, gl = ops.rbf_backward(Xd, dev(Z), dev(np.float32([0.6])), dev(lsv), ops.as_padded(dev(gK)),
                                   symmetric=sym)
     z64 = torch.tensor(Z.astype(np.float64), requires_grad=True)
     v64 = torch.tensor(float(np.float32(0.6)), dtype=torch.float64, requires_grad=True)
