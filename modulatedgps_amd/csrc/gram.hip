@@ -617,22 +617,48 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
 }
 
 // out[b][i][j] = alpha * sum_z ws[z][b][i][j]; mode 0 full, 1 lower triangle
-// (zero above), 2 symmetric (the upper triangle mirrors the lower).
+// (zero above), 2 symmetric (the upper triangle mirrors the lower).  Grid
+// (32-column tile, 32-row tile, batch), 256 threads: the source tile (the
+// mirrored one above the diagonal in mode 2) is summed with row-contiguous
+// loads into LDS and written out transposed where needed -- coalesced both ways,
+// no index divisions.
 __global__ __launch_bounds__(256) void gram_x6_reduce_kernel(const float* __restrict__ ws, int64_t bstride,
                                                              int64_t zstride, int nsplit, int64_t MI, int64_t MJ,
-                                                             int64_t total, float alpha, int mode,
-                                                             float* __restrict__ out, int64_t ldo, int64_t so) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= total) return;
-  const int64_t b = idx / (MI * MJ), rem = idx % (MI * MJ);
-  const int64_t i = rem / MJ, j = rem % MJ;
-  float v = 0.f;
-  if (!(mode == 1 && j > i)) {
-    const int64_t src = b * bstride + ((mode == 2 && j > i) ? j * MJ + i : i * MJ + j);
-    for (int z = 0; z < nsplit; ++z) v += ws[(int64_t)z * zstride + src];
-    v *= alpha;
+                                                             float alpha, int mode, float* __restrict__ out,
+                                                             int64_t ldo, int64_t so) {
+  __shared__ float sT[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t bi = blockIdx.y, bj = blockIdx.x, b = blockIdx.z;
+  const bool mirror = mode == 2 && bj > bi;
+  const bool skip = mode == 1 && bj > bi;  // a zero tile
+  const int64_t ti = mirror ? bj : bi, tj = mirror ? bi : bj;
+  if (!skip) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t r = 32 * ti + ty + 8 * k, c = 32 * tj + tx;
+      float v = 0.f;
+      if (r < MI && c < MJ) {
+        const float* src = ws + b * bstride + r * MJ + c;
+        for (int z = 0; z < nsplit; ++z) v += src[(int64_t)z * zstride];
+      }
+      sT[ty + 8 * k][tx] = v * alpha;
+    }
   }
-  out[b * so + i * ldo + j] = v;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int li = ty + 8 * k;
+    const int64_t i = 32 * bi + li, j = 32 * bj + tx;
+    if (i >= MI || j >= MJ) continue;
+    float v;
+    if (skip || (mode == 1 && j > i))
+      v = 0.f;
+    else if (mirror || (mode == 2 && bi == bj && j > i))
+      v = sT[tx][li];
+    else
+      v = sT[li][tx];
+    out[b * so + i * ldo + j] = v;
+  }
 }
 
 // Row image of X (M x N f32) for the gram's X side: [row block rb][k-step ns]
@@ -790,6 +816,7 @@ static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, c
   if (ldo < MJ) return -16;
   if (batch > 1 && so < ldo * MI) return -17;
   if (MI == 0 || MJ == 0 || batch == 0) return MGP_OK;
+  if (batch > 65535) return MGP_ERR_UNSUPPORTED;  // the reduction's grid
   if (!aligned16(X) || !aligned16(Y) || (W && !aligned16(W))) return MGP_ERR_ALIGN;
   if (!workspace || workspace_bytes < mgp_gram_x6_workspace_bytes(MI, MJ, N, batch, mode)) return MGP_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
@@ -816,9 +843,8 @@ static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, c
 #undef MGP_GRAM_X6
   int st = launch_status();
   if (st) return st;
-  const int64_t total = (int64_t)batch * MI * MJ;
-  hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, bstride,
-                     zstride, nsplit, MI, MJ, total, alpha, (int)mode, out, ldo, so);
+  hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((MJ + 31) / 32), (unsigned)((MI + 31) / 32), (unsigned)batch),
+                     dim3(256), 0, s, ws, bstride, zstride, nsplit, MI, MJ, alpha, (int)mode, out, ldo, so);
   return launch_status();
 }
 
@@ -868,6 +894,7 @@ extern "C" int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI
   if (ldo < MJ) return -16;
   if (batch > 1 && so < ldo * MI) return -17;
   if (MI == 0 || MJ == 0 || batch == 0) return MGP_OK;
+  if (batch > 65535) return MGP_ERR_UNSUPPORTED;  // the reduction's grid
   if (!aligned16(ximg) || !aligned16(Y) || !aligned16(W)) return MGP_ERR_ALIGN;
   if (!workspace || workspace_bytes < mgp_gram_x6_workspace_bytes(MI, MJ, N, batch, mode)) return MGP_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
@@ -890,8 +917,7 @@ extern "C" int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI
                        w_bound);
   int st = launch_status();
   if (st) return st;
-  const int64_t total = (int64_t)batch * MI * MJ;
-  hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, bstride,
-                     zstride, nsplit, MI, MJ, total, alpha, (int)mode, out, ldo, so);
+  hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((MJ + 31) / 32), (unsigned)((MI + 31) / 32), (unsigned)batch),
+                     dim3(256), 0, s, ws, bstride, zstride, nsplit, MI, MJ, alpha, (int)mode, out, ldo, so);
   return launch_status();
 }
