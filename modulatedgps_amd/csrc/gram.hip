@@ -142,6 +142,56 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
   out[i * ldo + j] = v;
 }
 
+// Narrow grams (MJ <= 16, e.g. g_q_mu = A G_mu^T with K columns): a 128-column
+// MFMA tile would be 1/16 used, so lanes stride over n instead: wave w keeps RW
+// rows x JMAX columns of sums (RW JMAX = 64 registers), each X element is read
+// once, Y's rows per 4 RW-row block; the lane and chunk sums are float64.
+template <int JMAX>
+__global__ __launch_bounds__(256) void gram_narrow_kernel(const float* __restrict__ X, int64_t ldx, int64_t MI,
+                                                          const float* __restrict__ Y, int64_t ldy, int64_t MJ,
+                                                          int64_t N, int64_t chunk, double* __restrict__ part) {
+  constexpr int RW = 64 / JMAX;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + w) * RW;
+  const int64_t nb = (int64_t)blockIdx.y * chunk, ne = nb + chunk < N ? nb + chunk : N;
+  float acc[RW][JMAX];
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) acc[r][j] = 0.f;
+  for (int64_t n = nb + lane; n < ne; n += 64) {
+    float y[JMAX], x[RW];
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) y[j] = j < MJ ? Y[(int64_t)j * ldy + n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < RW; ++r) x[r] = i0 + r < MI ? X[(i0 + r) * ldx + n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int j = 0; j < JMAX; ++j) acc[r][j] = fmaf(x[r], y[j], acc[r][j]);
+  }
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) {
+      double v = (double)acc[r][j];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0 && i0 + r < MI && j < MJ) part[((int64_t)blockIdx.y * MI + i0 + r) * MJ + j] = v;
+    }
+}
+
+// out[i][j] = alpha * sum over the chunks of part[ch][i][j] (fixed order).
+__global__ __launch_bounds__(256) void gram_narrow_fold_kernel(const double* __restrict__ part, int nch, int64_t MI,
+                                                               int64_t MJ, float alpha, float* __restrict__ out,
+                                                               int64_t ldo) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= MI * MJ) return;
+  double v = 0.0;
+  for (int ch = 0; ch < nch; ++ch) v += part[(int64_t)ch * MI * MJ + idx];
+  out[(idx / MJ) * ldo + idx % MJ] = (float)(alpha * v);
+}
+
 
 // ------------------------------------------------------------------ x6 gram
 // out[b][i][j] = alpha * sum_n X_b[i][n] (w_b[n]) Y_b[j][n] at f32 accuracy on
@@ -730,8 +780,13 @@ static int gram_splits(int64_t N, int tiles) {
   return s;
 }
 
+constexpr int64_t kNarrowChunk = 2048;  // n per workgroup of gram_narrow_kernel
+static bool gram_narrow(int64_t MJ, int32_t tri) { return !tri && MJ <= 16; }
+
 extern "C" size_t mgp_gram_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t tri) {
   if (MI <= 0 || MJ <= 0 || N <= 0) return 16;
+  if (gram_narrow(MJ, tri))
+    return (size_t)((N + kNarrowChunk - 1) / kNarrowChunk) * (size_t)MI * (size_t)MJ * sizeof(double);
   const int nbi = (int)((MI + kGT - 1) / kGT), nbj = (int)((MJ + kGT - 1) / kGT);
   const int tiles = tri ? nbi * (nbi + 1) / 2 : nbi * nbj;
   return (size_t)gram_splits(N, tiles) * (size_t)MI * (size_t)MJ * sizeof(float);
@@ -753,6 +808,26 @@ extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y,
   if (MI == 0 || MJ == 0) return MGP_OK;
   if (!workspace || workspace_bytes < mgp_gram_workspace_bytes(MI, MJ, N, tri)) return MGP_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
+  if (gram_narrow(MJ, tri)) {
+    const int64_t nch = N > 0 ? (N + kNarrowChunk - 1) / kNarrowChunk : 0;
+    if (nch > 65535 || (MI + 15) / 16 > ((int64_t)1 << 31)) return MGP_ERR_UNSUPPORTED;
+    double* part = (double*)workspace;
+    if (nch == 0) {
+      int st = hip_status(hipMemsetAsync(part, 0, MI * MJ * sizeof(double), s));
+      if (st) return st;
+    } else if (MJ <= 8) {
+      hipLaunchKernelGGL(gram_narrow_kernel<8>, dim3((unsigned)((MI + 31) / 32), (unsigned)nch), dim3(256), 0, s, X,
+                         ldx, MI, Y, ldy, MJ, N, kNarrowChunk, part);
+    } else {
+      hipLaunchKernelGGL(gram_narrow_kernel<16>, dim3((unsigned)((MI + 15) / 16), (unsigned)nch), dim3(256), 0, s,
+                         X, ldx, MI, Y, ldy, MJ, N, kNarrowChunk, part);
+    }
+    int st = launch_status();
+    if (st) return st;
+    hipLaunchKernelGGL(gram_narrow_fold_kernel, dim3((unsigned)((MI * MJ + 255) / 256)), dim3(256), 0, s, part,
+                       (int)(nch > 0 ? nch : 1), MI, MJ, alpha, out, ldo);
+    return launch_status();
+  }
   const int nbi = (int)((MI + kGT - 1) / kGT), nbj = (int)((MJ + kGT - 1) / kGT);
   const int tiles = tri ? nbi * (nbi + 1) / 2 : nbi * nbj;
   const int nsplit = N > 0 ? gram_splits(N, tiles) : 1;

@@ -235,3 +235,21 @@ def test_gram_f16_rows(device, MI, MJ, N, B, mode):
         ref = torch.tril(ref) + torch.tril(ref, -1).transpose(1, 2)
     got = to_np(got).reshape(B, MI, -1)[:, :, :MJ]
     assert normwise(got, ref.numpy()) < 4e-6
+
+
+@pytest.mark.parametrize("MI,MJ,N,tri", [(1024, 8, 65536, False), (300, 16, 5000, False), (77, 5, 3001, False),
+                                         (40, 3, 100, False), (200, 200, 4000, True), (130, 70, 777, False)])
+def test_gram_f32(device, MI, MJ, N, tri):
+    """mgp_gram (X Y^T over N, float32): the narrow lane-strided path for MJ <= 16
+    (g_q_mu = A G_mu^T) and the f32-MFMA tiles otherwise, against float64."""
+    from modulatedgps_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(MI * 3 + N)
+    X = torch.randn(MI, N, generator=g)
+    Y = X[:MJ] if tri else torch.randn(MJ, N, generator=g)
+    Xd = ops.padded(MI, N, device).copy_(X.to(device))
+    Yd = ops.padded(MJ, N, device).copy_(Y.to(device))
+    got = ops.gram(Xd, Yd, N=N, alpha=-0.5, tri=tri)
+    ref = -0.5 * X.double() @ Y.double().T
+    if tri:
+        ref = torch.tril(ref)
+    assert normwise(to_np(got)[:, :MJ], ref.numpy()) < 2e-6
