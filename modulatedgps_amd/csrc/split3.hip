@@ -558,6 +558,177 @@ __global__ __launch_bounds__(256, 2) void grad_a_s_kernel(const bf16x8* __restri
   }
 }
 
+// B-b on split-f16 images (grad_a_s_kernel<true> restated for LDS economy):
+// gA = 2 sum_k (S_k A) diag(Gv_k) + gA0.  Item = (row tile t of 128, column tile
+// tn of 128) as grad_a_s_kernel, but each wave owns a 64 x 64 quarter (row half
+// wr = w / 2, column half wc = w % 2: 2 sub-tiles x 2 column blocks), so a T
+// fragment read from LDS feeds two column blocks, and two experts run per pass
+// of the main loop, sharing every B fragment (A's image).  Per wave and k-step:
+// 8 LDS reads, 4 B loads, 24 MFMAs (grad_a_s_kernel: 8 LDS reads and 2 B loads
+// per 12) -- half the LDS bytes per MFMA, which bound that kernel.  Odd K: the
+// last pass pairs the last expert with itself at weight 0.
+__global__ __launch_bounds__(256, 2) void grad_a_s_f16_kernel(const bf16x8* __restrict__ Sfr, uint32_t s_bytes,
+                                                             const bf16x8* __restrict__ Afr, uint32_t afr_bytes,
+                                                             int nmk, int nTn, int K, int64_t M, int64_t N,
+                                                             const float* __restrict__ Gv, int64_t ldg,
+                                                             const float* __restrict__ gA0, int64_t ld0,
+                                                             bf16x8* __restrict__ gAfr,
+                                                             const float* __restrict__ s_bound,
+                                                             const float* __restrict__ a_bound) {
+  __shared__ bf16x8 sL[2][2][4 * 3 * 64];  // [stage][expert of the pair][sub-tile][plane][lane]
+  const int nT = nmk / 8, nmb = nmk / 2;
+  int t, tn;
+  col_major_item(blockIdx.x, nT, nTn, t, tn);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int64_t nbw = 4 * (int64_t)tn + 2 * wc;  // the wave's first column block
+  int64_t ncol[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) ncol[c] = 32 * (nbw + c) + (lane & 31);
+  const float unscale = ldexpf(1.f, -(img_exp(*s_bound) + img_exp(*a_bound)));
+  const __amdgpu_buffer_rsrc_t rT = img_rsrc(Sfr, s_bytes), rB = img_rsrc(Afr, afr_bytes);
+  const uint32_t sexp = (uint32_t)nmb * (uint32_t)nmk * 3u * kFragBytes;  // one expert's S image
+  const uint32_t tb = (uint32_t)(4 * t * nmk) * 3u * kFragBytes;
+  const uint32_t sB0 = (uint32_t)(nbw * nmk) * 3u * kFragBytes, sBc = (uint32_t)nmk * 3u * kFragBytes;
+  const uint32_t vB = 16u * lane;
+  // T stage units (both experts): e = tid + 256 s -> sub-tile e / 128, plane (e / 64) % 2
+  uint32_t vT[2];
+  int dT[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int e = tid + 256 * s2, i = e / 128, p = (e / 64) % 2;
+    vT[s2] = (uint32_t)((i * nmk * 192 + p * 64 + (e & 63)) * 16);
+    dT[s2] = (3 * i + p) * 64 + (e & 63);
+  }
+  floatx16 out[2][2];
+#pragma unroll
+  for (int il = 0; il < 2; ++il)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) out[il][c][e] = 0.f;
+
+  for (int k = 0; k < K; k += 2) {
+    const int k1 = k + 1 < K ? k + 1 : k;
+    const uint32_t tb0 = (uint32_t)k * sexp + tb, tb1 = (uint32_t)k1 * sexp + tb;
+    floatx16 acc0[2][2], acc1[2][2];
+#pragma unroll
+    for (int il = 0; il < 2; ++il)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          acc0[il][c][e] = 0.f;
+          acc1[il][c][e] = 0.f;
+        }
+    auto load_b = [&](bf16x8 (&b)[2][3], int mk) {
+      const uint32_t o = (uint32_t)mk * 3u * kFragBytes;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) b[c][p] = ld_frag(rB, vB, sB0 + c * sBc + o + p * kFragBytes);
+    };
+    auto load_t = [&](u32x4v (&st)[4], int mk) {
+      const uint32_t o = (uint32_t)mk * 192u * 16u;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        st[s2] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s2], tb0 + o, 0);
+        st[2 + s2] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s2], tb1 + o, 0);
+      }
+    };
+    auto store_t = [&](int buf, const u32x4v (&st)[4]) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        reinterpret_cast<u32x4v*>(sL[buf][0])[dT[s2]] = st[s2];
+        reinterpret_cast<u32x4v*>(sL[buf][1])[dT[s2]] = st[2 + s2];
+      }
+    };
+    auto compute = [&](int buf, const bf16x8 (&b)[2][3]) {
+#pragma unroll
+      for (int il = 0; il < 2; ++il) {
+        const int i = 2 * wr + il;
+        bf16x8 a0[3], a1[3];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          a0[p] = sL[buf][0][(i * 3 + p) * 64 + lane];
+          a1[p] = sL[buf][1][(i * 3 + p) * 64 + lane];
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc0[il][c] = mfma_fmt<2, true>(a0, b[c], acc0[il][c]);
+          acc1[il][c] = mfma_fmt<2, true>(a1, b[c], acc1[il][c]);
+        }
+      }
+    };
+    bf16x8 b0[2][3], b1[2][3];
+    u32x4v st[4];
+    load_t(st, 0);
+    load_b(b0, 0);
+    store_t(0, st);
+    __syncthreads();
+#pragma nounroll
+    for (int mk = 0; mk < nmk; mk += 2) {
+      load_t(st, mk + 1);
+      load_b(b1, mk + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      store_t(1, st);
+      __syncthreads();
+      const int m2 = mk + 2 < nmk ? mk + 2 : nmk - 1;  // after the last pair: harmless reload
+      load_t(st, m2);
+      load_b(b0, m2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      store_t(0, st);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float g0 = ncol[c] < N ? Gv[(int64_t)k * ldg + ncol[c]] * unscale : 0.f;
+      const float g1 = (k + 1 < K && ncol[c] < N) ? Gv[(int64_t)(k + 1) * ldg + ncol[c]] * unscale : 0.f;
+#pragma unroll
+      for (int il = 0; il < 2; ++il)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          out[il][c][e] = fmaf(g1, acc1[il][c][e], fmaf(g0, acc0[il][c][e], out[il][c][e]));
+    }
+  }
+
+  // gA = 2 out + gA0, stored as the split image (bf16 x6, for B-d)
+  const int64_t i0 = 128 * (int64_t)t;
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)gA0, (short)0, (int)(uint32_t)(M * ld0 * 4), 0x00020000);
+  const uint32_t soff = (uint32_t)((i0 * ld0 + 128 * (int64_t)tn) * 4), ld32 = (uint32_t)ld0;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int nl = 32 * (2 * wc + c) + (lane & 31);
+    const bool ok = ncol[c] < N;
+#pragma unroll
+    for (int il = 0; il < 2; ++il) {
+      const int i = 2 * wr + il;
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
+        const float a0 = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
+        v[e] = ok ? fmaf(2.f, out[il][c][e], a0) : 0.f;  // rows >= M read 0 (outside the resource)
+      }
+      const int64_t mk = 8 * (int64_t)t + 2 * i;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float u[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[j] = v[8 * s2 + j];
+        store_split(gAfr + (((nbw + c) * nmk + mk + s2) * 3) * 64 + lane, u);
+      }
+    }
+  }
+}
+
 // B-d: gKuf = L^-T gA = Linv^T gA as f32 [M][ld]; T image = Linv (lower in
 // (k, i)), B image = gA; items and main loop as K5 (one "expert").
 __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restrict__ gAfr,
@@ -1324,9 +1495,9 @@ static int conditional_backward(
                        nmk, 2 * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, (const float*)trailer(Sfr, lower_planes(M, K)),
                        (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)));
   else if (f16)
-    hipLaunchKernelGGL(grad_a_s_kernel<true>, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
-                       (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes, nmk, 2 * nTn, K,
-                       M, N, Gv, ldg, gA0, ldn, gAfr, (const float*)trailer(Sfr, lower_planes(M, K)),
+    hipLaunchKernelGGL(grad_a_s_f16_kernel, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
+                       (uint32_t)lower_planes(M, K), (const bf16x8*)Afr, (uint32_t)afr_bytes, nmk, 2 * nTn, K, M, N,
+                       Gv, ldg, gA0, ldn, gAfr, (const float*)trailer(Sfr, lower_planes(M, K)),
                        (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)));
   else
     hipLaunchKernelGGL(grad_a_s_kernel<false>, dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
