@@ -776,11 +776,21 @@ __device__ __forceinline__ void trsm_stats_x6_item(
   float a_scale = 1.f;
   if constexpr (F16OUT) a_scale = ldexpf(1.f, img_exp(sqrtf(*a_var)));
   // q_mu rows of this row tile -> LDS [128][KMAX] before the main loop (whose
-  // barriers publish it), so the epilogue never waits on a global load
+  // barriers publish it), so the epilogue never waits on a global load.  F16OUT:
+  // also max |q_mu| of the tile (sQ[128 KMAX], as float bits; the caller zeroes
+  // it), the power-of-two scale of the split q_mu operand of the stats MFMAs
   if (stats) {
+    float qmax = 0.f;
     for (int idx = threadIdx.x; idx < 128 * KMAX; idx += 256) {
       const int r = idx / KMAX, kk = idx % KMAX;
-      sQ[idx] = (i0 + r < M && kk < K) ? q_mu[(i0 + r) * ldq + kk] : 0.f;
+      const float q = (i0 + r < M && kk < K) ? q_mu[(i0 + r) * ldq + kk] : 0.f;
+      sQ[idx] = q;
+      qmax = fmaxf(qmax, fabsf(q));
+    }
+    if constexpr (F16OUT) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+      if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(sQ + 128 * KMAX), __float_as_uint(qmax));
     }
   }
   floatx16 acc[4][2];
@@ -801,6 +811,85 @@ __device__ __forceinline__ void trsm_stats_x6_item(
   // contribution to the stats of 64-row stats tile i / 2 (stats[st][0][n] = sum A^2,
   // stats[st][1 + kk][n] = sum A q_mu[., kk]); acc[i] dies after its sub-tile, which
   // keeps the live set to the remaining accumulators + 2 (1 + KMAX) sums (no spills)
+  if constexpr (F16OUT) {
+    // ---- split-f16: the A image, and the stats q_mu^T A on the matrix cores --
+    // per 16-row k-step, the image fragments of acc[i][c] (B operand, k = rows)
+    // times the split q_mu fragment (A operand: rows kk < K, k = the same 16
+    // rows, from sQ) into sq[c] (32 x 32, rows kk); sum A^2 stays VALU.  Stats
+    // tile st = 2 t + i / 2 (64 rows) as the VALU path.
+    const int qe = img_exp(__uint_as_float(reinterpret_cast<const unsigned int*>(sQ)[128 * KMAX]));
+    const float q_scale = ldexpf(1.f, qe), s_unscale = ldexpf(1.f, -(qe + img_exp(sqrtf(*a_var))));
+    const int r = lane & 31, h = lane >> 5;
+    floatx16 sq[2];
+    float a2[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if ((i & 1) == 0) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          a2[c] = 0.f;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sq[c][e] = 0.f;
+        }
+      }
+      const int64_t mk = 8 * (int64_t)t + 2 * i;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 qf[3];
+        if (stats) {
+          halfx8 qh, ql;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float x = (r < K ? sQ[(32 * i + 16 * s2 + kperm(h, j)) * KMAX + (r < KMAX ? r : 0)] : 0.f) * q_scale;
+            const _Float16 xh = (_Float16)x;
+            qh[j] = xh;
+            ql[j] = (_Float16)(x - (float)xh);
+          }
+          qf[0] = __builtin_bit_cast(bf16x8, qh);
+          qf[1] = __builtin_bit_cast(bf16x8, ql);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int64_t nb = 8 * (int64_t)tn + 2 * w + c;
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j];
+          store_split_f16<X8OUT>(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v, a_scale, Af32 != nullptr);
+          if (stats) {
+            halfx8 vh, vl;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float x = v[j] * a_scale;
+              const _Float16 xh = (_Float16)x;
+              vh[j] = xh;
+              vl[j] = (_Float16)(x - (float)xh);
+              a2[c] = fmaf(v[j], v[j], a2[c]);
+            }
+            const bf16x8 bf[3] = {__builtin_bit_cast(bf16x8, vh), __builtin_bit_cast(bf16x8, vl), bf16x8{}};
+            sq[c] = mfma_fmt<2, true>(qf, bf, sq[c]);
+          }
+        }
+      }
+      if (stats && (i & 1)) {
+        const int64_t st = 2 * (int64_t)t + (i >> 1);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int64_t n = (int64_t)tn * kX6BN + 64 * w + 32 * c + (lane & 31);
+          const float s_a2 = a2[c] + __shfl_xor(a2[c], 32, 64);
+          if (n < N && 64 * st < M) {
+            float* dst = stats + st * (K + 1) * lds_ + n;
+            if (lane < 32) dst[0] = s_a2;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int kk = acc_row(e, lane);
+              if (kk < K) dst[(int64_t)(1 + kk) * lds_] = sq[c][e] * s_unscale;
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
   float a2[2], qm[2][KMAX];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -813,10 +902,7 @@ __device__ __forceinline__ void trsm_stats_x6_item(
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j];
-        if constexpr (F16OUT)
-          store_split_f16<X8OUT>(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v, a_scale, Af32 != nullptr);
-        else
-          store_split(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v);
+        store_split(Afr + ((nb * nmk + mk + s2) * 3) * 64 + lane, v);
       }
     }
     if (!stats) continue;
@@ -875,16 +961,20 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
     const float* __restrict__ a_var, float* __restrict__ a_bound, const float* __restrict__ t_bound = nullptr,
     const float* __restrict__ k_bound = nullptr) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
-  __shared__ float sQ[128 * KMAX];
+  __shared__ float sQ[128 * KMAX + 1];  // + the tile's max |q_mu| (F16OUT)
   const int nT = nmk / 8, nP = (nT + 1) / 2;
   int p, tn;
   if constexpr (F16OUT)
     if (blockIdx.x == 0 && threadIdx.x == 0) *a_bound = sqrtf(*a_var);
   col_major_item(blockIdx.x, nP, nTn, p, tn);
+  if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
+  __syncthreads();
   trsm_stats_x6_item<KMAX, F16OUT, F16IN, X8OUT>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu,
                                           ldq, K, Afr, stats, lds_, Af32, lda, a_var, t_bound, k_bound);
   if (nT - 1 - p == p) return;
   __syncthreads();  // the epilogue's sQ reads before the next item's sQ stores
+  if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
+  __syncthreads();
   trsm_stats_x6_item<KMAX, F16OUT, F16IN, X8OUT>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K,
                                           Afr, stats, lds_, Af32, lda, a_var, t_bound, k_bound);
 }

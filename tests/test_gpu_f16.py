@@ -101,7 +101,9 @@ def test_expert_conditional_f16_accuracy(device):
                                        cross="f8")
     errs["f16x8 chain"] = (normwise(to_np(fm).T, mu_ref), normwise(to_np(fv).T, var_ref))
     print("fmean / fvar normwise error vs float64:", errs)
-    assert errs["f16"][0] == errs["x6"][0]            # fmean comes from K4's stats in both
+    # fmean comes from K4's stats: float32 VALU sums (x6) vs split-f16 MFMAs (f16),
+    # both float32-class (measured 1.016e-6 vs 1.011e-6)
+    assert errs["f16"][0] < 1.05 * errs["x6"][0]
     assert errs["f16"][1] < 1e-4
     assert errs["f16"][1] < 1.5 * errs["x6"][1]        # measured 7.34e-7 vs x6 7.31e-7
     assert errs["f16 chain"][0] < 1e-4 and errs["f16 chain"][1] < 1e-4
