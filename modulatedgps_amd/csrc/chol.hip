@@ -893,22 +893,24 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
 // all in float64 (M^3 work; Kuu is badly conditioned).  dgemm: C = op(A) op(B)
 // on v_mfma_f64_16x16x4_f64: 64 x 64 tile per workgroup (4 waves x 32 x 32 =
 // 2 x 2 MFMA blocks each), 16-deep LDS chunks.
-template <bool TA, bool TB>
+template <bool TA, bool TB, int BN = 64>
 __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A, int64_t lda,
                                                     const double* __restrict__ B, int64_t ldb,
                                                     double* __restrict__ C, int64_t ldc, int64_t M) {
-  __shared__ double sa[64][17], sb[16][65];  // sa[i][k] = op(A), sb[k][j] = op(B)
+  // 64 x BN tile; wave w: rows wi .. wi + 31, columns wj .. wj + BN / 2 - 1 (NB 16-wide blocks)
+  constexpr int NB = BN / 32, LB = BN / 16;  // MFMA column blocks per wave, B loads per thread
+  __shared__ double sa[64][17], sb[16][BN + 1];  // sa[i][k] = op(A), sb[k][j] = op(B)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wi = (w >> 1) * 32, wj = (w & 1) * 32;
-  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
-  doublex4 acc[2][2];
+  const int wi = (w >> 1) * 32, wj = (w & 1) * (BN / 2);
+  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * BN;
+  doublex4 acc[2][NB];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = doublex4{0.0, 0.0, 0.0, 0.0};
-  // chunk k0 .. k0 + 15: thread loads 4 elements of each operand (coalesced along
-  // the contiguous index), one chunk ahead in registers
-  double ra[4], rb[4];
+    for (int b = 0; b < NB; ++b) acc[a][b] = doublex4{0.0, 0.0, 0.0, 0.0};
+  // chunk k0 .. k0 + 15: thread loads 4 elements of op(A) and LB of op(B) (coalesced
+  // along the contiguous index), one chunk ahead in registers
+  double ra[4], rb[LB];
   auto load = [&](int64_t k0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -916,7 +918,11 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A
       const int r_a = TA ? idx % 64 : idx / 16, k_a = TA ? idx / 64 : idx % 16;
       const int64_t ia = i0 + r_a, kA = k0 + k_a;
       ra[q] = (ia < M && kA < M) ? (TA ? A[kA * lda + ia] : A[ia * lda + kA]) : 0.0;
-      const int c_b = TB ? idx / 16 : idx % 64, k_b = TB ? idx % 16 : idx / 64;
+    }
+#pragma unroll
+    for (int q = 0; q < LB; ++q) {
+      const int idx = tid + 256 * q;
+      const int c_b = TB ? idx / 16 : idx % BN, k_b = TB ? idx % 16 : idx / BN;
       const int64_t jb = j0 + c_b, kB = k0 + k_b;
       rb[q] = (jb < M && kB < M) ? (TB ? B[jb * ldb + kB] : B[kB * ldb + jb]) : 0.0;
     }
@@ -926,7 +932,11 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A
     for (int q = 0; q < 4; ++q) {
       const int idx = tid + 256 * q;
       sa[TA ? idx % 64 : idx / 16][TA ? idx / 64 : idx % 16] = ra[q];
-      sb[TB ? idx % 16 : idx / 64][TB ? idx / 16 : idx % 64] = rb[q];
+    }
+#pragma unroll
+    for (int q = 0; q < LB; ++q) {
+      const int idx = tid + 256 * q;
+      sb[TB ? idx % 16 : idx / BN][TB ? idx / 16 : idx % BN] = rb[q];
     }
   };
   load(0);
@@ -936,23 +946,22 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A
     if (k0 + 16 < M) load(k0 + 16);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      double av[2], bv[2];
+      double av[2], bv[NB];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        av[t] = sa[wi + 16 * t + (lane & 15)][4 * ks + (lane >> 4)];
-        bv[t] = sb[4 * ks + (lane >> 4)][wj + 16 * t + (lane & 15)];
-      }
+      for (int t = 0; t < 2; ++t) av[t] = sa[wi + 16 * t + (lane & 15)][4 * ks + (lane >> 4)];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) bv[t] = sb[4 * ks + (lane >> 4)][wj + 16 * t + (lane & 15)];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
     }
     __syncthreads();
   }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t i = i0 + wi + 16 * a + (lane >> 4) + 4 * r, j = j0 + wj + 16 * b + (lane & 15);
@@ -1126,14 +1135,14 @@ extern "C" int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT
   double* Li = Ld + M * M;   // Linv = LinvT^T
   double* G = Li + M * M;
   double* T = G + M * M;
-  const dim3 eg((unsigned)((M * M + 255) / 256)), gg((unsigned)((M + 63) / 64), (unsigned)((M + 63) / 64));
+  const dim3 eg((unsigned)((M * M + 255) / 256)), gg((unsigned)((M + 31) / 32), (unsigned)((M + 63) / 64));  // 64 x 32 tiles: 2 x the workgroups of 64 x 64 (measured faster at M = 1024)
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, L, ldl, Ld, M, nullptr, (int64_t)0);
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 1, LinvT, ldli, Li, M, nullptr, (int64_t)0);
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, gL, ldg, G, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL((dgemm_kernel<true, false>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M);      // L^T gL
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M);      // L^T gL
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 2, nullptr, (int64_t)0, T, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL((dgemm_kernel<false, false>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M);     // P Linv
-  hipLaunchKernelGGL((dgemm_kernel<true, false>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M);      // Linv^T (.)
+  hipLaunchKernelGGL((dgemm_kernel<false, false, 32>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M);     // P Linv
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M);      // Linv^T (.)
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 3, nullptr, (int64_t)0, T, M, gKuu, ldo);
   return launch_status();
 }

@@ -609,7 +609,6 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
 #pragma unroll
         for (int tb = 0; tb < 2; ++tb) acc[ta][tb] = mfma_fmt<2, true>(a, c[tb], acc[ta][tb]);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
   };
 

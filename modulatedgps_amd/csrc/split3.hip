@@ -1408,6 +1408,8 @@ extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y,
                         int64_t N, float alpha, int32_t tri, float* out, int64_t ldo, void* workspace,
                         size_t workspace_bytes, mgp_stream_t stream);
 
+constexpr int kRowSumChunks = 32;  // column chunks of row_sums_kernel
+
 namespace {
 struct CondBwdWs {  // workspace carve-up (256-B aligned pieces)
   size_t sfr, ga0, gafr, lifr, P, LT, part, bnd, gram, total;
@@ -1425,7 +1427,7 @@ CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
   w.lifr = o; o += al256(mgp_x6_lower_bytes(M, 1));
   w.P = o;    o += al256((size_t)K * M * ldm * 4);
   w.LT = o;   o += al256((size_t)K * M * ldm * 4);
-  w.part = o; o += al256((size_t)K * 8);
+  w.part = o; o += al256((size_t)K * kRowSumChunks * 8);  // row_sums partials
   w.bnd = o;  o += 256;  // split-f16 bound: max |Gv|
   w.gram = o;
   size_t g = mgp_gram_x6_workspace_bytes(M, M, N, K, 2);
@@ -1439,15 +1441,18 @@ CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
 }
 }  // namespace
 
-// part[k] = sum_n x[k][n] (one block per row), then out = sum_k part[k] (fixed order).
-__global__ __launch_bounds__(1024) void row_sums_kernel(const float* __restrict__ x, int64_t cols, int64_t ld,
-                                                        double* __restrict__ part) {
+// part[k][c] = sum of x[k][n] over column chunk c (grid: rows x kRowSumChunks), then
+// out = sum of all parts (fixed order).
+__global__ __launch_bounds__(256) void row_sums_kernel(const float* __restrict__ x, int64_t cols, int64_t ld,
+                                                       double* __restrict__ part) {
   __shared__ double scratch[16];
   const float* row = x + (int64_t)blockIdx.x * ld;
+  const int64_t per = (cols + kRowSumChunks - 1) / kRowSumChunks;
+  const int64_t nb = (int64_t)blockIdx.y * per, ne = nb + per < cols ? nb + per : cols;
   double v = 0.0;
-  for (int64_t n = threadIdx.x; n < cols; n += 1024) v += (double)row[n];
+  for (int64_t n = nb + threadIdx.x; n < ne; n += 256) v += (double)row[n];
   v = mgp::block_sum<double>(v, scratch);
-  if (threadIdx.x == 0) part[blockIdx.x] = v;
+  if (threadIdx.x == 0) part[blockIdx.x * kRowSumChunks + blockIdx.y] = v;
 }
 
 __global__ void sum_parts_kernel(const double* __restrict__ part, int rows, double* __restrict__ out) {
@@ -1633,8 +1638,8 @@ static int conditional_backward(
   if (st) return st;
   st = mgp_gram(A, lda, M, Gmu, ldg, K, N, 1.f, 0, g_q_mu, ldgq, gws, gwsb, stream);
   if (st) return st;
-  hipLaunchKernelGGL(row_sums_kernel, dim3((unsigned)K), dim3(1024), 0, s, Gv, N, ldg, part);
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1), 0, s, part, (int)K, g_var);
+  hipLaunchKernelGGL(row_sums_kernel, dim3((unsigned)K, kRowSumChunks), dim3(256), 0, s, Gv, N, ldg, part);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1), 0, s, part, (int)K * kRowSumChunks, g_var);
   return launch_status();
 }
 

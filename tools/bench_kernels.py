@@ -79,6 +79,9 @@ def main():
                           ops._lib.load().mgp_gram_x6_workspace_bytes(M, M, N, 1, 1)), dtype=torch.uint8, device=dev)
     gbnd = (A32[:, :N].abs().max().reshape(1), A32[:, :N].abs().max().reshape(1), Gv[:, :N].abs().max().reshape(1))
     arows = ops.split_rows_f16(A32, gbnd[0], N=N)
+    Lc, LinvTc, _ = ops.kuu_potrf_trtri([Z], [var], [lsc], 1e-6, want_L=True)
+    gLc = ops.padded(M, M, dev)
+    gLc.copy_(torch.tril(torch.randn(M, M, device=dev, generator=g)))
     cb = ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N)
     wsc = torch.empty(ops.conditional_backward_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev)
     A32h = ops.padded(M, N, dev)   # the f16 chain's training K4: f16 A image + f32 A
@@ -120,6 +123,7 @@ def main():
         "gram_f16_rows_P": lambda: ops.gram_x6(A32, A32, Gv, mode=2, N=N, out=P, workspace=wsg, bounds=gbnd,
                                                x_rows=arows),
         "rbf_bwd": lambda: ops.rbf_backward(X, Z, var, lsc, gK),
+        "chol_bwd": lambda: ops.chol_backward(Lc[0], LinvTc[0], gLc),
         "cond_bwd_x6": lambda: ops.conditional_backward_x6(Afr, A32, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
                                                            out=cb, workspace=wsc),
         "cond_bwd_f16": lambda: ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
