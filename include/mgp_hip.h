@@ -267,6 +267,19 @@ int mgp_expert_conditional_f16x8(const void* Afr, size_t afr_bytes, const void* 
                                  const float* stats, int64_t lds, const float* variance, int64_t M,
                                  int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
                                  void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+/* Training forward (split-f16): mgp_expert_conditional_f16 that also writes
+ * C_k = L_k^T A of every expert as a split-f16 B-layout image (Cfr, at least
+ * mgp_c_images_bytes(M, N, K) bytes), for mgp_conditional_backward_f16c.  colmax:
+ * DEVICE max column 2-norm of tril(q_sqrt) (mgp_colnorm_max); the images are
+ * scaled by the bound colmax * sqrt(variance) >= |C|. */
+size_t mgp_c_images_bytes(int64_t M, int64_t N, int32_t K);
+int mgp_colnorm_max(const float* q_sqrt, int64_t ldq, int64_t strideq, int64_t M, int32_t K, float* out,
+                    mgp_stream_t stream);
+int mgp_expert_conditional_f16c(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                const float* stats, int64_t lds, const float* variance, int64_t M,
+                                int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                                void* workspace, size_t workspace_bytes, void* Cfr, size_t cfr_bytes,
+                                const float* colmax, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- backward of K1-K5
  * Gram products over the data dimension (float32 MFMA, deterministic split-K):
@@ -360,6 +373,18 @@ int mgp_conditional_backward_f16x8(const void* Afr, size_t afr_bytes, const floa
                                  int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm,
                                  int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
                                  mgp_stream_t stream);
+/* mgp_conditional_backward_f16 with the forward's C_k images (mgp_expert_conditional_f16c
+ * on the same Afr, q_sqrt and colmax; l_bound = DEVICE bound of that call's Lfr
+ * image): the q_sqrt-weighted part of gA as 2 sum_k L_k C_k diag(Gv_k) on the
+ * triangular L_k -- half the products of the S_k = L_k L_k^T form, and no S_k. */
+int mgp_conditional_backward_f16c(const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+                                  const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq,
+                                  const float* LinvT, int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg,
+                                  int64_t M, int64_t N, int32_t K, float* g_q_mu, int64_t ldgq, float* g_q_sqrt,
+                                  int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm,
+                                  int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes,
+                                  const void* Cfr, size_t cfr_bytes, const float* colmax, const float* l_bound,
+                                  mgp_stream_t stream);
 
 /* Reverse mode of Lm = chol(Kuu) (models.py:141): gKuu = sym(Lm^-T Phi(Lm^T gL) Lm^-1),
  * Phi = lower triangle with halved diagonal, in float64 from the float32 L,

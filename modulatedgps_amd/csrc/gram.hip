@@ -394,7 +394,8 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
             acc[ta][tb] = mfma_x6(a, c[tb], acc[ta][tb]);
         }
       }
-      __builtin_amdgcn_sched_barrier(0);  // keep the next k-step's fragment reads after these MFMAs
+      // x6: keep the next k-step's fragment reads after these MFMAs (registers)
+      if constexpr (!F16) __builtin_amdgcn_sched_barrier(0);
     }
   };
 

@@ -358,14 +358,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const void* p, uint32
 // ------------------------------------------------------------------ K5 (x6)
 // F16: split-f16 images (NPL = 2) scaled by 2^img_exp(*a_bound), 2^img_exp(*l_bound).
 // X8: their hi planes on f16 MFMA and cross terms on e4m3 MFMA (mfma_f8x).
-template <int NPL, bool F16 = false, bool X8 = false>
+// COUT (training, split-f16): C_k = L_k^T A itself is also written, as a split-f16
+// B-layout image per expert (Cfr + k cexp, scale 2^img_exp(bound), bound =
+// *colmax *a_bound (1 + 2^-10) >= |C|: |C[m'][n]| <= ||L_k[:, m']|| ||A[:, n]|| and
+// ||A[:, n]||^2 <= variance), for the backward's gA = 2 sum_k L_k (C_k diag(Gv_k)).
+template <int NPL, bool F16 = false, bool X8 = false, bool COUT = false>
 __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
                                                                 const bf16x8* __restrict__ Lfr,
                                                                 uint32_t afr_bytes, uint32_t lfr_bytes,
                                                                 int nmk, int nmb, int nTn, int K,
                                                                 int64_t N, float* __restrict__ part,
                                                                 int64_t ldp, const float* __restrict__ a_bound,
-                                                                const float* __restrict__ l_bound) {
+                                                                const float* __restrict__ l_bound,
+                                                                bf16x8* __restrict__ Cfr = nullptr, int64_t cexp = 0,
+                                                                const float* __restrict__ colmax = nullptr) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];  // 2 x 12 KiB: [row sub-tile][plane][lane]
   int t, tn, k;
   x6_item(blockIdx.x, nTn, K, t, tn, k);
@@ -376,6 +382,22 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   x6_mainloop<1, 2, NPL, F16, X8>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
               img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
+  if constexpr (COUT) {
+    const float cmul = ldexpf(1.f, img_exp(*colmax * *a_bound * 1.0009765625f) -
+                                       (img_exp(*a_bound) + img_exp(*l_bound)));
+    bf16x8* Ck = Cfr + (int64_t)k * cexp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j] * cmul;
+          store_split_f16(Ck + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + 2 * i + s2) * 3) * 64 + lane, v, 1.f);
+        }
+  }
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
   const int64_t nbase = (int64_t)tn * kX6BN + 64 * w + (lane & 31);
   float* dst = part + ((int64_t)k * nTp + t) * ldp;
@@ -729,6 +751,128 @@ __global__ __launch_bounds__(256, 2) void grad_a_s_f16_kernel(const bf16x8* __re
   }
 }
 
+// B-b from the forward's C images (split-f16 training, mgp_conditional_backward_f16c):
+// gA = 2 sum_k L_k (C_k diag(Gv_k)) + gA0 -- the triangular L_k instead of the full
+// S_k = L_k L_k^T, so half of grad_a_s's products, and no S_k build.  T = L_k's
+// image with rows m, k-steps over m' <= m (DIAG 2, mk < 8 t + 8), B = C_k's image
+// (one column sub-tile per wave).  A workgroup takes the row-tile pair (nT - 1 - p,
+// p) of a column tile for every expert in turn (K4's balancing): the pairs of a
+// column tile then do equal work per expert and stay in step on one XCD, so each
+// C_k column strip is read from HBM about once and served to the other pairs
+// from L2 (one row tile per workgroup: the light tiles ran ahead through the
+// experts and every strip came from HBM/MALL ~4.5 times).
+__device__ __forceinline__ void grad_a_c_store(const floatx16 (&out)[4][1], int t, int tn, int w, int lane,
+                                               int nmk, int64_t M, int64_t N, const float* __restrict__ gA0,
+                                               int64_t ld0, bf16x8* __restrict__ gAfr) {
+  const int64_t nb = 4 * (int64_t)tn + w;
+  const int64_t n = 32 * nb + (lane & 31);
+  const int64_t i0 = 128 * (int64_t)t;
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)gA0, (short)0, (int)(uint32_t)(M * ld0 * 4), 0x00020000);
+  const uint32_t soff = (uint32_t)((i0 * ld0 + 128 * (int64_t)tn) * 4), ld32 = (uint32_t)ld0;
+  const int nl = 32 * w + (lane & 31);
+  const bool ok = n < N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
+      const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
+      v[e] = ok ? fmaf(2.f, out[i][0][e], b0) : 0.f;  // rows >= M read 0 (outside the resource)
+    }
+    const int64_t mk = 8 * (int64_t)t + 2 * i;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = v[8 * s2 + j];
+      store_split(gAfr + ((nb * nmk + mk + s2) * 3) * 64 + lane, u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void grad_a_c_kernel(const bf16x8* __restrict__ Ltfr, uint32_t lt_bytes,
+                                                         const bf16x8* __restrict__ Cfr, int64_t cexp,
+                                                         uint32_t c_bytes, int nmk, int nTn, int K, int64_t M,
+                                                         int64_t N, const float* __restrict__ Gv, int64_t ldg,
+                                                         const float* __restrict__ gA0, int64_t ld0,
+                                                         bf16x8* __restrict__ gAfr,
+                                                         const float* __restrict__ l_bound,
+                                                         const float* __restrict__ a_bound,
+                                                         const float* __restrict__ colmax) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];
+  const int nT = nmk / 8, nmb = nmk / 2, nP = (nT + 1) / 2;
+  int p, tn;
+  col_major_item(blockIdx.x, nP, nTn, p, tn);
+  const int t1 = nT - 1 - p, t2 = p;  // t1 == t2: the middle tile of an odd nT, alone
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nb = 4 * (int64_t)tn + w;
+  const int64_t n = 32 * nb + (lane & 31);
+  floatx16 acc[4][1], out1[4][1], out2[4][1];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      out1[i][0][e] = 0.f;
+      out2[i][0][e] = 0.f;
+    }
+  const float unscale =
+      ldexpf(1.f, -(img_exp(*l_bound) + img_exp(*colmax * *a_bound * 1.0009765625f)));
+  for (int k = 0; k < K; ++k) {
+    const __amdgpu_buffer_rsrc_t rT = img_rsrc(Ltfr, lt_bytes), rB = img_rsrc(Cfr + (int64_t)k * cexp, c_bytes);
+    const float g = n < N ? Gv[(int64_t)k * ldg + n] * unscale : 0.f;
+    x6_mainloop<2, 1, 2, true>(acc, sL, rT, (uint32_t)(((int64_t)k * nmb + 4 * t1) * nmk) * 3u * kFragBytes, rB,
+                               (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, 8 * t1 + 8, nmk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) out1[i][0][e] = fmaf(g, acc[i][0][e], out1[i][0][e]);
+    if (t2 != t1) {
+      x6_mainloop<2, 1, 2, true>(acc, sL, rT, (uint32_t)(((int64_t)k * nmb + 4 * t2) * nmk) * 3u * kFragBytes, rB,
+                                 (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, 8 * t2 + 8, nmk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) out2[i][0][e] = fmaf(g, acc[i][0][e], out2[i][0][e]);
+    }
+  }
+  grad_a_c_store(out1, t1, tn, w, lane, nmk, M, N, gA0, ld0, gAfr);
+  if (t2 != t1) grad_a_c_store(out2, t2, tn, w, lane, nmk, M, N, gA0, ld0, gAfr);
+}
+
+// max over k, j of ||tril(q_sqrt[k])[:, j]||_2 -> *out (float bits, atomicMax; zeroed
+// beforehand).  Workgroup = (32 columns, expert k): thread (ty, tx) sums rows
+// ty, ty + 8, ... of column 32 blockIdx.x + tx (row-contiguous loads), LDS sums
+// the 8 partials, one atomic per workgroup.
+__global__ __launch_bounds__(256) void colnorm_max_kernel(const float* __restrict__ q, int64_t ldq, int64_t sq,
+                                                          int64_t M, unsigned int* __restrict__ out) {
+  __shared__ float part[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t j = (int64_t)blockIdx.x * 32 + tx;
+  const float* Q = q + (int64_t)blockIdx.y * sq;
+  float v = 0.f;
+  if (j < M) {
+#pragma unroll 8
+    for (int64_t i = ty; i < M; i += 8) {
+      const float x = i >= j ? Q[i * ldq + j] : 0.f;
+      v = fmaf(x, x, v);
+    }
+  }
+  part[ty][tx] = v;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float c = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) c += part[r][threadIdx.x];
+    c = sqrtf(c);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) c = fmaxf(c, __shfl_xor(c, off, 32));
+    if (threadIdx.x == 0) atomicMax(out, __float_as_uint(c));
+  }
+}
+
 // B-d: gKuf = L^-T gA = Linv^T gA as f32 [M][ld]; T image = Linv (lower in
 // (k, i)), B image = gA; items and main loop as K5 (one "expert").
 __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restrict__ gAfr,
@@ -1071,7 +1215,8 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
                               const float* stats, int64_t lds, const float* variance, int64_t M, int64_t N,
                               int32_t K, int planes, float* fmean, float* fvar, int64_t ldf, void* workspace,
                               size_t workspace_bytes, mgp_stream_t stream, bool f16 = false,
-                              bool x8 = false) {
+                              bool x8 = false, void* Cfr = nullptr, size_t cfr_bytes = 0,
+                              const float* colmax = nullptr) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!Lfr) return -3;
@@ -1104,11 +1249,22 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
                        (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N),                           \
                        (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N, part, ldp, a_bound,     \
                        l_bound);
+  if (Cfr) {  // training: + the C_k images (mgp_expert_conditional_f16c)
+    if (!f16 || x8 || planes != 2) return MGP_ERR_UNSUPPORTED;
+    if (!colmax) return -18;
+    const size_t cexp = cols_planes(M, N);
+    if (cfr_bytes < (size_t)K * cexp) return -17;
+    if (!aligned16(Cfr)) return MGP_ERR_ALIGN;
+    hipLaunchKernelGGL((expert_cond_x6_kernel<2, true, false, true>), grid, dim3(256), 0, s, (const bf16x8*)Afr,
+                       (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk,
+                       nmb, nTn, K, N, part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
+  } else {
   MGP_K5_CASE(3, false, false)
   MGP_K5_CASE(2, false, false)
   MGP_K5_CASE(1, false, false)
   MGP_K5_CASE(2, true, false)
   MGP_K5_CASE(2, true, true)
+  }
 #undef MGP_K5_CASE
   int st = launch_status();
   if (st) return st;
@@ -1373,6 +1529,39 @@ extern "C" int mgp_expert_conditional_f16(const void* Afr, size_t afr_bytes, con
                             workspace, workspace_bytes, stream, true);
 }
 
+// Training: mgp_expert_conditional_f16 that also writes C_k = L_k^T A per expert as a
+// split-f16 B-layout image (Cfr, mgp_c_images_bytes; colmax from mgp_colnorm_max
+// of q_sqrt), consumed by mgp_conditional_backward_f16c.
+extern "C" size_t mgp_c_images_bytes(int64_t M, int64_t N, int32_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 16;
+  return (size_t)K * cols_planes(M, N);
+}
+
+extern "C" int mgp_colnorm_max(const float* q_sqrt, int64_t ldq, int64_t strideq, int64_t M, int32_t K,
+                               float* out, mgp_stream_t stream) {
+  if (!q_sqrt) return -1;
+  if (ldq < M) return -2;
+  if (M < 0) return -4;
+  if (K < 1) return -5;
+  if (!out) return -6;
+  hipStream_t s = (hipStream_t)stream;
+  int st = hip_status(hipMemsetAsync(out, 0, sizeof(float), s));
+  if (st || M == 0) return st;
+  hipLaunchKernelGGL(colnorm_max_kernel, dim3((unsigned)((M + 31) / 32), (unsigned)K), dim3(256), 0, s, q_sqrt, ldq,
+                     strideq, M, (unsigned int*)out);
+  return launch_status();
+}
+
+extern "C" int mgp_expert_conditional_f16c(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
+                                           const float* stats, int64_t lds, const float* variance, int64_t M,
+                                           int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                                           void* workspace, size_t workspace_bytes, void* Cfr, size_t cfr_bytes,
+                                           const float* colmax, mgp_stream_t stream) {
+  if (!Cfr) return -16;
+  return expert_cond_planes(Afr, afr_bytes, Lfr, lfr_bytes, stats, lds, variance, M, N, K, 2, fmean, fvar, ldf,
+                            workspace, workspace_bytes, stream, true, false, Cfr, cfr_bytes, colmax);
+}
+
 // Split-f16 images with the X8 plane (mgp_split_lower_f16, mgp_split_cols_f16,
 // mgp_trsm_stats_f16x8): hi products on f16, cross terms on e4m3 (mfma_f8x).
 extern "C" int mgp_expert_conditional_f16x8(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
@@ -1501,7 +1690,8 @@ static int conditional_backward(
     int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
     float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
     float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream,
-    bool f16, bool x8 = false) {
+    bool f16, bool x8 = false, const void* Cfr = nullptr, size_t cfr_bytes = 0, const float* colmax = nullptr,
+    const float* l_bound = nullptr) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!A) return -3;
@@ -1546,6 +1736,19 @@ static int conditional_backward(
   const int nmk = (int)(Mp / 16), nmb = (int)(Mp / 32), nT = (int)(Mp / kX6BM);
   const int nTn = (int)(x6_np(N) / kX6BN);
   int st;
+  const bool cpath = f16 && !x8 && Cfr;  // B-b from the forward's C_k images
+  if (cpath) {
+    if (!colmax || !l_bound) return -32;
+    if (cfr_bytes < mgp_c_images_bytes(M, N, K)) return -31;
+    if (!aligned16(Cfr)) return MGP_ERR_ALIGN;
+    // L_k's image (rows m, k-steps over m' <= m) into the S image's space; Linv's image
+    const int64_t nfrag = (int64_t)K * nmb * nmk, nf1 = (int64_t)nmb * nmk;
+    hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
+                       ldqs, strideq, M, nmb, nmk, nfrag, Sfr, l_bound);
+    hipLaunchKernelGGL((split_tri_kernel<true, true>), dim3((unsigned)((nf1 + 3) / 4)), dim3(256), 0, s, LinvT, ldl,
+                       (int64_t)0, M, nmb, nmk, nf1, LIfr);
+    if ((st = launch_status())) return st;
+  } else {
   // 1. S_k = L_k L_k^T (x6 gram over M of tril(q_sqrt), into the LT buffer) and its
   //    full split images; the image of Linv (T operand of B-d)
   hipLaunchKernelGGL(tril_copy_kernel, dim3((unsigned)((M * M + 255) / 256), (unsigned)K), dim3(256), 0, s, q_sqrt,
@@ -1568,6 +1771,7 @@ static int conditional_backward(
                        (int64_t)0, M, nmb, nmk, nf1, LIfr);
     if ((st = launch_status())) return st;
   }
+  }
   // 2. gA0 = q_mu G_mu - 2 A sum_k Gv_k
   {
     const int rows = 128;
@@ -1583,8 +1787,13 @@ static int conditional_backward(
                          rows, gA0, ldn);
     if ((st = launch_status())) return st;
   }
-  // 3. gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0
-  if (f16 && x8)
+  // 3. gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0  (C path: 2 sum_k L_k C_k diag(Gv_k) + gA0)
+  if (cpath)
+    hipLaunchKernelGGL(grad_a_c_kernel, dim3((unsigned)((nT + 1) / 2 * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
+                       (uint32_t)lower_planes(M, K), (const bf16x8*)Cfr, (int64_t)(cols_planes(M, N) / 16),
+                       (uint32_t)cols_planes(M, N), nmk, 2 * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, l_bound,
+                       (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)), colmax);
+  else if (f16 && x8)
     hipLaunchKernelGGL((grad_a_s_kernel<true, true>), dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s,
                        (const bf16x8*)Sfr, (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes,
                        nmk, 2 * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, (const float*)trailer(Sfr, lower_planes(M, K)),
@@ -1665,6 +1874,22 @@ extern "C" int mgp_conditional_backward_f16(
   return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
                               N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
                               workspace_bytes, stream, true);
+}
+
+// mgp_conditional_backward_f16 with the forward's C_k images (mgp_expert_conditional_f16c
+// with the same Afr, q_sqrt and colmax; l_bound = the bound of its Lfr image):
+// B-b as 2 sum_k L_k C_k diag(Gv_k), no S_k = L_k L_k^T.
+extern "C" int mgp_conditional_backward_f16c(
+    const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+    const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+    int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
+    float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
+    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, const void* Cfr,
+    size_t cfr_bytes, const float* colmax, const float* l_bound, mgp_stream_t stream) {
+  if (!Cfr) return -30;
+  return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
+                              N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
+                              workspace_bytes, stream, true, false, Cfr, cfr_bytes, colmax, l_bound);
 }
 
 // Afr from mgp_trsm_stats_f16x8 with the f32 A (all three planes): S_k A on f16 hi

@@ -40,7 +40,12 @@ import torch
 
 from . import ops
 from .broadcasting_lik import BroadcastingLikelihood
-from .config import conditional_mode, default_device, default_jitter, expert_planes, forward_image_format
+from .config import (conditional_mode, default_device, default_jitter, expert_cross, expert_planes,
+                     forward_image_format)
+
+# Largest set of C_k = L_k^T A images (per layer) the training step keeps for the
+# backward (mgp_conditional_backward_f16c); beyond it the backward rebuilds S_k = L_k L_k^T.
+C_IMAGES_MAX_BYTES = 8 << 30
 from .kernels import SquaredExponential
 from .likelihoods import MultiClass
 
@@ -224,10 +229,13 @@ class SVGPModified:
     def x6_expert(self, N, Afr, Lfr, stats, bufs, timing=None, fmt="x6"):
         """K5 on images: fmean, fvar [K, N] (x6 mode)."""
         with _Stage(timing, "expert_cond"):
+            c_out = bufs.get("c_out")  # training (split-f16): C_k images for the backward
+            if c_out is not None:
+                ops.colnorm_max(self.q_sqrt, out=c_out[1])
             return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, self.num_inducing, N,
                                              self.num_latent_gps, fmean=bufs.get("fmean"),
                                              fvar=bufs.get("fvar"), workspace=bufs.get("ws_expert"),
-                                             planes=expert_planes(), fmt=fmt)
+                                             planes=expert_planes(), fmt=fmt, c_out=c_out)
 
     def conditional_experts(self, X, k0, k1, LinvT=None):
         """fmean, fvar [k1 - k0, N] of experts k0 .. k1 - 1 only (the expert-parallel
@@ -386,6 +394,11 @@ class SMGP(SGP):
             for L, M in (("f", Mf), ("a", Ma)):  # kept for the backward pass
                 b["A32_" + L] = ops.padded(M, N, dev)
             b["G"] = ops.padded(4 * K, N, dev).unflatten(0, (4, K))
+            if (forward_image_format(True) == "f16" and expert_cross() == "f16"
+                    and ops.c_images_bytes(Mx, N, K) <= C_IMAGES_MAX_BYTES):
+                for L in ("f", "a"):  # K5 writes C_k per expert; the backward reads them
+                    b["Cfr_" + L] = torch.empty(ops.c_images_bytes(Mx, N, K), dtype=torch.uint8, device=dev)
+                    b["colmax_" + L] = torch.empty(1, dtype=torch.float32, device=dev)
             b["ws_cbwd"] = torch.empty(ops.conditional_backward_workspace_bytes(Mx, N, K), dtype=torch.uint8,
                                        device=dev)
         self._bufs[key] = b
@@ -484,7 +497,8 @@ class SMGP(SGP):
         bufs = {L: {"Kuf": b["Kuf_" + L], "A": b["A_" + L], "stats": b["stats_" + L],
                     "fmean": b["mu_" + L], "fvar": b["var_" + L], "ws_expert": b["ws_expert"],
                     "Afr": b.get("Afr_" + L, b.get("Afr")), "Tfr": b.get("Tfr_" + L, b.get("Tfr")),
-                    "A32": b.get("A32_" + L)} for L, _ in layers}
+                    "A32": b.get("A32_" + L),
+                    "c_out": (b["Cfr_" + L], b["colmax_" + L]) if "Cfr_" + L in b else None} for L, _ in layers}
         if b["x6"] and "Tfr_a" in b:
             # both layers' K4 then both K5 in stream order on the main stream: the
             # matrix-core kernels fill the chip alone, and a cross-stream hand-off
@@ -600,9 +614,14 @@ class SMGP(SGP):
         for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
             M = layer.num_inducing
             with _Stage(timing, "conditional_bwd"):
+                cimg = None
+                if "Cfr_" + L in b:  # the forward's C_k images (mgp_conditional_backward_f16c)
+                    cimg = (b["Cfr_" + L], b["colmax_" + L],
+                            ops.image_bound(b["Lfr_" + L], M, K=layer.num_latent_gps))
                 g = ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], layer.q_sqrt,
                                                 layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
-                                                workspace=b["ws_cbwd"], fmt=forward_image_format(True))
+                                                workspace=b["ws_cbwd"], fmt=forward_image_format(True),
+                                                c_images=cimg)
             with _Stage(timing, "chol_bwd"):
                 gKuu = ops.chol_backward(b["L_" + L], b["LinvT_" + L], g["g_Lm"])
             with _Stage(timing, "rbf_bwd"):

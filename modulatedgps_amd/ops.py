@@ -349,12 +349,13 @@ def split_cols_x6(A, out=None, fmt="x6"):
 
 
 def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=None, workspace=None, planes=3,
-                          fmt="x6", cross=None):
+                          fmt="x6", cross=None, c_out=None):
     """fmean, fvar [K, N] of the whitened K-expert conditional from split-bf16 images
     (planes < 3: K5 on the leading bf16 planes only, mgp_expert_conditional_planes;
     fmt "f16": from split-f16 images, mgp_expert_conditional_f16, or with cross "f8"
     (default: config.expert_cross()) mgp_expert_conditional_f16x8, the cross terms
-    on the e4m3 MFMA)."""
+    on the e4m3 MFMA).  c_out = (Cfr, colmax) (f16, cross "f16"; colmax from colnorm_max):
+    also write C_k = L_k^T A as images for the backward (mgp_expert_conditional_f16c)."""
     _check(stats, "stats", 3)
     dev = stats.device
     if fmean is None:
@@ -369,9 +370,16 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
     if _fmt(fmt) == "f16":
         from .config import expert_cross
         entry = "mgp_expert_conditional_f16x8" if (cross or expert_cross()) == "f8" else "mgp_expert_conditional_f16"
-        _lib.call(entry, Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
-                  stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(),
-                  fvar.data_ptr(), _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
+        args = [Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(), stats.data_ptr(), _ld(stats),
+                variance.data_ptr(), M, N, K, fmean.data_ptr(), fvar.data_ptr(), _ld(fmean), workspace.data_ptr(),
+                workspace.numel()]
+        if c_out is not None:
+            if entry != "mgp_expert_conditional_f16":
+                raise ValueError("c_out needs f16 cross terms")
+            Cfr, colmax = c_out
+            entry = "mgp_expert_conditional_f16c"
+            args += [Cfr.data_ptr(), Cfr.numel(), colmax.data_ptr()]
+        _lib.call(entry, *args, _stream())
     elif planes == 3:
         _lib.call("mgp_expert_conditional_x6", Afr.data_ptr(), Afr.numel(), Lfr.data_ptr(), Lfr.numel(),
                   stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, fmean.data_ptr(),
@@ -565,12 +573,13 @@ def conditional_backward_workspace_bytes(M, N, K):
 
 
 def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None, fmt="x6",
-                            cross=None):
+                            cross=None, c_images=None):
     """Backward of one layer's conditional (see include/mgp_hip.h): returns dict of
     g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1]).
     fmt: format of A's image Afr ("f16": mgp_conditional_backward_f16; with cross "f8",
     default config.expert_cross(), mgp_conditional_backward_f16x8 -- Afr then comes
-    from trsm_stats_x6(..., A=..., cross="f8"))."""
+    from trsm_stats_x6(..., A=..., cross="f8")).  c_images = (Cfr, colmax, l_bound) from
+    expert_conditional_x6(..., c_out=...) (f16, cross "f16"): mgp_conditional_backward_f16c."""
     K = q_mu.shape[1]
     dev = q_mu.device
     if out is None:
@@ -587,13 +596,43 @@ def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None
     entry = "mgp_conditional_backward_" + _fmt(fmt)
     if entry.endswith("f16") and (cross or expert_cross()) == "f8":
         entry += "x8"
-    _lib.call(entry, Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A),
-              q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), q_mu.data_ptr(), _ld(q_mu),
-              LinvT.data_ptr(), _ld(LinvT), Gmu.data_ptr(), Gv.data_ptr(), _ld(Gmu), M, N, K,
-              o["g_q_mu"].data_ptr(), _ld(o["g_q_mu"]), o["g_q_sqrt"].data_ptr(), _ld(o["g_q_sqrt"]),
-              o["g_q_sqrt"].stride(0), o["g_Kuf"].data_ptr(), _ld(o["g_Kuf"]), o["g_Lm"].data_ptr(),
-              _ld(o["g_Lm"]), o["g_var"].data_ptr(), workspace.data_ptr(), workspace.numel(), _stream())
+    args = [Afr.data_ptr(), Afr.numel(), A.data_ptr(), _ld(A),
+            q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), q_mu.data_ptr(), _ld(q_mu),
+            LinvT.data_ptr(), _ld(LinvT), Gmu.data_ptr(), Gv.data_ptr(), _ld(Gmu), M, N, K,
+            o["g_q_mu"].data_ptr(), _ld(o["g_q_mu"]), o["g_q_sqrt"].data_ptr(), _ld(o["g_q_sqrt"]),
+            o["g_q_sqrt"].stride(0), o["g_Kuf"].data_ptr(), _ld(o["g_Kuf"]), o["g_Lm"].data_ptr(),
+            _ld(o["g_Lm"]), o["g_var"].data_ptr(), workspace.data_ptr(), workspace.numel()]
+    if c_images is not None:
+        if entry != "mgp_conditional_backward_f16":
+            raise ValueError("c_images need the split-f16 format with f16 cross terms")
+        Cfr, colmax, l_bound = c_images
+        entry = "mgp_conditional_backward_f16c"
+        args += [Cfr.data_ptr(), Cfr.numel(), colmax.data_ptr(), l_bound.data_ptr()]
+    _lib.call(entry, *args, _stream())
     return out
+
+
+def c_images_bytes(M, N, K):
+    """Bytes of the C_k = L_k^T A images of expert_conditional_x6(..., c_out=...)."""
+    return _lib.load().mgp_c_images_bytes(M, N, K)
+
+
+def colnorm_max(q_sqrt, out=None):
+    """max over experts and columns of ||tril(q_sqrt[k])[:, j]||_2 (float32 device [1])."""
+    _check(q_sqrt, "q_sqrt", 3)
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=q_sqrt.device)
+    K, M = q_sqrt.shape[0], q_sqrt.shape[1]
+    _lib.call("mgp_colnorm_max", q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), M, K, out.data_ptr(), _stream())
+    return out
+
+
+def image_bound(img, M, K=None, N=None):
+    """The device bound in a split image's trailer (float32 view [1]): lower images
+    (K given) or column images (N given)."""
+    lib = _lib.load()
+    size = lib.mgp_x6_lower_bytes(M, K) if K is not None else lib.mgp_x6_cols_bytes(M, N)
+    return img.view(torch.uint8)[size - 256:size - 252].view(torch.float32)
 
 
 # --------------------------------------------------------------------------- K7
