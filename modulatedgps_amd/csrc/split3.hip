@@ -761,7 +761,8 @@ __global__ __launch_bounds__(256, 2) void grad_a_s_f16_kernel(const bf16x8* __re
 // C_k column strip is read from HBM about once and served to the other pairs
 // from L2 (one row tile per workgroup: the light tiles ran ahead through the
 // experts and every strip came from HBM/MALL ~4.5 times).
-__device__ __forceinline__ void grad_a_c_store(const floatx16 (&out)[4][1], int t, int tn, int w, int lane,
+template <int NC>
+__device__ __forceinline__ void grad_a_c_store(const floatx16 (&out)[4][NC], int c, int t, int tn, int w, int lane,
                                                int nmk, int64_t M, int64_t N, const float* __restrict__ gA0,
                                                int64_t ld0, bf16x8* __restrict__ gAfr) {
   const int64_t nb = 4 * (int64_t)tn + w;
@@ -779,7 +780,7 @@ __device__ __forceinline__ void grad_a_c_store(const floatx16 (&out)[4][1], int 
     for (int e = 0; e < 16; ++e) {
       const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
       const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
-      v[e] = ok ? fmaf(2.f, out[i][0][e], b0) : 0.f;  // rows >= M read 0 (outside the resource)
+      v[e] = ok ? fmaf(2.f, out[i][c][e], b0) : 0.f;  // rows >= M read 0 (outside the resource)
     }
     const int64_t mk = 8 * (int64_t)t + 2 * i;
 #pragma unroll
@@ -792,6 +793,48 @@ __device__ __forceinline__ void grad_a_c_store(const floatx16 (&out)[4][1], int 
   }
 }
 
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_from(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_from<I + 1, N>(f);
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_from<0, N>(f);
+}
+
+// One continuous pipeline over the K L k-steps of a row tile (L = 8 t + 8 per
+// expert), in blocks of 8 k-steps: for each 8-row-step block of m' (outer), for
+// each expert k, its 8 k-steps.  T (L_k's row slab, via registers into the LDS
+// double buffer), B (C_k's fragments, straight to registers) and g = Gv_k[n] are
+// loaded PD k-steps ahead into a register ring of PD + 1 sets, across expert and
+// block boundaries; every load of a k-step is issued before any of a later one
+// (vector loads complete in order), so the wait for k-step s + 1's T slab never
+// forces a younger prefetch.  Block order keeps the workgroups of a column tile in
+// step: all start the first pass (row tile nT - 1 - p, nT - p blocks) at block 0 and
+// advance one block per unit time, and the second pass (row tile p) runs its blocks
+// downwards, which puts every workgroup at block nT - time in it -- so each C_k
+// strip is fetched about twice per column tile, not once per workgroup.
+// The per-column expert weights need no second accumulator set: acc holds the
+// running sum in units of the current expert's g, sum (g_j / g_k) P_j, rescaled by
+// g_k / g_k' at each expert switch (every 8 k-steps) and by the last g at the end
+// -- each rescale is one f32 rounding relative to the running total, as for
+// out += g acc.  |g| is clamped from below to 2^-40 max_k |g_k[n]| (the clamp moves
+// the result by < 2^-40 of the largest contribution; the quotient stays < 2^82 of
+// it).  DIAG masks are not applied: the zero blocks of the diagonal tile are
+// zero-filled in the image (8 % more MFMAs, no branch in the pipeline).
+// NC: 32-column sub-tiles per wave (workgroup = 128 rows x 128 NC columns).
+// grad_a_c_kernel's prefetch distance and column sub-tiles per wave (c3, MI355X:
+// PD 3 / NC 1 1.72 ms; PD 1 / NC 2 1.77 ms, 264 B of spill in its epilogue)
+#ifndef MGP_GAC_PD
+#define MGP_GAC_PD 3
+#define MGP_GAC_NC 1
+#endif
+constexpr int kGacPD = MGP_GAC_PD, kGacNC = MGP_GAC_NC;
+
+template <int PD, int NC>
 __global__ __launch_bounds__(256, 2) void grad_a_c_kernel(const bf16x8* __restrict__ Ltfr, uint32_t lt_bytes,
                                                          const bf16x8* __restrict__ Cfr, int64_t cexp,
                                                          uint32_t c_bytes, int nmk, int nTn, int K, int64_t M,
@@ -801,45 +844,154 @@ __global__ __launch_bounds__(256, 2) void grad_a_c_kernel(const bf16x8* __restri
                                                          const float* __restrict__ l_bound,
                                                          const float* __restrict__ a_bound,
                                                          const float* __restrict__ colmax) {
+  constexpr int U = PD + 1;
+  static_assert(8 % U == 0, "the ring cycles within an expert's 8 k-steps (and the LDS double buffer)");
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   const int nT = nmk / 8, nmb = nmk / 2, nP = (nT + 1) / 2;
   int p, tn;
   col_major_item(blockIdx.x, nP, nTn, p, tn);
   const int t1 = nT - 1 - p, t2 = p;  // t1 == t2: the middle tile of an odd nT, alone
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nb = 4 * (int64_t)tn + w;
-  const int64_t n = 32 * nb + (lane & 31);
-  floatx16 acc[4][1], out1[4][1], out2[4][1];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      out1[i][0][e] = 0.f;
-      out2[i][0][e] = 0.f;
-    }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t nb = 4 * NC * (int64_t)tn + NC * w;  // column blocks nb .. nb + NC - 1 (32 wide)
   const float unscale =
       ldexpf(1.f, -(img_exp(*l_bound) + img_exp(*colmax * *a_bound * 1.0009765625f)));
-  for (int k = 0; k < K; ++k) {
-    const __amdgpu_buffer_rsrc_t rT = img_rsrc(Ltfr, lt_bytes), rB = img_rsrc(Cfr + (int64_t)k * cexp, c_bytes);
-    const float g = n < N ? Gv[(int64_t)k * ldg + n] * unscale : 0.f;
-    x6_mainloop<2, 1, 2, true>(acc, sL, rT, (uint32_t)(((int64_t)k * nmb + 4 * t1) * nmk) * 3u * kFragBytes, rB,
-                               (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, 8 * t1 + 8, nmk);
+  const __amdgpu_buffer_rsrc_t rT = img_rsrc(Ltfr, lt_bytes);
+  const __amdgpu_buffer_rsrc_t rG =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Gv, (short)0, (int)(uint32_t)(K * ldg * 4), 0x00020000);
+  uint32_t vG[NC];
+  float gmin[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int64_t n = 32 * (nb + c) + (lane & 31);
+    vG[c] = (uint32_t)(n < N ? n : 0) * 4u;
+    float gmax = 0.f;
+    for (int k = 0; k < K; ++k)
+      gmax = fmaxf(gmax, fabsf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                             rG, vG[c], (uint32_t)(k * ldg * 4), 0))));
+    gmin[c] = fmaxf(gmax * 0x1p-40f, 0x1p-126f);
+  }
+  // T stage: thread tid moves units e = tid + 256 s (s = 0, 1): row sub-tile e / 128,
+  // plane (e / 64) % 2, lane e % 64
+  uint32_t vT[2];
+  int dT[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int e = tid + 256 * s, i = e / 128, pl = (e / 64) % 2;
+    vT[s] = (uint32_t)((i * nmk * 192 + pl * 64 + (e & 63)) * 16);
+    dT[s] = (3 * i + pl) * 64 + (e & 63);
+  }
+  const uint32_t vB = 16u * lane;
+  for (int pass = 0; pass < (t2 != t1 ? 2 : 1); ++pass) {
+    const int t = pass ? t2 : t1;
+    const int L = 8 * t + 8, S = K * L;
+    u32x4v st[U][2];
+    bf16x8 bb[U][NC][3];
+    // the load stream's k-step: 8-step block lmb (outer; the second pass runs it
+    // downwards), expert lk, mk = 8 lmb + lj; index ls
+    const int dmb = pass ? -1 : 1;
+    int lk = 0, lmb = pass ? t : 0, lj = 0, ls = 0;
+    auto issue = [&](auto jc) {
+      constexpr int J = decltype(jc)::value;
+      const int lmk = 8 * lmb + lj;
+      const uint32_t ot = (uint32_t)(((int64_t)lk * nmb + 4 * t) * nmk + lmk) * 192u * 16u;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) st[J][s] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s], ot, 0);
+      const __amdgpu_buffer_rsrc_t rB = img_rsrc(Cfr + (int64_t)lk * cexp, c_bytes);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint32_t ob = (uint32_t)((nb + c) * nmk + lmk) * 3u * kFragBytes;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) bb[J][c][pl] = ld_frag(rB, vB, ob + pl * kFragBytes);
+      }
+      if (ls < S - 1) {  // advance (the stream stays on the last k-step once it is reached)
+        ++ls;
+        if (++lj == 8) {
+          lj = 0;
+          if (++lk == K) {
+            lk = 0;
+            lmb += dmb;
+          }
+        }
+      }
+    };
+    auto loadg = [&](int k, float (&g)[NC]) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float x =
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rG, vG[c], (uint32_t)(k * ldg * 4), 0));
+        g[c] = __builtin_copysignf(fmaxf(fabsf(x), gmin[c]), x);
+      }
+    };
+    floatx16 acc[4][NC];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) out1[i][0][e] = fmaf(g, acc[i][0][e], out1[i][0][e]);
-    if (t2 != t1) {
-      x6_mainloop<2, 1, 2, true>(acc, sL, rT, (uint32_t)(((int64_t)k * nmb + 4 * t2) * nmk) * 3u * kFragBytes, rB,
-                                 (uint32_t)(nb * nmk) * 3u * kFragBytes, 0, 8 * t2 + 8, nmk);
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][c][e] = 0.f;
+    // compute stream: expert ck; acc in units of gcur (= expert ck's g)
+    int ck = 0;
+    float gcur[NC], gnext[NC];
+    loadg(0, gcur);
+    static_for<PD>([&](auto jc) { issue(jc); });
+#pragma unroll
+    for (int s = 0; s < 2; ++s) reinterpret_cast<u32x4v*>(sL[0])[dT[s]] = st[0][s];
+    __syncthreads();
+    // the 8 k-steps of one (block, expert)
+#pragma nounroll
+    for (int s0 = 0; s0 < S; s0 += 8) {
+      static_for<8>([&](auto jc) {
+        constexpr int JJ = decltype(jc)::value, J = JJ % U;
+        issue(std::integral_constant<int, (J + PD) % U>{});
+        if constexpr (JJ == 0) loadg(ck + 1 < K ? ck + 1 : 0, gnext);  // needed at JJ = 7
+        __builtin_amdgcn_sched_barrier(0);
+        // NC = 1: all 8 LDS reads in flight before the first MFMA (3 MFMAs per
+        // fragment pair would wait on each read); NC = 2: two sub-tiles at a time
+        constexpr int RB = NC == 1 ? 4 : 2;
+#pragma unroll
+        for (int i0 = 0; i0 < 4; i0 += RB) {
+          bf16x8 a[RB][3];
+#pragma unroll
+          for (int i = 0; i < RB; ++i)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl) a[i][pl] = sL[J % 2][((i0 + i) * 3 + pl) * 64 + lane];
+          if constexpr (RB == 4) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < RB; ++i)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[i0 + i][c] = mfma_fmt<2, true>(a[i], bb[J][c], acc[i0 + i][c]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (JJ == 7) {  // end of the expert's 8 k-steps: to units of the next one's g
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const float r = gcur[c] / gnext[c];
+            gcur[c] = gnext[c];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int e = 0; e < 16; ++e) acc[i][c][e] *= r;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) reinterpret_cast<u32x4v*>(sL[(J + 1) % 2])[dT[s]] = st[(J + 1) % U][s];
+        __syncthreads();
+      });
+      if (++ck == K) ck = 0;
+    }
+    // acc is in units of gcur (the wrapped-around expert 0's g after the last block)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float gl = gcur[c] * unscale;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) out2[i][0][e] = fmaf(g, acc[i][0][e], out2[i][0][e]);
+        for (int e = 0; e < 16; ++e) acc[i][c][e] *= gl;
+      // column block nb + c as (128-column tile, wave) of the one-block store
+      grad_a_c_store(acc, c, t, (int)((nb + c) / 4), (int)((nb + c) % 4), lane, nmk, M, N, gA0, ld0, gAfr);
     }
   }
-  grad_a_c_store(out1, t1, tn, w, lane, nmk, M, N, gA0, ld0, gAfr);
-  if (t2 != t1) grad_a_c_store(out2, t2, tn, w, lane, nmk, M, N, gA0, ld0, gAfr);
 }
 
 // max over k, j of ||tril(q_sqrt[k])[:, j]||_2 -> *out (float bits, atomicMax; zeroed
@@ -1789,9 +1941,9 @@ static int conditional_backward(
   }
   // 3. gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0  (C path: 2 sum_k L_k C_k diag(Gv_k) + gA0)
   if (cpath)
-    hipLaunchKernelGGL(grad_a_c_kernel, dim3((unsigned)((nT + 1) / 2 * 2 * nTn)), dim3(256), 0, s, (const bf16x8*)Sfr,
-                       (uint32_t)lower_planes(M, K), (const bf16x8*)Cfr, (int64_t)(cols_planes(M, N) / 16),
-                       (uint32_t)cols_planes(M, N), nmk, 2 * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, l_bound,
+    hipLaunchKernelGGL((grad_a_c_kernel<kGacPD, kGacNC>), dim3((unsigned)((nT + 1) / 2 * (2 / kGacNC) * nTn)), dim3(256), 0, s,
+                       (const bf16x8*)Sfr, (uint32_t)lower_planes(M, K), (const bf16x8*)Cfr,
+                       (int64_t)(cols_planes(M, N) / 16), (uint32_t)cols_planes(M, N), nmk, (2 / kGacNC) * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, l_bound,
                        (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)), colmax);
   else if (f16 && x8)
     hipLaunchKernelGGL((grad_a_s_kernel<true, true>), dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s,

@@ -114,6 +114,68 @@ def test_conditional_backward(device, N, M, K, D, ls):
     assert float(g["g_var"].cpu()) == pytest.approx(float(v.grad), rel=1e-5)
 
 
+@pytest.mark.parametrize("N,M,K,D,ls", [(2000, 64, 3, 2, 1.0), (4097, 200, 4, 3, 1.2), (8192, 512, 8, 8, 2.0)])
+@pytest.mark.parametrize("pattern", ["normal", "adversarial"])
+def test_conditional_backward_c_images(device, N, M, K, D, ls, pattern):
+    """The split-f16 training backward from the forward's C_k = L_k^T A images
+    (grad_a_c_kernel: one pipeline over all experts, the accumulator kept in units
+    of the current expert's G_v and rescaled at each expert boundary).  "adversarial"
+    G_v: an all-zero expert, all-zero columns, 1e-30 entries and columns whose experts
+    differ by 1e12 -- the rescale chain's clamp must neither blow up nor lose the
+    large terms."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(11)
+    X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
+    L = p.pred
+    f32 = lambda a: np.asarray(a, np.float32)
+    Xt, Zt = torch.as_tensor(f32(X), device=device), torch.as_tensor(f32(L["Z"]), device=device)
+    var = torch.as_tensor([L["variance"]], dtype=torch.float32, device=device)
+    lst = torch.as_tensor([ls], dtype=torch.float32, device=device)
+    qmu = torch.as_tensor(f32(L["q_mu"]), device=device)
+    qs = ops.as_padded(torch.as_tensor(f32(L["q_sqrt"])), device=device)
+    gmu = rng.standard_normal((K, N)).astype(np.float32)
+    gv = rng.standard_normal((K, N)).astype(np.float32)
+    if pattern == "adversarial":
+        gv[1] = 0.0
+        gv[:, 5:40] = 0.0
+        gv[0, 40:80] = 1e-30
+        gv[2, 80:120] *= 1e6
+        gv[0, 80:120] *= 1e-6
+        gv[:, 120:130] = 1e-30
+    Gmu, Gv = ops.padded(K, N, device), ops.padded(K, N, device)
+    Gmu.copy_(torch.as_tensor(gmu))
+    Gv.copy_(torch.as_tensor(gv))
+    _, LinvT, _ = ops.kuu_potrf_trtri([Zt], [var], [lst], 1e-6)
+    Khr = ops.rbf_kuf_x6(Xt, Zt, var, lst, fmt="f16")
+    Thr = ops.split_upper_x6(LinvT[0], fmt="f16")
+    A = ops.padded(M, N, device)
+    Ahr, sth = ops.trsm_stats_x6(Thr, Khr, qmu, M, N, A=A, f16_variance=var, in_fmt="f16", cross="f16")
+    Lhr = ops.split_lower_x6(qs, fmt="f16")
+    Cfr = torch.empty(ops.c_images_bytes(M, N, K), dtype=torch.uint8, device=device)
+    colmax = ops.colnorm_max(qs)
+    ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmt="f16", cross="f16", c_out=(Cfr, colmax))
+    g = ops.conditional_backward_x6(Ahr, A, qs, qmu, LinvT[0], Gmu, Gv, M, N, fmt="f16", cross="f16",
+                                    c_images=(Cfr, colmax, ops.image_bound(Lhr, M, K=K)))
+    g_s = ops.conditional_backward_x6(Ahr, A, qs, qmu, LinvT[0], Gmu, Gv, M, N, fmt="f16", cross="f16")
+    A64 = torch.tensor(to_np(A)[:, :N], requires_grad=True)
+    Linv = to_np(LinvT[0]).T
+    q_sqrt = torch.tensor(f32(L["q_sqrt"]).astype(np.float64))
+    LTA = torch.tril(q_sqrt).transpose(1, 2) @ A64
+    fvar = -(A64 ** 2).sum(0)[None, :] + (LTA ** 2).sum(1)
+    loss = (torch.tensor(gmu.astype(np.float64)) * (A64.T @ torch.tensor(f32(L["q_mu"]).astype(np.float64))).T).sum() \
+        + (torch.tensor(gv.astype(np.float64)) * fvar).sum()
+    loss.backward()
+    gKuf_ref = Linv.T @ A64.grad.numpy()
+    got = to_np(g["g_Kuf"])[:, :N]
+    assert np.isfinite(got).all()
+    assert normwise(got, gKuf_ref) < 1e-4
+    # column-wise too: the tiny and zero-weight columns must not pick up noise
+    cols = np.linalg.norm(got - gKuf_ref, axis=0) / np.maximum(np.linalg.norm(gKuf_ref, axis=0), 1e-30)
+    assert np.quantile(cols, 0.99) < 1e-3
+    assert normwise(got, to_np(g_s["g_Kuf"])[:, :N]) < 1e-4
+    assert normwise(to_np(g["g_Lm"]), to_np(g_s["g_Lm"])) < 1e-4
+
+
 @pytest.mark.parametrize("M,D,ls", [(64, 2, 0.8), (200, 3, 1.0), (1024, 8, 1.0)])
 def test_chol_backward(device, M, D, ls):
     """Reverse mode of Lm = chol(Kuu) against float64 autograd."""

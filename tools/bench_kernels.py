@@ -87,6 +87,11 @@ def main():
     A32h = ops.padded(M, N, dev)   # the f16 chain's training K4: f16 A image + f32 A
     ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, Afr=Ahr, stats=sth, A=A32h, f16_variance=var, in_fmt="f16", cross="f8")
     cbh = ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N, fmt="f16")
+    Cfr = torch.empty(ops.c_images_bytes(M, N, K), dtype=torch.uint8, device=dev)
+    colmax = ops.colnorm_max(q_sqrt)
+    ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmean=fm6, fvar=fv6, fmt="f16", cross="f16",
+                              c_out=(Cfr, colmax))
+    cimg = (Cfr, colmax, ops.image_bound(Lhr, M, K=K))
     torch.cuda.synchronize()
     runs = {
         "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
@@ -128,6 +133,9 @@ def main():
                                                            out=cb, workspace=wsc),
         "cond_bwd_f16": lambda: ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
                                                             out=cbh, workspace=wsc, fmt="f16", cross="f16"),
+        "cond_bwd_f16c": lambda: ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
+                                                             out=cbh, workspace=wsc, fmt="f16", cross="f16",
+                                                             c_images=cimg),
         "cond_bwd_f16x8": lambda: ops.conditional_backward_x6(Ahr, A32h, q_sqrt, q_mu, LinvT[0], Gmu, Gv, M, N,
                                                               out=cbh, workspace=wsc, fmt="f16", cross="f8"),
     }
@@ -152,7 +160,8 @@ def main():
             out[name]["tflops"] = M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12
     for name, fl in (("gram_x6_P", K * M * M * N), ("gram_x6_Lm", M * M * N), ("gram_f16_P", K * M * M * N),
                      ("gram_f16_rows_P", K * M * M * N),
-                     ("cond_bwd_x6", (2 * K + 1) * M * M * N), ("cond_bwd_f16", (2 * K + 1) * M * M * N)):
+                     ("cond_bwd_x6", (2 * K + 1) * M * M * N), ("cond_bwd_f16", (2 * K + 1) * M * M * N),
+                     ("cond_bwd_f16c", (K + 1) * M * M * N)):
         if name in out:
             out[name]["tflops"] = fl / (out[name]["median_ms"] * 1e-3) / 1e12
     if "rbf_bwd" in out:
