@@ -1906,6 +1906,7 @@ static int conditional_backward(
   if (cpath) {
     if (!colmax || !l_bound) return -32;
     if (cfr_bytes < mgp_c_images_bytes(M, N, K)) return -31;
+    if ((int64_t)K * ldg * 4 >= ((int64_t)1 << 32)) return MGP_ERR_UNSUPPORTED;  // grad_a_c's Gv resource
     if (!aligned16(Cfr)) return MGP_ERR_ALIGN;
     // L_k's image (rows m, k-steps over m' <= m) into the S image's space; Linv's image
     const int64_t nfrag = (int64_t)K * nmb * nmk, nf1 = (int64_t)nmb * nmk;

@@ -114,7 +114,8 @@ def test_conditional_backward(device, N, M, K, D, ls):
     assert float(g["g_var"].cpu()) == pytest.approx(float(v.grad), rel=1e-5)
 
 
-@pytest.mark.parametrize("N,M,K,D,ls", [(2000, 64, 3, 2, 1.0), (4097, 200, 4, 3, 1.2), (8192, 512, 8, 8, 2.0)])
+@pytest.mark.parametrize("N,M,K,D,ls", [(2000, 64, 3, 2, 1.0), (4097, 200, 4, 3, 1.2), (3000, 300, 5, 2, 1.0),
+                                        (8192, 512, 8, 8, 2.0)])
 @pytest.mark.parametrize("pattern", ["normal", "adversarial"])
 def test_conditional_backward_c_images(device, N, M, K, D, ls, pattern):
     """The split-f16 training backward from the forward's C_k = L_k^T A images
