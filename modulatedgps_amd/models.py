@@ -43,9 +43,12 @@ from .broadcasting_lik import BroadcastingLikelihood
 from .config import (conditional_mode, default_device, default_jitter, expert_cross, expert_planes,
                      forward_image_format)
 
-# Largest set of C_k = L_k^T A images (per layer) the training step keeps for the
-# backward (mgp_conditional_backward_f16c); beyond it the backward rebuilds S_k = L_k L_k^T.
-C_IMAGES_MAX_BYTES = 8 << 30
+# The training step keeps each layer's C_k = L_k^T A images for the backward
+# (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
+# device's HBM (config 5: 2 x 51.5 GB of 288 GB); beyond it the backward rebuilds
+# S_k = L_k L_k^T.  C_IMAGES_MAX_BYTES (per layer), when set, overrides it.
+C_IMAGES_HBM_FRACTION = 0.4
+C_IMAGES_MAX_BYTES = None
 from .kernels import SquaredExponential
 from .likelihoods import MultiClass
 
@@ -394,10 +397,12 @@ class SMGP(SGP):
             for L, M in (("f", Mf), ("a", Ma)):  # kept for the backward pass
                 b["A32_" + L] = ops.padded(M, N, dev)
             b["G"] = ops.padded(4 * K, N, dev).unflatten(0, (4, K))
-            if (forward_image_format(True) == "f16" and expert_cross() == "f16"
-                    and ops.c_images_bytes(Mx, N, K) <= C_IMAGES_MAX_BYTES):
+            cb = ops.c_images_bytes(Mx, N, K)
+            limit = (C_IMAGES_MAX_BYTES if C_IMAGES_MAX_BYTES is not None else
+                     C_IMAGES_HBM_FRACTION * torch.cuda.get_device_properties(dev).total_memory / 2)
+            if forward_image_format(True) == "f16" and expert_cross() == "f16" and cb <= limit:
                 for L in ("f", "a"):  # K5 writes C_k per expert; the backward reads them
-                    b["Cfr_" + L] = torch.empty(ops.c_images_bytes(Mx, N, K), dtype=torch.uint8, device=dev)
+                    b["Cfr_" + L] = torch.empty(cb, dtype=torch.uint8, device=dev)
                     b["colmax_" + L] = torch.empty(1, dtype=torch.float32, device=dev)
             b["ws_cbwd"] = torch.empty(ops.conditional_backward_workspace_bytes(Mx, N, K), dtype=torch.uint8,
                                        device=dev)
