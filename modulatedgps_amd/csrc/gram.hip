@@ -595,21 +595,20 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
     const char* sy_ = sY[buf][e];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 c[2][3];
+      // all 8 fragment reads of the k-step in flight before its first MFMA
+      bf16x8 c[2][3], a[2][3];
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < 2; ++p) {
           c[t2][p] = *reinterpret_cast<const bf16x8*>(sy_ + (2 * (vb + t2) + ks) * kXG2 + p * 1024 + lane * 16);
+          a[t2][p] = *reinterpret_cast<const bf16x8*>(sX[buf] + (2 * (wb_ + t2) + ks) * kXG2 + p * 1024 + lane * 16);
+        }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ta = 0; ta < 2; ++ta) {
-        bf16x8 a[3];
+      for (int ta = 0; ta < 2; ++ta)
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-          a[p] = *reinterpret_cast<const bf16x8*>(sX[buf] + (2 * (wb_ + ta) + ks) * kXG2 + p * 1024 + lane * 16);
-#pragma unroll
-        for (int tb = 0; tb < 2; ++tb) acc[ta][tb] = mfma_fmt<2, true>(a, c[tb], acc[ta][tb]);
-      }
+        for (int tb = 0; tb < 2; ++tb) acc[ta][tb] = mfma_fmt<2, true>(a[ta], c[tb], acc[ta][tb]);
     }
   };
 
