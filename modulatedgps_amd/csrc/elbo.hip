@@ -188,7 +188,9 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
         }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
-        sa[k] = sqrtf(va + jitter);
+        // max(va, 0): a float32 marginal variance can round below -jitter where
+        // the reference's float64 one sits at ~0 (the sqrt would be NaN)
+        sa[k] = sqrtf(fmaxf(va, 0.f) + jitter);
         if constexpr (MOD) {
           const float s2a = lik_var_a[k];
           const float da = y - ma[k];
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
         }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
-        sa[k] = sqrtf(va + jitter);
+        sa[k] = sqrtf(fmaxf(va, 0.f) + jitter);  // as in the forward
         if constexpr (MOD) {
           const float s2a = lik_var_a[k];
           const float da = y - ma[k];
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     for (int k = 0; k < KMAX; ++k) {
       if (k < K) {
         float gma = gx[k] * inv_tau;
-        float gva = gxz[k] * inv_tau * 0.5f / sa[k];
+        float gva = (var_a[(int64_t)k * ldf + n] > 0.f) ? gxz[k] * inv_tau * 0.5f / sa[k] : 0.f;
         float gmf, gvf;
         if constexpr (MC) {
           gmf = gve_mc * dpm[k];
@@ -657,7 +659,7 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
     if (k < K) {
-      const float logit = fmaf(zw[k], sqrtf(var_a[(int64_t)k * ldf + n] + jitter), mu_a[(int64_t)k * ldf + n]);
+      const float logit = fmaf(zw[k], sqrtf(fmaxf(var_a[(int64_t)k * ldf + n], 0.f) + jitter), mu_a[(int64_t)k * ldf + n]);
       x[k] = (-logf(-logf(uw[k])) + logit) * inv_tau;
       xm = fmaxf(xm, x[k]);
     }
@@ -677,8 +679,8 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
       if constexpr (MC)
         ay = fmaf(e, fmaf(zy[k], sqrtf(ps[k] - ps[k] * ps[k] + jitter), ps[k]), ay);
       else
-        ay = fmaf(e, fmaf(zy[k], sqrtf(v + lik_var[k] + jitter), m), ay);
-      af = fmaf(e, fmaf(zy[k], sqrtf(v + jitter), m), af);
+        ay = fmaf(e, fmaf(zy[k], sqrtf(fmaxf(v, 0.f) + lik_var[k] + jitter), m), ay);
+      af = fmaf(e, fmaf(zy[k], sqrtf(fmaxf(v, 0.f) + jitter), m), af);
     }
   if (sy) sy[(int64_t)s * N + n] = ay / den;
   if (sf) sf[(int64_t)s * N + n] = af / den;

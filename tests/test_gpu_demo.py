@@ -92,8 +92,6 @@ def _median(iters, elbos, lo, hi):
     return float(np.median(v))
 
 
-@pytest.mark.xfail(reason="a non-finite Adam step near iteration 1485 (Kuu factorisation then fails "
-                   "on NaN parameters); under investigation", strict=False)
 @pytest.mark.timeout(600)
 def test_demo_tf2_modified_multiclass_drop_in(device):
     """demos/demo_tf2_modified_multiclass.py (SMGPModified with the MultiClass /
