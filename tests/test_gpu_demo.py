@@ -120,3 +120,28 @@ def test_demo_tf2_modified_multiclass_drop_in(device):
     assign = g["assign_"]
     assert assign.shape == (g["Xtrain"].shape[0], 2)
     assert np.allclose(assign.sum(1), 1.0, atol=1e-5)
+
+
+@pytest.mark.timeout(600)
+def test_demo_tf2_2d_drop_in(device):
+    """demos/demo_tf2_2d.py (2-D inputs, SMGP, K = 3, 2000 Adam steps; reference
+    demos/demo_tf2_2d.py:22-62).  Readings of final_figs/demo_tf2_2d_2.png's
+    ELBO panel: about -228 at iteration 5, about -25 at 500, about -2 from
+    1500 to 2000.  The stump predictions (x2 = 0.75 and x1 = -0.25 slices)
+    ran through the demo's own numpy lines."""
+    g = runpy.run_path(os.path.join(ROOT, "demos", "demo_tf2_2d.py"), run_name="__main__")
+    iters, elbos = g["iters"], g["elbos"]
+    assert iters[0] == 5 and iters[-1] == 2000 and len(iters) == 400
+    assert np.all(np.isfinite(elbos))
+    first = elbos[0]
+    e500 = _median(iters, elbos, 450, 550)
+    final = _median(iters, elbos, 1900, 2000)
+    print(f"demo_tf2_2d ELBO: iter 5 {first:.3f}, ~500 {e500:.3f}, ~2000 {final:.3f}")
+    assert -270 < first < -190
+    assert -50 < e500 < -10
+    assert -8 < final < 0.5
+    n_test = g["Xtest"].shape[0]
+    for a, fm, fv in zip(g["stump_assign"], g["stump_fmean"], g["stump_fvar"]):
+        assert a.shape == (n_test, 3) and np.allclose(a.sum(1), 1.0, atol=1e-5)
+        assert fm.shape == (n_test, 3) and np.all(fv > 0)
+    assert g["samples_y"].shape == (100, g["Xtrain"].shape[0], 1)
