@@ -145,3 +145,30 @@ def test_demo_tf2_2d_drop_in(device):
         assert a.shape == (n_test, 3) and np.allclose(a.sum(1), 1.0, atol=1e-5)
         assert fm.shape == (n_test, 3) and np.all(fv > 0)
     assert g["samples_y"].shape == (100, g["Xtrain"].shape[0], 1)
+
+
+@pytest.mark.timeout(600)
+def test_demo_tf2_2d_modified_multiclass_drop_in(device):
+    """demos/demo_tf2_2d_modified_multiclass.py (2-D inputs, SMGPModified with
+    MultiClass / RobustMax, K = 2, 2000 Adam steps; reference
+    demos/demo_tf2_2d_modified_multiclass.py:22-64).  Readings of
+    final_figs/demo_tf2_2d_modified_multiclass_2.png's ELBO panel: about -4.3
+    at iteration 5, -1.1 at 500, 0.0 at 1000, +1.05 at 2000."""
+    g = runpy.run_path(os.path.join(ROOT, "demos", "demo_tf2_2d_modified_multiclass.py"), run_name="__main__")
+    iters, elbos = g["iters"], g["elbos"]
+    assert iters[0] == 5 and iters[-1] == 2000 and len(iters) == 400
+    assert np.all(np.isfinite(elbos))
+    first = elbos[0]
+    e500 = _median(iters, elbos, 450, 550)
+    e1000 = _median(iters, elbos, 950, 1050)
+    final = _median(iters, elbos, 1900, 2000)
+    print(f"demo_tf2_2d_modified_multiclass ELBO: iter 5 {first:.3f}, ~500 {e500:.3f}, ~1000 {e1000:.3f}, "
+          f"~2000 {final:.3f}")
+    assert -5.2 < first < -3.4
+    assert -1.7 < e500 < -0.5
+    assert -0.8 < e1000 < 0.8
+    assert 0.4 < final < 1.8
+    n_test = g["Xtest"].shape[0]
+    for a, fm, fv in zip(g["stump_assign"], g["stump_fmean"], g["stump_fvar"]):
+        assert a.shape == (n_test, 2) and np.allclose(a.sum(1), 1.0, atol=1e-5)
+        assert fm.shape == (n_test, 2) and np.all(fv >= 0)
