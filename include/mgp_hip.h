@@ -538,6 +538,34 @@ int mgp_predict_samples_multiclass(const float* mu_f, const float* var_f, const 
 int mgp_philox_normal2(uint64_t seed, int64_t n_offset, int64_t N, int32_t K, int32_t S, float* z,
                        mgp_stream_t stream);
 
+/* ---------------------------------------------------------------- method-level API
+ * The stages K6 fuses, for the reference's public methods.  Latents are
+ * expert-major [K][ldf]; sample s of point n is column s * stride_s + n
+ * (stride_s = 0: one S-invariant conditional for S tiled copies of X).  Noise:
+ * explicit [S][N][K] arrays (nullable) or K6's own Philox streams (z: stream 0,
+ * u: stream 1, keyed by (n + n_offset, s, k / 4)), so the three calls below with
+ * one seed reproduce mgp_elbo_terms with that seed.
+ *
+ * SMGP.W_dist (models.py:55-60): assign_layer.predict_f -> reparameterize
+ * (utils.py:26-27): logits[s][n][k] = mu_a + z sqrt(var_a + jitter). */
+int mgp_assign_logits(const float* mu_a, const float* var_a, int64_t ldf, int64_t stride_s, int64_t N,
+                      int32_t K, int32_t S, float jitter, const float* noise_z, uint64_t seed, int64_t n_offset,
+                      float* logits, mgp_stream_t stream);
+/* RelaxedOneHotCategorical(temperature = tau, logits).sample() (TFP 0.18,
+ * models.py:60,73): W[r] = softmax((g + logits[r]) / tau), g = -log(-log u), rows
+ * r = s * N + n of logits / W [S * N][K]. */
+int mgp_relaxed_onehot_sample(const float* logits, int64_t N, int32_t K, int32_t S, float tau,
+                              const float* noise_u, uint64_t seed, int64_t n_offset, float* W,
+                              mgp_stream_t stream);
+/* SMGP.E_log_p_Y(Xt, Y, W) (models.py:63-67): out[n] = logsumexp_s(sum_k W ve) - log S,
+ * W [S][N][K].  lik_var == NULL: the pred likelihood is MultiClass / RobustMax
+ * (multiclass_eps); assign_lik_var != NULL: SMGPModified.E_log_p_Y (models.py:112-123),
+ * which also reads the assign latents mu_a / var_a. */
+int mgp_e_log_p_y(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a, int64_t ldf,
+                  int64_t stride_s, const float* Y, const float* lik_var, const float* assign_lik_var,
+                  float multiclass_eps, const float* W, int64_t N, int32_t K, int32_t S, float* out,
+                  mgp_stream_t stream);
+
 /* ---------------------------------------------------------------- optimizer
  * KL gradient folded into the ELBO gradient: g_q_mu -= q_mu / num_data,
  * g_q_sqrt[k] -= tril(L_k - diag(1 / L_k[m,m])) / num_data (models.py:79). */

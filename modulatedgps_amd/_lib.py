@@ -175,6 +175,12 @@ SIGNATURES = {
                                               c_ptr]),
     "mgp_predict_samples_multiclass": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, ctypes.c_float, c_i64, c_i32, c_i32, ctypes.c_float,
                                                  ctypes.c_float, c_ptr, c_ptr, c_ptr, c_u64, c_i64, c_ptr, c_ptr, c_ptr]),
+    "mgp_assign_logits": (ctypes.c_int, [c_ptr, c_ptr, c_i64, c_i64, c_i64, c_i32, c_i32, ctypes.c_float, c_ptr,
+                                         c_u64, c_i64, c_ptr, c_ptr]),
+    "mgp_relaxed_onehot_sample": (ctypes.c_int, [c_ptr, c_i64, c_i32, c_i32, ctypes.c_float, c_ptr, c_u64, c_i64,
+                                                 c_ptr, c_ptr]),
+    "mgp_e_log_p_y": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_ptr, ctypes.c_float,
+                                     c_ptr, c_i64, c_i32, c_i32, c_ptr, c_ptr]),
 }
 
 _lib = None

@@ -1008,6 +1008,9 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
                     hipEvent_t prep_done = nullptr) {
   if (!workspace || workspace_bytes < mgp_chol_workspace_bytes(a.M, batch)) return MGP_ERR_WORKSPACE;
   if (!aligned16(workspace)) return MGP_ERR_ALIGN;
+  // the diagonal tiles of L and L^-T are written with 16-byte stores
+  const bool lay4 = a.ldl % 4 == 0 && (batch <= 1 || a.strideL % 4 == 0);
+  if ((a.L && !aligned16(a.L)) || (a.LinvT && !aligned16(a.LinvT)) || !lay4) return MGP_ERR_ALIGN;
   a.Mp = chol_mp(a.M);
   a.nb = (int)(a.Mp / CB);
   a.strideWS = chol_ws_doubles_per_batch(a.M);

@@ -188,9 +188,10 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
         }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
-        // max(va, 0): a float32 marginal variance can round below -jitter where
-        // the reference's float64 one sits at ~0 (the sqrt would be NaN)
-        sa[k] = sqrtf(fmaxf(va, 0.f) + jitter);
+        // max(va + jitter, 0): a float32 marginal variance can round below -jitter
+        // where the reference's float64 one sits at ~0 (the sqrt would be NaN); on
+        // (-jitter, 0] the value is the reference's sqrt(va + jitter) (utils.py:27)
+        sa[k] = sqrtf(fmaxf(va + jitter, 0.f));
         if constexpr (MOD) {
           const float s2a = lik_var_a[k];
           const float da = y - ma[k];
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
         }
         ma[k] = mu_a[(int64_t)k * ldf + n];
         const float va = var_a[(int64_t)k * ldf + n];
-        sa[k] = sqrtf(fmaxf(va, 0.f) + jitter);  // as in the forward
+        sa[k] = sqrtf(fmaxf(va + jitter, 0.f));  // as in the forward
         if constexpr (MOD) {
           const float s2a = lik_var_a[k];
           const float da = y - ma[k];
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     for (int k = 0; k < KMAX; ++k) {
       if (k < K) {
         float gma = gx[k] * inv_tau;
-        float gva = (var_a[(int64_t)k * ldf + n] > 0.f) ? gxz[k] * inv_tau * 0.5f / sa[k] : 0.f;
+        float gva = (var_a[(int64_t)k * ldf + n] + jitter > 0.f) ? gxz[k] * inv_tau * 0.5f / sa[k] : 0.f;
         float gmf, gvf;
         if constexpr (MC) {
           gmf = gve_mc * dpm[k];
@@ -659,7 +660,7 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
     if (k < K) {
-      const float logit = fmaf(zw[k], sqrtf(fmaxf(var_a[(int64_t)k * ldf + n], 0.f) + jitter), mu_a[(int64_t)k * ldf + n]);
+      const float logit = fmaf(zw[k], sqrtf(fmaxf(var_a[(int64_t)k * ldf + n] + jitter, 0.f)), mu_a[(int64_t)k * ldf + n]);
       x[k] = (-logf(-logf(uw[k])) + logit) * inv_tau;
       xm = fmaxf(xm, x[k]);
     }
@@ -679,8 +680,8 @@ __global__ __launch_bounds__(256) void predict_samples_kernel(
       if constexpr (MC)
         ay = fmaf(e, fmaf(zy[k], sqrtf(ps[k] - ps[k] * ps[k] + jitter), ps[k]), ay);
       else
-        ay = fmaf(e, fmaf(zy[k], sqrtf(fmaxf(v, 0.f) + lik_var[k] + jitter), m), ay);
-      af = fmaf(e, fmaf(zy[k], sqrtf(fmaxf(v, 0.f) + jitter), m), af);
+        ay = fmaf(e, fmaf(zy[k], sqrtf(fmaxf(v + lik_var[k] + jitter, 0.f)), m), ay);
+      af = fmaf(e, fmaf(zy[k], sqrtf(fmaxf(v + jitter, 0.f)), m), af);
     }
   if (sy) sy[(int64_t)s * N + n] = ay / den;
   if (sf) sf[(int64_t)s * N + n] = af / den;
@@ -701,9 +702,221 @@ __global__ __launch_bounds__(256) void philox_normal2_kernel(uint32_t key0, uint
   }
 }
 
+// ------------------------------------------------------------------ method-level API
+// The pieces K6 fuses, as separate kernels for the reference's public methods.
+// Latents are expert-major [K][ldf]; the sample s of point n sits in column
+// s * stride_s + n (stride_s = 0: the S-invariant conditional of S tiled copies).
+// Noise: explicit [S][N][K] arrays or the same Philox streams K6 draws (stream 0 =
+// z, stream 1 = u, keyed by (global n, s, k / 4)), so W_dist(seed) -> sample ->
+// E_log_p_Y reproduces _build_likelihood(seed).
+
+// SMGP.W_dist's logits (models.py:56-59, utils.py:26-27):
+// log_assign[s][n][k] = mu_a + z sqrt(var_a + jitter).  One thread per (s, n).
+__global__ __launch_bounds__(256) void assign_logits_kernel(
+    const float* __restrict__ mu_a, const float* __restrict__ var_a, int64_t ldf, int64_t stride_s, int64_t N,
+    int K, int S, float jitter, const float* __restrict__ noise_z, uint32_t key0, uint32_t key1,
+    int64_t n_offset, float* __restrict__ logits) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * (int64_t)S) return;
+  const int s = (int)(idx / N);
+  const int64_t n = idx % N, col = (int64_t)s * stride_s + n, o = idx * K;
+  const uint32_t ng = (uint32_t)(n + n_offset);
+  for (int kb = 0; 4 * kb < K; ++kb) {
+    float zz[4];
+    if (noise_z == nullptr) box_muller4(philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 0u}, key0, key1), zz);
+    for (int e = 0; e < 4 && 4 * kb + e < K; ++e) {
+      const int k = 4 * kb + e;
+      const float z = noise_z ? noise_z[o + k] : zz[e];
+      logits[o + k] = fmaf(z, sqrtf(fmaxf(var_a[(int64_t)k * ldf + col] + jitter, 0.f)),
+                           mu_a[(int64_t)k * ldf + col]);
+    }
+  }
+}
+
+// RelaxedOneHotCategorical(temperature, logits).sample() (TFP 0.18,
+// models.py:60,73): W = exp(log_softmax((g + logits) / tau)), g = -log(-log u),
+// over rows r = s * N + n of logits [S * N][K].  One thread per row.
+template <int KMAX>
+__global__ __launch_bounds__(256) void relaxed_onehot_kernel(const float* __restrict__ logits, int64_t N, int K,
+                                                             int S, float inv_tau,
+                                                             const float* __restrict__ noise_u, uint32_t key0,
+                                                             uint32_t key1, int64_t n_offset,
+                                                             float* __restrict__ W) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * (int64_t)S) return;
+  const int s = (int)(idx / N);
+  const int64_t n = idx % N, o = idx * K;
+  const uint32_t ng = (uint32_t)(n + n_offset);
+  float x[KMAX], xm = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < (KMAX + 3) / 4; ++kb) {
+    if (4 * kb >= K) break;
+    u32x4 w{0u, 0u, 0u, 0u};
+    if (noise_u == nullptr) w = philox4x32_10(u32x4{ng, (uint32_t)s, (uint32_t)kb, 1u}, key0, key1);
+    const uint32_t uw[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * kb + e;
+      if (k < KMAX && k < K) {
+        const float u = noise_u ? noise_u[o + k] : u01(uw[e]);
+        x[k] = (-logf(-logf(u)) + logits[o + k]) * inv_tau;
+        xm = fmaxf(xm, x[k]);
+      }
+    }
+  }
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < K) {
+      x[k] = __expf(x[k] - xm);
+      den += x[k];
+    }
+  const float r = 1.f / den;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < K) W[o + k] = x[k] * r;
+}
+
+// SMGP.E_log_p_Y(Xt, Y, W) (models.py:63-67): logsumexp_s(sum_k W ve) - log S per
+// point; MOD: SMGPModified.E_log_p_Y (models.py:112-123), the assignment
+// likelihood's var-exp on the assign latents adds its own logsumexp; MC: the pred
+// likelihood is MultiClass / RobustMax (ve is one value per (s, n), times sum_k W).
+template <int KMAX, bool MOD, bool MC>
+__global__ __launch_bounds__(256) void e_log_p_y_kernel(
+    const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
+    const float* __restrict__ var_a, int64_t ldf, int64_t stride_s, const float* __restrict__ Y,
+    const float* __restrict__ lik_var, const float* __restrict__ lik_var_a, const float* __restrict__ W,
+    int64_t N, int K, int S, float mc_a, float mc_b, float* __restrict__ out) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  constexpr float kHalfLog2Pi = 0.91893853320467274f;
+  const float y = Y[n];
+  float mx = -INFINITY, sm = 0.f, mxa = -INFINITY, sma = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const int64_t col = (int64_t)s * stride_s + n;
+    const float* w = W + ((int64_t)s * N + n) * K;
+    float l = 0.f, la = 0.f;
+    if constexpr (MC) {
+      float mu[KMAX], var[KMAX], dm[KMAX], dv[KMAX], ws = 0.f;
+      load_latents<KMAX>(mu_f, var_f, ldf, col, K, mu, var);
+      const float p = robustmax_p<KMAX, false>((int)y, mu, var, K, dm, dv);
+      for (int k = 0; k < K; ++k) ws += w[k];
+      l = fmaf(p, mc_a - mc_b, mc_b) * ws;
+    } else {
+      for (int k = 0; k < K; ++k) {
+        const float s2 = lik_var[k], d = y - mu_f[(int64_t)k * ldf + col];
+        l = fmaf(w[k], -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_f[(int64_t)k * ldf + col]) / s2, l);
+      }
+    }
+    if constexpr (MOD) {
+      for (int k = 0; k < K; ++k) {
+        const float s2 = lik_var_a[k], d = y - mu_a[(int64_t)k * ldf + col];
+        la = fmaf(w[k], -kHalfLog2Pi - 0.5f * logf(s2) - 0.5f * (d * d + var_a[(int64_t)k * ldf + col]) / s2, la);
+      }
+    }
+    if (l > mx) { sm = sm * __expf(mx - l) + 1.f; mx = l; } else { sm += __expf(l - mx); }
+    if constexpr (MOD) {
+      if (la > mxa) { sma = sma * __expf(mxa - la) + 1.f; mxa = la; } else { sma += __expf(la - mxa); }
+    }
+  }
+  float v = mx + logf(sm) - logf((float)S);
+  if constexpr (MOD) v += mxa + logf(sma) - logf((float)S);
+  out[n] = v;
+}
+
 }  // namespace mgp
 
 using namespace mgp;
+
+extern "C" int mgp_assign_logits(const float* mu_a, const float* var_a, int64_t ldf, int64_t stride_s, int64_t N,
+                                 int32_t K, int32_t S, float jitter, const float* noise_z, uint64_t seed,
+                                 int64_t n_offset, float* logits, mgp_stream_t stream) {
+  if (!mu_a) return -1;
+  if (!var_a) return -2;
+  if (ldf < (S > 1 ? stride_s * (S - 1) + N : N)) return -3;
+  if (stride_s < 0) return -4;
+  if (N < 0) return -5;
+  if (K < 1) return -6;
+  if (S < 1) return -7;
+  if (!(jitter >= 0.f)) return -8;
+  if (n_offset < 0) return -11;
+  if (!logits) return -12;
+  if (N == 0) return MGP_OK;
+  const int64_t total = N * (int64_t)S;
+  hipLaunchKernelGGL(assign_logits_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, mu_a, var_a, ldf, stride_s, N, K, S, jitter, noise_z,
+                     (uint32_t)(seed & 0xffffffffu), (uint32_t)(seed >> 32), n_offset, logits);
+  return launch_status();
+}
+
+extern "C" int mgp_relaxed_onehot_sample(const float* logits, int64_t N, int32_t K, int32_t S, float tau,
+                                         const float* noise_u, uint64_t seed, int64_t n_offset, float* W,
+                                         mgp_stream_t stream) {
+  if (!logits) return -1;
+  if (N < 0) return -2;
+  if (K < 1) return -3;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -4;
+  if (!(tau > 0.f)) return -5;
+  if (n_offset < 0) return -8;
+  if (!W) return -9;
+  if (N == 0) return MGP_OK;
+  const int64_t total = N * (int64_t)S;
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+  hipStream_t s = (hipStream_t)stream;
+#define MGP_RO_CASE(KM)                                                                                        \
+  if (K <= KM) {                                                                                                \
+    hipLaunchKernelGGL(relaxed_onehot_kernel<KM>, grid, block, 0, s, logits, N, K, S, 1.f / tau, noise_u, k0, k1, \
+                       n_offset, W);                                                                            \
+  } else
+  MGP_RO_CASE(4) MGP_RO_CASE(8) MGP_RO_CASE(16) MGP_RO_CASE(32) {}
+#undef MGP_RO_CASE
+  return launch_status();
+}
+
+extern "C" int mgp_e_log_p_y(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
+                             int64_t ldf, int64_t stride_s, const float* Y, const float* lik_var,
+                             const float* assign_lik_var, float multiclass_eps, const float* W, int64_t N,
+                             int32_t K, int32_t S, float* out, mgp_stream_t stream) {
+  const bool mc = lik_var == nullptr, mod = assign_lik_var != nullptr;
+  if (!mu_f) return -1;
+  if (!var_f) return -2;
+  if (mod && !mu_a) return -3;
+  if (mod && !var_a) return -4;
+  if (ldf < (S > 1 ? stride_s * (S - 1) + N : N)) return -5;
+  if (stride_s < 0) return -6;
+  if (!Y) return -7;
+  if (mc && !(multiclass_eps > 0.f && multiclass_eps < 1.f)) return -10;
+  if (!W) return -11;
+  if (N < 0) return -12;
+  if (K < 1 || (mc && K < 2)) return -13;
+  if (K > 32) return MGP_ERR_UNSUPPORTED;
+  if (S < 1) return -14;
+  if (!out) return -15;
+  if (N == 0) return MGP_OK;
+  float a = 0.f, b = 0.f;
+  if (mc) {
+    a = logf(1.f - multiclass_eps);
+    b = logf(multiclass_eps / (float)(K - 1));
+  }
+  const dim3 grid((unsigned)((N + 255) / 256)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define MGP_ELPY(KM, MOD, MC)                                                                                  \
+  hipLaunchKernelGGL((e_log_p_y_kernel<KM, MOD, MC>), grid, block, 0, s, mu_f, var_f, mu_a, var_a, ldf,        \
+                     stride_s, Y, lik_var, assign_lik_var, W, N, K, S, a, b, out)
+#define MGP_ELPY_CASE(KM)                                                                                      \
+  if (K <= KM) {                                                                                                \
+    if (mc && mod) MGP_ELPY(KM, true, true);                                                                    \
+    else if (mc) MGP_ELPY(KM, false, true);                                                                     \
+    else if (mod) MGP_ELPY(KM, true, false);                                                                    \
+    else MGP_ELPY(KM, false, false);                                                                            \
+  } else
+  MGP_ELPY_CASE(4) MGP_ELPY_CASE(8) MGP_ELPY_CASE(16) MGP_ELPY_CASE(32) {}
+#undef MGP_ELPY_CASE
+#undef MGP_ELPY
+  return launch_status();
+}
 
 static int predict_samples_run(const float* mu_f, const float* var_f, const float* mu_a, const float* var_a,
                                int64_t ldf, const float* lik_var, int64_t N, int32_t K, int32_t S, float tau,

@@ -1899,6 +1899,8 @@ static int conditional_backward(
   if (!aligned16(workspace) || !aligned16(Afr)) return MGP_ERR_ALIGN;
   const size_t img = mgp_x6_cols_bytes(M, N);
   if (img >= ((size_t)1 << 32) || (size_t)M * ((N + 3) / 4 * 4) * 4 >= ((size_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  // the S_k / L_k image is addressed through one 32-bit buffer resource by the gA kernels
+  if (lower_planes(M, K) >= ((size_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const CondBwdWs L = cond_bwd_layout(M, N, K);
   char* ws = (char*)workspace;

@@ -262,22 +262,120 @@ class SVGPModified:
         return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, k1 - k0,
                                          planes=expert_planes(), fmt=fmt)
 
+    def _marginals_kn(self, Xnew):
+        """Xnew [..., N, D] -> (fmean, fvar, S, N, stride_s, lead): expert-major [K, cols]
+        marginals where sample s of point n is column s * stride_s + n.  S tiled copies
+        of one input (SGP.integrate, models.py:35-36) are computed once (stride_s = 0)."""
+        X = self.kernel._x(Xnew)
+        if X.dim() == 2:
+            fm, fv = self.conditional_kn(X)
+            return fm, fv, 1, X.shape[0], 0, ()
+        lead, N = X.shape[:-2], X.shape[-2]
+        Xs = X.reshape(-1, N, X.shape[-1])
+        S = Xs.shape[0]
+        if S > 1 and bool(torch.equal(Xs, Xs[:1].expand_as(Xs))):
+            fm, fv = self.conditional_kn(Xs[0])
+            return fm, fv, S, N, 0, lead
+        fm, fv = self.conditional_kn(Xs.reshape(-1, X.shape[-1]))
+        return fm, fv, S, N, N, lead
+
+    def posterior(self, precompute_cache=None):
+        """SVGPModified.posterior (models.py:148-160): the posterior plugin object whose
+        _conditional_fused runs K1-K5 on this layer's current state (a NOCACHE-style
+        view: the variational parameters are read at call time, whatever the cache type)."""
+        return IndependentPosteriorSingleOutputModified(
+            self.kernel, self.inducing_variable, self.q_mu, self.q_sqrt, whiten=self.whiten,
+            mean_function=None, precompute_cache=precompute_cache, layer=self)
+
+    @property
+    def trainable_variables(self):
+        """GPflow Module.trainable_variables of the layer: Z, q_mu, q_sqrt, kernel variance
+        and lengthscales (device tensors holding the constrained values)."""
+        return (self.Z, self.q_mu, self.q_sqrt, self.kernel.variance, self.kernel.lengthscales)
+
     def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
-        """GPflow SVGP.predict_f(Xnew, full_cov=False) through the Modified posterior
-        (models.py:129-144).  Xnew [..., N, D] -> mean, var [..., N, K]."""
+        """GPflow SVGP.predict_f(Xnew): posterior(NOCACHE).fused_predict_f, i.e. the
+        Modified posterior's _conditional_fused (models.py:129-144).
+        Xnew [..., N, D] -> mean, var [..., N, K]."""
+        return self.posterior(PrecomputeCacheType.NOCACHE).fused_predict_f(Xnew, full_cov, full_output_cov)
+
+
+class PrecomputeCacheType:
+    """gpflow.posteriors.PrecomputeCacheType (TENSOR / VARIABLE / NOCACHE)."""
+    TENSOR = "tensor"
+    VARIABLE = "variable"
+    NOCACHE = "nocache"
+
+
+class IndependentPosteriorSingleOutputModified:
+    """The reference's posterior plugin (models.py:126-144): GPflow's IndependentPosterior
+    with _conditional_fused overridden to Knn = K_diag, Kmm = Kuu + jitter,
+    Kmn = K(Z, Xnew), base_conditional(white=True).  Here _conditional_fused is the
+    K1 -> K3 -> K4 -> K5 chain of the layer it was made from (SVGPModified.posterior)."""
+
+    def __init__(self, kernel, inducing_variable, q_mu, q_sqrt, whiten=True, mean_function=None,
+                 precompute_cache=None, layer=None):
+        if not whiten:
+            raise NotImplementedError("only the whitened posterior is on the hot path")
+        if mean_function is not None:
+            raise NotImplementedError("the reference layers use the Zero mean function")
+        if layer is None:
+            raise ValueError("the posterior runs on an SVGPModified layer's kernels (layer=...)")
+        self.kernel, self.X_data, self.q_mu, self.q_sqrt = kernel, inducing_variable, q_mu, q_sqrt
+        self.whiten, self.mean_function = whiten, mean_function
+        self.cache_type = precompute_cache
+        self._layer = layer
+
+    def _conditional_fused(self, Xnew, full_cov=False, full_output_cov=False):
+        """(fmean, fvar) [..., N, K] of the whitened SVGP marginals (models.py:129-144)."""
         if full_cov or full_output_cov:
             raise NotImplementedError("full_cov predictions are not used by the SMGP path")
-        X = self.kernel._x(Xnew)
-        lead = X.shape[:-2]
-        Xf = X.reshape(-1, X.shape[-1])
-        if len(lead) and X.shape[0] > 1 and bool(torch.equal(X, X[:1].expand_as(X))):
-            Xf = X.reshape(-1, *X.shape[-2:])[0]            # tiled copies (SGP.integrate)
-            fm, fv = self.conditional_kn(Xf)
-            shape = (*lead, Xf.shape[0], self.num_latent_gps)
+        fm, fv, S, N, stride, lead = self._layer._marginals_kn(Xnew)
+        K = fm.shape[0]
+        shape = (*lead, N, K)
+        if stride == 0 and len(lead):
             return fm.t().expand(shape), fv.t().expand(shape)
-        fm, fv = self.conditional_kn(Xf)
-        shape = (*lead, X.shape[-2], self.num_latent_gps)
         return fm.t().reshape(shape), fv.t().reshape(shape)
+
+    def fused_predict_f(self, Xnew, full_cov=False, full_output_cov=False):
+        """GPflow BasePosterior.fused_predict_f: _conditional_fused + the (Zero) mean function."""
+        return self._conditional_fused(Xnew, full_cov, full_output_cov)
+
+    def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
+        return self.fused_predict_f(Xnew, full_cov, full_output_cov)
+
+
+class RelaxedOneHotCategorical:
+    """tfp.distributions.RelaxedOneHotCategorical(temperature, logits) as SMGP.W_dist
+    returns it (models.py:60): logits [S * N, K] on the device; sample() runs the
+    Gumbel-softmax kernel.  The first sample uses the key the logits were drawn with,
+    so W_dist(Xt) -> sample(1) -> E_log_p_Y reproduces _build_likelihood with that key."""
+
+    def __init__(self, temperature, logits, rows, seed=None, n_offset=0):
+        self.temperature = float(temperature)
+        self.logits = logits
+        self._S, self._N = rows
+        self._seed = seed
+        self._n_offset = int(n_offset)
+        self._draws = 0
+
+    def sample(self, sample_shape=1, noise_u=None, seed=None):
+        """[n, S * N, K] relaxed one-hot samples; noise_u: explicit uniforms [n?, S, N, K]."""
+        n = int(sample_shape if not isinstance(sample_shape, (tuple, list)) else sample_shape[0])
+        outs = []
+        for i in range(n):
+            u = None
+            if noise_u is not None:
+                u = noise_u[i] if noise_u.dim() == 4 else noise_u
+            if seed is not None:
+                key = _splitmix64(int(seed) + i) if i else int(seed)
+            else:
+                key = self._seed if self._draws == 0 and self._seed is not None else _splitmix64(
+                    (self._seed or 0) * 0x100000001B3 + 0x5EED + self._draws)
+            self._draws += 1
+            outs.append(ops.relaxed_onehot_sample(self.logits, self._S, self._N, self.temperature, noise_u=u,
+                                                  seed=key, n_offset=self._n_offset))
+        return torch.stack(outs)
 
 
 class SGP:
@@ -349,7 +447,9 @@ class SMGP(SGP):
 
     # ------------------------------------------------------------------ internals
     def _buffers(self, N, train=False):
-        key = (N, conditional_mode(), bool(train))
+        # the image formats decide which buffers exist (e.g. the C_k images of the
+        # split-f16 training step), so a format switch between calls gets its own set
+        key = (N, conditional_mode(), bool(train), forward_image_format(train), expert_cross())
         b = self._bufs.get(key)
         if b is not None:
             return b
@@ -529,6 +629,41 @@ class SMGP(SGP):
         """Fresh Philox key per evaluation (TF's stateful RNG advances per call)."""
         self._draws += 1
         return _splitmix64(self.seed * 0x100000001B3 + self._draws)
+
+    # ------------------------------------------------------------------ reference methods
+    def W_dist(self, Xt, noise_z=None, seed=None, n_offset=0):
+        """SMGP.W_dist (models.py:55-61): the assign layer's marginals, reparameterised
+        with z ~ N(0, 1) [S, N, K] (utils.py:26-27) into logits [S * N, K], as a
+        RelaxedOneHotCategorical(1e-2).  noise_z: explicit normals [S, N, K]; else
+        Philox with `seed` (a fresh key per call when None), K6's z stream."""
+        fm, fv, S, N, stride, _ = self.assign_layer._marginals_kn(Xt)
+        if seed is None and noise_z is None:
+            seed = self.next_seed()
+        logits = ops.assign_logits(fm, fv, S, N, stride, noise_z=noise_z, seed=seed or 0, n_offset=n_offset)
+        return RelaxedOneHotCategorical(TAU, logits.reshape(S * N, self.K), (S, N), seed=seed, n_offset=n_offset)
+
+    def E_log_p_Y(self, Xt, Y, W_SND):
+        """SMGP.E_log_p_Y (models.py:63-67): logsumexp_S(sum_K W ve) - log S -> [N]
+        (device float32), ve the pred likelihood's variational expectation."""
+        fm, fv, S, N, stride, _ = self.pred_layer._marginals_kn(Xt)
+        Yd = _to_dev(Y, self.device).reshape(-1).contiguous()
+        W = _to_dev(W_SND, self.device)
+        mc = self._mc_eps()
+        lik_var = None if mc is not None else self.likelihood.likelihood.variance.reshape(-1)
+        extra = {}
+        if self._assign_lik_var() is not None:   # SMGPModified.E_log_p_Y (models.py:112-123)
+            fa, va, Sa, Na, stride_a, _ = self.assign_layer._marginals_kn(Xt)
+            if (Sa, Na, stride_a) != (S, N, stride):
+                raise ValueError("the two layers' marginals disagree in shape")
+            extra = dict(mu_a=fa, var_a=va, assign_lik_var=self._assign_lik_var())
+        return ops.e_log_p_y(fm, fv, Yd, lik_var, W, S, N, stride, multiclass_eps=mc, **extra)
+
+    @property
+    def trainable_variables(self):
+        """GPflow Module.trainable_variables (utils/training_utils.py:10): the device
+        tensors of trainable_parameters(), in its order (constrained values; the
+        optimiser keeps the unconstrained shadows, modulatedgps_amd.training.AdamTF)."""
+        return tuple(t for _, t, _ in self.trainable_parameters())
 
     # ------------------------------------------------------------------ ELBO
     def _build_likelihood(self, X, Y, noise=None, seed=None, n_offset=0, n_total=None,

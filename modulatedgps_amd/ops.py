@@ -793,3 +793,76 @@ def multiclass_predict(fmean, fvar, epsilon):
     _lib.call("mgp_multiclass_predict", fmean.data_ptr(), fvar.data_ptr(), _ld(fmean), N, K, float(epsilon),
               ym.data_ptr(), yv.data_ptr(), _stream())
     return ym, yv
+
+
+# --------------------------------------------------------------------------- method-level API
+def _latents_check(mu, var, name):
+    _check(mu, "mu_" + name, 2), _check(var, "var_" + name, 2)
+    if _ld(var) != _ld(mu) or var.shape != mu.shape:
+        raise ValueError(f"mu_{name} and var_{name} must share shape and leading dimension")
+
+
+def assign_logits(mu_a, var_a, S, N, stride_s=0, noise_z=None, seed=0, n_offset=0, jitter=None):
+    """SMGP.W_dist's logits (models.py:56-59, utils.py:26-27): [S, N, K] =
+    mu_a + z sqrt(var_a + jitter); mu_a / var_a expert-major [K, >= (S-1) stride_s + N]."""
+    jitter = default_jitter() if jitter is None else jitter
+    _latents_check(mu_a, var_a, "a")
+    K = mu_a.shape[0]
+    out = torch.empty(S, N, K, dtype=F32, device=mu_a.device)
+    zp = None
+    if noise_z is not None:
+        _check(noise_z, "noise_z", 3)
+        if tuple(noise_z.shape) != (S, N, K):
+            raise ValueError("explicit noise must be [S, N, K]")
+        noise_z = noise_z.contiguous()
+        zp = noise_z.data_ptr()
+    _lib.call("mgp_assign_logits", mu_a.data_ptr(), var_a.data_ptr(), _ld(mu_a), int(stride_s), N, K, S,
+              float(jitter), zp, int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), out.data_ptr(), _stream())
+    return out
+
+
+def relaxed_onehot_sample(logits, S, N, tau=1e-2, noise_u=None, seed=0, n_offset=0):
+    """RelaxedOneHotCategorical(tau, logits).sample() on logits [S * N, K] (rows s * N + n)."""
+    _check(logits, "logits")
+    K = logits.shape[-1]
+    if logits.numel() != S * N * K:
+        raise ValueError("logits must hold S * N rows of K")
+    logits = logits.contiguous()
+    W = torch.empty(S * N, K, dtype=F32, device=logits.device)
+    up = None
+    if noise_u is not None:
+        _check(noise_u, "noise_u")
+        if noise_u.numel() != S * N * K:
+            raise ValueError("explicit noise must be [S, N, K]")
+        noise_u = noise_u.contiguous()
+        up = noise_u.data_ptr()
+    _lib.call("mgp_relaxed_onehot_sample", logits.data_ptr(), N, K, S, float(tau), up,
+              int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), W.data_ptr(), _stream())
+    return W
+
+
+def e_log_p_y(mu_f, var_f, Y, lik_var, W, S, N, stride_s=0, mu_a=None, var_a=None, assign_lik_var=None,
+              multiclass_eps=None):
+    """SMGP.E_log_p_Y (models.py:63-67; SMGPModified :112-123 with assign_lik_var) -> [N]."""
+    _latents_check(mu_f, var_f, "f")
+    K = mu_f.shape[0]
+    Y = Y.reshape(-1)
+    _check(Y, "Y"), _check(W, "W")
+    if Y.numel() != N or not Y.is_contiguous():
+        raise ValueError("Y must be contiguous with N elements")
+    if W.numel() != S * N * K:
+        raise ValueError("W must be [S, N, K]")
+    W = W.contiguous()
+    if multiclass_eps is None:
+        _check(lik_var, "lik_var")
+    if assign_lik_var is not None:
+        _check(assign_lik_var, "assign_lik_var")
+        _latents_check(mu_a, var_a, "a")
+        if _ld(mu_a) != _ld(mu_f):
+            raise ValueError("the two layers' latents must share a leading dimension")
+    out = torch.empty(N, dtype=F32, device=mu_f.device)
+    ptr = lambda t: t.data_ptr() if t is not None else None
+    _lib.call("mgp_e_log_p_y", mu_f.data_ptr(), var_f.data_ptr(), ptr(mu_a), ptr(var_a), _ld(mu_f), int(stride_s),
+              Y.data_ptr(), None if multiclass_eps is not None else lik_var.data_ptr(), ptr(assign_lik_var),
+              float(multiclass_eps or 0.0), W.data_ptr(), N, K, S, out.data_ptr(), _stream())
+    return out

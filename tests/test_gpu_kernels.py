@@ -239,19 +239,21 @@ def test_elbo_terms_rounding_negative_assign_var(device):
     """A float32 marginal variance of the assign layer can round below -jitter
     where the reference's float64 one sits at ~0 (seen in demo_tf2_modified_
     multiclass after ~1400 Adam steps: the sqrt of the reparameterisation went
-    NaN and so did the step).  K6 samples with max(var, 0) + jitter: equal to
-    the oracle on the clamped variances, and the backward stays finite with a
-    zero variance gradient where the clamp is active."""
+    NaN and so did the step).  K6 samples with sqrt(max(var + jitter, 0)): equal
+    to the oracle on the clamped variances, the reference's own value on
+    (-jitter, 0], and the backward stays finite with a zero variance gradient
+    only where the clamp is active."""
     from modulatedgps_amd import ops
     N, K, S = 1000, 3, 25
     rng = np.random.default_rng(5)
     mu_f, mu_a = rng.standard_normal((2, N, K))
     var_f, var_a = rng.uniform(0.05, 1.0, (2, N, K))
     var_a[::7, 1] = -3e-6                      # below -jitter (1e-6)
+    var_a[3::7, 2] = -5e-7                     # inside (-jitter, 0]: the reference is finite there
     Y = rng.standard_normal((N, 1))
     lv = rng.uniform(0.2, 1.0, (1, K))
     z, u = R.explicit_noise(S, N, K, seed=3)
-    W = R.assignment_weights(mu_a[None], np.maximum(var_a, 0.0)[None], z, u)
+    W = R.assignment_weights(mu_a[None], np.maximum(var_a, -R.JITTER)[None], z, u)
     r = np.sum(R.e_log_p_y(mu_f[None], var_f[None], Y, lv, W, S))
     dev = lambda a: ops.as_padded(_t(a.T, device))
     args = (dev(mu_f), dev(var_f), dev(mu_a), dev(var_a), _t(Y[:, 0], device), _t(lv[0], device), S)
@@ -261,6 +263,7 @@ def test_elbo_terms_rounding_negative_assign_var(device):
     G = ops.elbo_terms_backward(*args, noise=noise)[0].float().cpu().numpy()
     assert np.all(np.isfinite(G[:, :K, :N]))
     assert np.all(G[3, 1, :N:7] == 0.0)
+    assert np.count_nonzero(G[3, 2, 3:N:7]) > 0.9 * len(range(3, N, 7))
 
 
 @pytest.mark.parametrize("N,M,K,D,ls", [(1000, 25, 3, 1, 0.5), (8192, 256, 4, 2, 0.15),

@@ -81,16 +81,21 @@ def test_elbo_and_grad(device, N, M, K, D, ls, S, modified, fmt):
     config.set_expert_cross("f8" if fmt == "f16x8" else "f16")
     try:
         # f16x8 (e4m3 cross terms, ~9x the f32-class error of K5's term by design):
-        # the near-cancelling assign.variance gradient at config-5 shapes measured
-        # 2.9-3.0e-4 normwise against float64, so its floor is 4e-4
-        _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, floor=4e-4 if fmt == "f16x8" else FLOOR)
+        # assign.variance's gradient is a near-cancelling sum over all N of the fvar_a
+        # terms K5 produces (d fvar / d variance = 1 - ||A||^2 + ||L^T A||^2 terms of
+        # opposite sign), so K5's 2^-15 per-product cross-term error shows there first:
+        # 2.9-3.0e-4 normwise against float64 at config-5 shapes.  Only that block gets
+        # the 4e-4 floor; every other block keeps FLOOR.
+        floors = {"assign.variance": 4e-4} if fmt == "f16x8" else None
+        _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, floors=floors)
     finally:
         config.set_expert_format(old)
         config.set_expert_cross(old_cross)
 
 
-def _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, floor=None):
+def _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, floor=None, floors=None):
     floor = FLOOR if floor is None else floor
+    floors = floors or {}
     X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
     a_var = np.linspace(0.3, 0.9, K)[None, :] if modified else None
     z, u = R.explicit_noise(S, N, K, seed=5)
@@ -110,7 +115,7 @@ def _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, floor=None):
         errs32[n] = normwise(g_f32[n].reshape(got.shape), ref)
     print({k: f"{v:.1e}/{errs32[k]:.1e}" for k, v in errs.items()})
     for n, err in errs.items():
-        assert err < max(floor, 1.5 * errs32[n]), (n, err, errs32[n])
+        assert err < max(floors.get(n, floor), 1.5 * errs32[n]), (n, err, errs32[n])
 
 
 def test_adam_step(device):
