@@ -27,6 +27,9 @@
 // recomputes the 64^3 panels it needs); every launch carries all `batch`
 // matrices (blockIdx.y).  nb + 1 launches per factorisation.
 #include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "mgp_common.hpp"
 
@@ -41,12 +44,21 @@ constexpr int kMaxBatch = 8;
 
 #ifdef MGP_DBG_STAMPS
 __device__ unsigned long long g_stamps[64 * 16];
+// persistent path: chain stamps [batch 2][step 128][8]; worker phase totals [batch 2][wg 128][8]
+__device__ unsigned long long g_pchain[2 * 128 * 8];
+__device__ unsigned long long g_pwork[2 * 128 * 8];
+#define PSTAMP(b, j, k) do { if (threadIdx.x == 0 && (b) < 2 && (j) < 128) g_pchain[((b) * 128 + (j)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define PWACC(b, w, k, v) do { if (threadIdx.x == 0 && (b) < 2 && (w) < 128) g_pwork[((b) * 128 + (w)) * 8 + (k)] += (v); } while (0)
+#define PNOW() __builtin_amdgcn_s_memtime()
 #define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 // 100 MHz reference clock (one time base for every CU): slots 14 / 15
 #define RSTAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(j, k) do {} while (0)
 #define RSTAMP(j, k) do {} while (0)
+#define PSTAMP(b, j, k) do {} while (0)
+#define PWACC(b, w, k, v) do {} while (0)
+#define PNOW() 0ull
 #endif
 
 struct CholArgs {
@@ -60,6 +72,9 @@ struct CholArgs {
   float* lt_absmax[kMaxBatch];                    // optional per batch: max |L^-T| (float bits, atomicMax)
   double* ws; int64_t strideWS;                   // per batch: W, B [Mp][Mp], D [nb][64][64]
   int64_t M, Mp; int nb;
+  // persistent path (chol_persist): per-batch sync words and the shared task table
+  int* sync; int64_t strideSync;                  // per batch: Wver[nb][nb], Bver[nb][nb], Dready[nb], head, err
+  int* tasks; int ntask;                          // task table (chol_task_order), built by chol_prep
 };
 
 __device__ __forceinline__ double* ws_W(const CholArgs& a, int b) { return a.ws + (int64_t)b * a.strideWS; }
@@ -153,6 +168,27 @@ __device__ __forceinline__ float tile_store_f32_max(float* __restrict__ g, int64
       g[(int64_t)r * ld + c] = v;
       m = fmaxf(m, fabsf(v));
     }
+  }
+  return m;
+}
+
+// Full 64x64 tile -> float32 global with 16-B stores (ld % 4 == 0, 16-B aligned rows:
+// chol_run checks both), optionally transposed; partial tiles fall back to the
+// element loop.  Returns this thread's max |stored value|.
+__device__ __forceinline__ float tile_store_f32_v4(float* __restrict__ g, int64_t ld, const double* __restrict__ s,
+                                                   bool transpose, int nr, int nc) {
+  if (nr < CB || nc < CB) return tile_store_f32_max(g, ld, s, transpose, nr, nc);
+  float m = 0.f;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 4, c = (idx & 15) * 4;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = (float)(transpose ? s[(c + k) * LDT + r] : s[r * LDT + c + k]);
+      m = fmaxf(m, fabsf(v[k]));
+    }
+    *reinterpret_cast<float4*>(g + (int64_t)r * ld + c) = make_float4(v[0], v[1], v[2], v[3]);
   }
   return m;
 }
@@ -688,6 +724,96 @@ __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, cons
   }
 }
 
+// ------------------------------------------------------------------ persistent-path task order
+// The single-launch factorisation (chol_persist) runs the tile work of all steps
+// from one task table; every product is formed once and handed on through the
+// workspace (no per-tile recomputation).  Task kinds (nb = Mp / 64 tile rows):
+//   PAN(i, j)   L_ij = W_ij D_j^T, in place of W_ij (i >= j + 2; L_{j+1,j} is the chain's);
+//   U(i, l, j)  trailing update W_il -= L_ij L_lj^T of step j (j < l <= i), except the
+//               look-ahead tile (j+1, j+1), which the chain updates and factors;
+//   XR(j, c)    row block j of X = L^-1: X_jc = D_j B_jc, in place of B_jc (c < j);
+//   FU(i, c, j) forward substitution B_ic -= L_ij X_jc (i > j, c <= j; X_jj = D_j).
+// Order per step j: the tasks the chain's next step waits for (PAN(j+2, j),
+// U(j+2, j+1, j), U(j+2, j+2, j)), the other panels, the other updates by column;
+// the forward-substitution work of step j (F_j = XR(j, .), FU(., ., j)), needed only
+// at the end, one step later:  A_0 B_0 C_0, A_1 B_1 C_1, F_0, A_2 B_2 C_2, F_1, ...,
+// F_{nb-2}, XR(nb-1, .).  Every dependency of a task lies earlier in the table or is
+// a chain output whose own inputs do, so in-order dequeueing cannot deadlock.
+enum { kTaskPan = 0, kTaskU = 1, kTaskXR = 2, kTaskFU = 3 };
+
+// block q: q < 4 (nb - 1): step j = q / 4, slot s = q % 4 (A_j, B_j, C_j, F_{j-1});
+// then F_{nb-2}, then the last row.
+__host__ __device__ inline int task_block_count(int nb) { return 4 * (nb - 1) + 2; }
+__host__ __device__ inline int task_block_size(int q, int nb) {
+  if (q < 4 * (nb - 1)) {
+    const int j = q / 4, slot = q % 4, T = nb - 1 - j;
+    if (slot == 0) return T >= 2 ? 3 : 0;
+    if (slot == 1) return T >= 3 ? T - 2 : 0;
+    if (slot == 2) return T * (T + 1) / 2 - 1 - (T >= 2 ? 2 : 0);
+    return j >= 1 ? (j - 1) + (nb - j) * j : 0;      // F_{j-1}
+  }
+  if (q == 4 * (nb - 1)) return nb >= 2 ? (nb - 2) + (nb - 1 - (nb - 2)) * (nb - 1) : 0;   // F_{nb-2}
+  return nb - 1;                                                                          // XR(nb-1, .)
+}
+__host__ __device__ inline int task_count(int nb) {
+  int n = 0;
+  for (int q = 0; q < task_block_count(nb); ++q) n += task_block_size(q, nb);
+  return n;
+}
+__host__ __device__ inline int task_encode(int kind, int j, int i, int l) {
+  return (kind << 24) | (j << 16) | (i << 8) | l;
+}
+// entry e of the forward-substitution block F_j
+__device__ __forceinline__ int task_f(int j, int e) {
+  if (e < j) return task_encode(kTaskXR, j, j, e);
+  e -= j;
+  return task_encode(kTaskFU, j, j + 1 + e / (j + 1), e % (j + 1));
+}
+__device__ __forceinline__ int task_entry(int q, int e, int nb) {
+  if (q < 4 * (nb - 1)) {
+    const int j = q / 4, slot = q % 4, T = nb - 1 - j;
+    if (slot == 0) {
+      if (e == 0) return task_encode(kTaskPan, j, j + 2, j);
+      return task_encode(kTaskU, j, j + 2, e == 1 ? j + 1 : j + 2);
+    }
+    if (slot == 1) return task_encode(kTaskPan, j, j + 3 + e, j);
+    if (slot == 2) {
+      // the column-major triangle (l = j+1 .., i = l ..) without (j+1, j+1), (j+2, j+1), (j+2, j+2)
+      int f = e + 2;
+      if (T >= 2 && f >= T) ++f;                       // (j+2, j+2) sits at f = T
+      int l = j + 1;
+      while (f >= nb - l) { f -= nb - l; ++l; }
+      return task_encode(kTaskU, j, l + f, l);
+    }
+    return task_f(j - 1, e);
+  }
+  if (q == 4 * (nb - 1)) return task_f(nb - 2, e);
+  return task_encode(kTaskXR, nb - 1, nb - 1, e);
+}
+
+// Per-batch sync words of the persistent path: Wver[nb][nb] (tile (i, l) of W: the
+// number of updates applied, then l + 1 once it holds L_il), Bver[nb][nb] (tile
+// (i, c) of B: updates applied, then +1 once it holds X_ic), Dready[nb], head (next
+// task), err (a bounded wait gave up).
+__host__ __device__ inline int64_t chol_sync_words(int nb) { return ((int64_t)2 * nb * nb + nb + 2 + 63) / 64 * 64; }
+
+// chol_prep's share of the persistent state: zero this batch's sync words (Dready[0]
+// = 1: prep factors tile (0, 0)) and, for batch 0, fill the task table (block q of
+// the order by workgroup q).
+__device__ __forceinline__ void prep_persist_state(const CholArgs& a, int b) {
+  const int nb = a.nb;
+  int* s = a.sync + (int64_t)b * a.strideSync;
+  const int64_t nw = chol_sync_words(nb), d0 = (int64_t)2 * nb * nb;
+  for (int64_t w = (int64_t)blockIdx.x * kCholThreads + threadIdx.x; w < nw; w += (int64_t)gridDim.x * kCholThreads)
+    s[w] = (w == d0) ? 1 : 0;
+  const int q = blockIdx.x;
+  if (b != 0 || q >= task_block_count(nb)) return;
+  int start = 0;
+  for (int r = 0; r < q; ++r) start += task_block_size(r, nb);
+  const int n = task_block_size(q, nb);
+  for (int e = threadIdx.x; e < n; e += kCholThreads) a.tasks[start + e] = task_entry(q, e, nb);
+}
+
 // ------------------------------------------------------------------ prep launch
 __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   __shared__ double s1[CB * LDT], s2[CB * LDT], col[CB];
@@ -708,6 +834,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   auto elem = [&](int64_t gr, int64_t gc) {
     return a.A ? input_elem(a, b, gr, gc) : kuu_elem(a, Zb, sil, varb, gr, gc);
   };
+  if (a.sync) prep_persist_state(a, b);
   if (blockIdx.x == 0) {  // factor tile (0, 0) straight from the input (dispatched first)
     if (threadIdx.x == 0) {
       a.info[b] = 0;
@@ -885,6 +1012,386 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   row_to_global(Bt(i, c), Mp, u);
 }
 
+// ------------------------------------------------------------------ persistent launch
+// chol_persist: the nb - 1 steps after chol_prep in ONE launch.  Per batch entry,
+// workgroup 0 is the CHAIN: it keeps D_j in LDS and, step after step, forms the
+// look-ahead panel P = W_{j+1,j} D_j^T, applies P P^T to W_{j+1,j+1}, factors it
+// (factor_diag_tile) and publishes D_{j+1}; it never waits for a launch boundary.
+// Workgroups 1.. are WORKERS: they take tasks from the table in order (one
+// returning atomic add per task) and wait only for the tiles and D a task reads.
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, the flag form with
+// sc1 payload): every byte another workgroup reads is stored write-through (sc1) by
+// 8/16-B buffer stores, every storing wave drains vmcnt(0), the workgroup barrier,
+// then ONE lane's relaxed agent-scope store of the version / ready word; consumers
+// poll with relaxed agent loads (sc1) and read every handed-off byte with sc1
+// buffer loads (no acquire fence needed).  Every wait is bounded: on a give-up the
+// workgroup records err and info and leaves.
+typedef __attribute__((address_space(1))) int gint;
+constexpr int kSc1 = 16;                 // buffer instruction aux bits: sc1
+constexpr uint32_t kSpinLimit = 1u << 22;  // polls (~s_sleep 2 each) before a wait gives up
+
+// sc1 buffer accesses: voff = this lane's part of the offset (a VGPR), soff = the
+// wave-uniform part (an SGPR: tile origin + compile-time element offsets)
+__device__ __forceinline__ double2 ld16c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kSc1));
+}
+__device__ __forceinline__ double ld8c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kSc1));
+}
+__device__ __forceinline__ void st16c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x, double y) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, make_double2(x, y)), r, voff, soff, kSc1);
+}
+__device__ __forceinline__ void st8c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
+  typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, x), r, voff, soff, kSc1);
+}
+// Lane offsets (bytes) of the two access patterns within a tile of leading dimension ld:
+//   pair pattern (tile_fetch / tile_store): element (tid / 32 + 8 it, 2 (tid % 32)), soff += 64 it ld
+//   row-stripe accumulator pattern (Blk4, blk4_foreach<true>): (16 w + lane / 16 + 4 q, 16 t + lane % 16)
+__device__ __forceinline__ uint32_t lane_off_pair(int64_t ld) {
+  return (uint32_t)((((int)threadIdx.x >> 5) * ld + (threadIdx.x & 31) * 2) * 8);
+}
+__device__ __forceinline__ uint32_t lane_off_row(int64_t ld) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  return (uint32_t)(((16 * w + (lane >> 4)) * ld + (lane & 15)) * 8);
+}
+// 64x64 f64 tile at byte offset `off` (leading dimension ld doubles), sc1 loads
+__device__ __forceinline__ void tile_fetch_c(TileRegs& t, __amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld) {
+  const uint32_t v = lane_off_pair(ld);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) t.v[it] = ld16c(r, v, off + (uint32_t)(it * 64 * ld));
+}
+__device__ __forceinline__ void row_from_global_c(Blk4& u, __amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld) {
+  const uint32_t v = lane_off_row(ld);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u.c[t][q] = ld8c(r, v, off + (uint32_t)((4 * q * ld + 16 * t) * 8));
+}
+__device__ __forceinline__ void row_to_global_c(__amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld, const Blk4& u) {
+  const uint32_t v = lane_off_row(ld);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st8c(r, v, off + (uint32_t)((4 * q * ld + 16 * t) * 8), u.c[t][q]);
+}
+__device__ __forceinline__ void tile_store_c(__amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld, const double* s) {
+  const uint32_t v = lane_off_pair(ld);
+  const int rr = threadIdx.x >> 5, c = (threadIdx.x & 31) * 2;
+#pragma unroll
+  for (int it = 0; it < 8; ++it)
+    st16c(r, v, off + (uint32_t)(it * 64 * ld), s[(rr + 8 * it) * LDT + c], s[(rr + 8 * it) * LDT + c + 1]);
+}
+__device__ __forceinline__ int flag_load(const int* p) {
+  return __hip_atomic_load((gint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void flag_store(int* p, int v) {
+  __hip_atomic_store((gint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// All threads: wait until every word p[k] >= v[k] (k < n <= 4; one lane polls each),
+// then the workgroup barrier.  Returns false (uniformly) when a wait gave up.
+__device__ __forceinline__ bool wait_all(const int* const (&p)[4], const int (&v)[4], int n, int* err,
+                                         int* s_flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int* mp = p[0];
+    int mv = v[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (lane == k) { mp = p[k]; mv = v[k]; }
+    bool ok = true;
+    for (uint32_t it = 0;; ++it) {
+      const bool mine = lane >= n || flag_load(mp) >= mv;
+      if (__all(mine)) break;
+      if (it >= kSpinLimit || flag_load(err) != 0) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) {
+      *s_flag = ok ? 1 : 0;
+      if (!ok) __hip_atomic_store((gint*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  const bool ok = *s_flag != 0;
+  __syncthreads();
+  return ok;
+}
+
+// All threads: one poll of the words (no wait); true (uniformly) when every p[k] >= v[k].
+__device__ __forceinline__ bool poll_all(const int* const (&p)[4], const int (&v)[4], int n, int* s_flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int* mp = p[0];
+    int mv = v[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (lane == k) { mp = p[k]; mv = v[k]; }
+    const bool mine = lane >= n || flag_load(mp) >= mv;
+    const bool all = __all(mine);
+    if (lane == 0) *s_flag = all ? 1 : 0;
+  }
+  __syncthreads();
+  const bool ok = *s_flag != 0;
+  __syncthreads();
+  return ok;
+}
+
+// every storing wave drains its sc1 stores, then one lane publishes `v` at p
+__device__ __forceinline__ void publish(int* p, int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) flag_store(p, v);
+}
+
+__global__ __launch_bounds__(kCholThreads) void chol_persist(CholArgs a) {
+  __shared__ double bufA[CB * LDT], bufB[CB * LDT], bufC[CB * LDT], col[CB];
+  __shared__ int s_task, s_flag;
+  const int b = blockIdx.y, nb = a.nb;
+  const int64_t Mp = a.Mp;
+  int* sync = a.sync + (int64_t)b * a.strideSync;
+  int* Wver = sync;
+  int* Bver = sync + nb * nb;
+  int* Dready = sync + 2 * nb * nb;
+  int* head = Dready + nb;
+  int* err = head + 1;
+  const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)ws_W(a, b), (short)0, (int)(uint32_t)(a.strideWS * 8), 0x00020000);
+  auto offW = [&](int i, int l) { return (uint32_t)(((int64_t)i * CB * Mp + (int64_t)l * CB) * 8); };
+  auto offB = [&](int i, int c) { return (uint32_t)((Mp * Mp + (int64_t)i * CB * Mp + (int64_t)c * CB) * 8); };
+  auto offD = [&](int j) { return (uint32_t)((2 * Mp * Mp + (int64_t)j * CB * CB) * 8); };
+  float* LinvT = a.LinvT + (int64_t)b * a.strideL;
+  float* lt_max = a.lt_absmax[0];
+#pragma unroll
+  for (int q = 1; q < kMaxBatch; ++q)
+    if (b == q) lt_max = a.lt_absmax[q];
+  auto store_linvT = [&](int c, int j, const double* sx) {  // X_jc -> LinvT block (c, j)
+    const int64_t gr = (int64_t)c * CB, gc = (int64_t)j * CB;
+    const float m = tile_store_f32_v4(LinvT + gr * a.ldl + gc, a.ldl, sx, true, (int)min<int64_t>(CB, a.M - gr),
+                                      (int)min<int64_t>(CB, a.M - gc));
+    if (lt_max) wave_absmax_atomic(m, lt_max);
+  };
+  auto store_L = [&](int i, int j, const double* s) {     // L block (i, j), float32
+    if (!a.L) return;
+    const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
+    tile_store_f32_v4(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s, false,
+                      (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
+  };
+  auto give_up = [&]() {
+    if (threadIdx.x == 0) atomicCAS(a.info + b, 0, -1);
+  };
+
+  if (blockIdx.x == 0) {
+    // ---------------------------------------------------------------- chain
+    double *sD = bufA, *s1 = bufB, *s2 = bufC;
+    {
+      TileRegs rD;
+      tile_fetch_c(rD, R, offD(0), CB);
+      tile_put(sD, rD);
+      __syncthreads();
+      store_linvT(0, 0, sD);                             // X_00 = D_0
+    }
+    for (int j = 0; j + 1 < nb; ++j) {
+      PSTAMP(b, j, 0);
+      const int* p[4] = {Wver + (j + 1) * nb + j, Wver + (j + 1) * nb + j + 1, Wver, Wver};
+      const int v[4] = {j, j, 0, 0};
+      if (!wait_all(p, v, 2, err, &s_flag)) { give_up(); return; }
+      PSTAMP(b, j, 1);
+      TileRegs r1, r2;
+      tile_fetch_c(r1, R, offW(j + 1, j), Mp);
+      tile_fetch_c(r2, R, offW(j + 1, j + 1), Mp);
+      tile_put(s1, r1);
+      tile_put(s2, r2);
+      __syncthreads();
+      PSTAMP(b, j, 2);
+      Blk4 pi = blk4_zero();
+      row_mma<true, 1>(pi, s1, sD, 1.0);                 // L_{j+1,j} = W_{j+1,j} D_j^T
+      row_to_global_c(R, offW(j + 1, j), Mp, pi);        // handed to the U tasks of column j + 1
+      __syncthreads();
+      blk4_to_lds<true>(s1, pi);
+      __syncthreads();
+      // column block 0 of W_{j+1,j+1} -= P P^T (one 16x16 block per wave); the rest
+      // beside the first panel sweep (factor_diag_tile's pending update).  The
+      // L_{j+1,j} stores drain meanwhile.
+      sub_outer_blk<4>(s2, 16 * (threadIdx.x >> 6), 0, s1, s1);
+      publish(Wver + (j + 1) * nb + j, j + 1);
+      __syncthreads();
+      PSTAMP(b, j, 3);
+      store_L(j + 1, j, s1);
+      factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1);
+      __syncthreads();
+      PSTAMP(b, j, 4);
+      tile_store_c(R, offD(j + 1), CB, s1);              // D_{j+1}, handed to the workers
+      publish(Dready + j + 1, 1);
+      PSTAMP(b, j, 5);
+      store_L(j + 1, j + 1, s2);
+      store_linvT(j + 1, j + 1, s1);                     // X_{j+1,j+1} = D_{j+1}
+      __syncthreads();
+      PSTAMP(b, j, 6);
+      double* t = sD; sD = s1; s1 = t;                   // D_{j+1} stays in LDS
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ workers
+  // Software-pipelined: the next task is dequeued while the current one's tiles load,
+  // and its tiles are loaded (when its inputs are already published) while the
+  // current one computes.  A task's operands: tile 1 -> s1, tile 2 -> s2 (optional),
+  // the read-modify-write tile in registers (optional), D_j -> sD (cached per step).
+  double *s1 = bufA, *s2 = bufB, *sD = bufC;
+  int dcur = -1;                                         // the step whose D is in sD
+  struct Plan { int kind, j, i, l; uint32_t o1, o2, ou; bool t2, u, d; };
+  auto decode = [&](int t, Plan& P) {
+    const int code = a.tasks[t];
+    P.kind = code >> 24; P.j = (code >> 16) & 255; P.i = (code >> 8) & 255; P.l = code & 255;
+    const int j = P.j, i = P.i, l = P.l;
+    P.t2 = P.u = P.d = false;
+    P.o2 = P.ou = 0;
+    if (P.kind == kTaskPan) { P.o1 = offW(i, j); P.d = true; }
+    else if (P.kind == kTaskU) {
+      P.o1 = offW(i, j); P.t2 = true;
+      if (l != i) { P.o2 = offW(l, j); P.u = true; P.ou = offW(i, l); }
+      else P.o2 = offW(i, i);
+    } else if (P.kind == kTaskXR) { P.o1 = offB(j, l); P.d = true; }
+    else {
+      P.o1 = offW(i, j);
+      if (l < j) { P.t2 = true; P.o2 = offB(j, l); P.u = true; P.ou = offB(i, l); }
+      else P.d = true;
+    }
+  };
+  auto deps = [&](const Plan& P, const int* (&p)[4], int (&v)[4]) {
+    const int j = P.j, i = P.i, l = P.l;
+    for (int k = 0; k < 4; ++k) { p[k] = Wver; v[k] = 0; }
+    if (P.kind == kTaskPan) {
+      p[0] = Dready + j; v[0] = 1; p[1] = Wver + i * nb + j; v[1] = j;
+      return 2;
+    }
+    if (P.kind == kTaskU) {
+      p[0] = Wver + i * nb + j; v[0] = j + 1; p[1] = Wver + i * nb + l; v[1] = j;
+      p[2] = Wver + l * nb + j; v[2] = j + 1;
+      return (l != i) ? 3 : 2;
+    }
+    if (P.kind == kTaskXR) {
+      p[0] = Dready + j; v[0] = 1; p[1] = Bver + j * nb + l; v[1] = j - l;
+      return 2;
+    }
+    p[0] = Wver + i * nb + j; v[0] = j + 1;
+    if (l < j) {
+      p[1] = Bver + j * nb + l; v[1] = j - l + 1; p[2] = Bver + i * nb + l; v[2] = j - l;
+      return 3;
+    }
+    p[1] = Dready + j; v[1] = 1;
+    return 2;
+  };
+  struct Regs { TileRegs r1, r2; Blk4 u; };
+  auto issue = [&](const Plan& P, Regs& G) {
+    tile_fetch_c(G.r1, R, P.o1, Mp);
+    if (P.t2) tile_fetch_c(G.r2, R, P.o2, Mp);
+    if (P.u) row_from_global_c(G.u, R, P.ou, Mp);
+  };
+  auto dequeue = [&]() {
+    if (threadIdx.x == 0) s_task = atomicAdd(head, 1);
+    __syncthreads();
+    const int t = s_task;
+    __syncthreads();
+    return t;
+  };
+
+  int tc = dequeue();
+  if (tc >= a.ntask) return;
+  Plan P;
+  decode(tc, P);
+  Regs G;
+  {
+    const int* p[4];
+    int v[4];
+    const int n = deps(P, p, v);
+    if (!wait_all(p, v, n, err, &s_flag)) { give_up(); return; }
+    issue(P, G);
+  }
+  const int wid = blockIdx.x;
+  for (;;) {
+    unsigned long long c0 = PNOW();
+    const int tn = dequeue();                            // overlaps the loads in flight
+    unsigned long long c1 = PNOW();
+    PWACC(b, wid, 0, c1 - c0);
+    if (P.d && dcur != P.j) {
+      TileRegs rD;
+      tile_fetch_c(rD, R, offD(P.j), CB);
+      tile_put(sD, rD);
+      dcur = P.j;
+      PWACC(b, wid, 7, 1);
+    }
+    tile_put(s1, G.r1);
+    if (P.t2) tile_put(s2, G.r2);
+    Blk4 u = P.u ? G.u : blk4_zero();
+    __syncthreads();
+    unsigned long long c2 = PNOW();
+    PWACC(b, wid, 2, c2 - c1);
+    // the next task's operands, in flight during this task's MFMAs (when published)
+    Plan Q;
+    bool have = tn < a.ntask, issued = false;
+    const int* pq[4];
+    int vq[4], nq = 0;
+    if (have) {
+      decode(tn, Q);
+      nq = deps(Q, pq, vq);
+      if (poll_all(pq, vq, nq, &s_flag)) { issue(Q, G); issued = true; }
+    }
+    unsigned long long c3 = PNOW();
+    PWACC(b, wid, 3, c3 - c2);
+    PWACC(b, wid, 6, issued ? 1 : 0);
+    PWACC(b, wid, 5, 1);
+    const int j = P.j, i = P.i, l = P.l;
+    if (P.kind == kTaskPan) {                            // L_ij = W_ij D_j^T in place
+      Blk4 pi = blk4_zero();
+      row_mma<true, 1>(pi, s1, sD, 1.0);
+      row_to_global_c(R, offW(i, j), Mp, pi);
+      __syncthreads();
+      blk4_to_lds<true>(s1, pi);
+      publish(Wver + i * nb + j, j + 1);
+      __syncthreads();
+      store_L(i, j, s1);
+    } else if (P.kind == kTaskU && l != i) {             // W_il -= L_ij L_lj^T
+      row_mma<true, 0>(u, s1, s2, -1.0);
+      row_to_global_c(R, offW(i, l), Mp, u);
+      publish(Wver + i * nb + l, j + 1);
+    } else if (P.kind == kTaskU) {                       // lower blocks of W_ii -= L_ij L_ij^T
+      diag_lower_update(s2, s1);
+      __syncthreads();
+      tile_store_c(R, offW(i, i), Mp, s2);
+      publish(Wver + i * nb + i, j + 1);
+    } else if (P.kind == kTaskXR) {                      // X_jc = D_j B_jc in place, LinvT block (c, j)
+      Blk4 x = blk4_zero();
+      col_mma_lower(x, sD, s1);
+      __syncthreads();
+      blk4_to_lds<false>(s1, x);
+      __syncthreads();
+      tile_store_c(R, offB(j, l), Mp, s1);
+      publish(Bver + j * nb + l, j - l + 1);
+      store_linvT(l, j, s1);
+    } else {                                             // FU: B_ic -= L_ij X_jc (X_jj = D_j)
+      if (l < j) row_mma<false, 0>(u, s1, s2, -1.0);
+      else row_mma<false, 2>(u, s1, sD, -1.0);
+      row_to_global_c(R, offB(i, l), Mp, u);
+      publish(Bver + i * nb + l, j - l + 1);
+    }
+    __syncthreads();
+    unsigned long long c4 = PNOW();
+    PWACC(b, wid, 4, c4 - c3);
+    if (!have) break;
+    if (!issued) {
+      if (!wait_all(pq, vq, nq, err, &s_flag)) { give_up(); return; }
+      issue(Q, G);
+    }
+    PWACC(b, wid, 1, PNOW() - c4);
+    P = Q;
+  }
+}
+
 // ------------------------------------------------------------------ Cholesky backward
 // Reverse mode of Lm = chol(Kuu) (GPflow base_conditional's cholesky,
 // models.py:141), as in PyTorch / Murray (2016):
@@ -997,11 +1504,44 @@ static int64_t chol_ws_doubles_per_batch(int64_t M) {
 extern "C" int mgp_dbg_chol_stamps(unsigned long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
 }
+extern "C" int mgp_dbg_persist_stamps(unsigned long long* chain, unsigned long long* work, int reset) {
+  if (reset) {
+    static unsigned long long zeros[2 * 128 * 8] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_pchain), zeros, sizeof(zeros));
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pwork), zeros, sizeof(zeros));
+  }
+  hipMemcpyFromSymbol(chain, HIP_SYMBOL(g_pchain), sizeof(g_pchain));
+  return (int)hipMemcpyFromSymbol(work, HIP_SYMBOL(g_pwork), sizeof(g_pwork));
+}
 #endif
 
+static int64_t chol_task_ints(int nb) { return ((int64_t)task_count(nb) + 63) / 64 * 64; }
+
+// doubles of every batch entry, then the persistent path's sync words (per batch)
+// and its task table (shared)
 extern "C" size_t mgp_chol_workspace_bytes(int64_t M, int32_t batch) {
   if (M <= 0 || batch <= 0) return 0;
-  return (size_t)chol_ws_doubles_per_batch(M) * (size_t)batch * sizeof(double);
+  const int nb = (int)(chol_mp(M) / CB);
+  return (size_t)chol_ws_doubles_per_batch(M) * (size_t)batch * sizeof(double) +
+         (size_t)(chol_sync_words(nb) * batch + chol_task_ints(nb)) * sizeof(int);
+}
+
+// Persistent launch (chol_persist) with MGP_CHOL_PERSIST=1 (measured at c3: 0.27-0.28 ms
+// standalone at 48-64 workers per layer against 0.28 ms for the per-step launches, 445 vs
+// 434 us in the ELBO step -- the chain -> worker -> chain hand-offs of every step cost what
+// the launch boundaries did); sizes it supports: task codes hold 8-bit tile
+// indices, the per-batch buffer resource 31-bit offsets.
+static bool chol_persist_ok(int nb, int64_t strideWS) {
+  const char* e = getenv("MGP_CHOL_PERSIST");   // read per call (tuning runs switch it in-process)
+  const int env = e ? atoi(e) : 0;
+  return env != 0 && nb >= 3 && nb <= 128 && strideWS * 8 < ((int64_t)1 << 31);
+}
+// Worker workgroups per batch entry (MGP_CHOL_WORKERS overrides)
+static int chol_persist_workers(int nb) {
+  const char* e = getenv("MGP_CHOL_WORKERS");
+  const int env = e ? atoi(e) : 0;
+  if (env > 0) return env;
+  return std::min(48, std::max(2, 2 * nb));
 }
 
 static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s,
@@ -1015,6 +1555,13 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
   a.nb = (int)(a.Mp / CB);
   a.strideWS = chol_ws_doubles_per_batch(a.M);
   a.ws = (double*)workspace;
+  const bool persist = chol_persist_ok(a.nb, a.strideWS);
+  if (persist) {
+    a.strideSync = chol_sync_words(a.nb);
+    a.sync = (int*)((char*)workspace + (size_t)a.strideWS * batch * sizeof(double));
+    a.tasks = a.sync + a.strideSync * batch;
+    a.ntask = task_count(a.nb);
+  }
   const dim3 block(kCholThreads);
   hipLaunchKernelGGL(chol_prep, dim3(a.nb * a.nb + 1, batch), block, 0, s, a);
   int st = launch_status();
@@ -1022,6 +1569,10 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
   if (prep_done) {
     st = hip_status(hipEventRecord(prep_done, s));
     if (st) return st;
+  }
+  if (persist) {
+    hipLaunchKernelGGL(chol_persist, dim3(1 + chol_persist_workers(a.nb), batch), block, 0, s, a);
+    return launch_status();
   }
   for (int j = 0; j < a.nb; ++j) {
     const int T = a.nb - j - 1;

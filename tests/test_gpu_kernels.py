@@ -38,8 +38,16 @@ def test_rbf_kuf_kuu(device, N, M, D, ard):
     assert np.array_equal(Kuu, Kuu.T)
 
 
+@pytest.fixture(params=["steps", "persist"])
+def chol_path(request, monkeypatch):
+    """K3's two launch structures: one launch per panel step (default) and the single
+    persistent launch (chol_persist, MGP_CHOL_PERSIST=1; the library reads it per call)."""
+    monkeypatch.setenv("MGP_CHOL_PERSIST", "1" if request.param == "persist" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("M,batch", [(1, 1), (25, 2), (64, 1), (100, 2), (256, 2), (1024, 2)])
-def test_potrf_trtri(device, M, batch):
+def test_potrf_trtri(device, M, batch, chol_path):
     from modulatedgps_amd import ops
     rng = np.random.default_rng(M)
     As = []
@@ -63,7 +71,7 @@ def test_potrf_trtri(device, M, batch):
         assert normwise(Lt.T, Li) < tol
 
 
-def test_potrf_reports_non_spd(device):
+def test_potrf_reports_non_spd(device, chol_path):
     from modulatedgps_amd import ops
     M = 130
     A = np.eye(M)
@@ -117,7 +125,7 @@ def test_kuu_factorisation_matches_float64(device):
 
 
 @pytest.mark.parametrize("M", [300, 1024])
-def test_kuu_linvt_bound_and_bounded_split(device, M):
+def test_kuu_linvt_bound_and_bounded_split(device, M, chol_path):
     """mgp_kuu_potrf_trtri_ex: K3 writes max |LinvT| into the L^-T images' trailers
     (bit-exact vs the reduction of the written LinvT), and the bounded split then
     gives the same split-f16 image as mgp_split_upper_f16's own reduction."""
@@ -143,7 +151,7 @@ def test_kuu_linvt_bound_and_bounded_split(device, M):
 
 
 @pytest.mark.parametrize("M,dup", [(1024, 0.0), (1024, 1e-3), (700, 1e-2)])
-def test_kuu_factorisation_ill_conditioned(device, M, dup):
+def test_kuu_factorisation_ill_conditioned(device, M, dup, chol_path):
     """K3 on badly conditioned Kuu (inducing points with near-duplicates, cond up
     to ~1e9): L and L^-1 against float64 LAPACK, to float32 output rounding
     amplified by at most cond(L) eps64."""
