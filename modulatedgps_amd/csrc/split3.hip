@@ -38,6 +38,8 @@
 // straight from global into registers one k-step ahead; 48 MFMAs per wave.
 // The triangle is exploited at row-tile granularity (k-steps start at 128 t);
 // the zero blocks inside the diagonal tile come from Lfr's zero fill.
+#include <stdlib.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -443,6 +445,140 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
     if constexpr (F16) s *= unscale;
     const int64_t n = nbase + 32 * c;
     if (lane < 32 && n < N) dst[n] = s;
+  }
+}
+
+// ------------------------------------------------------------------ K5 (split-f16) on 16x16x32 MFMAs
+// The same contraction, items and split-f16 images as expert_cond_x6_kernel<2, true>,
+// on v_mfma_f32_16x16x32_f16 (16 cycles per 16x16x32 block: the same cycles per flop
+// as 32x32x16; the chip can hold a different clock per shape under load,
+// MI355X_MICROARCH.md, DVFS give-back item 7).  No new image format: one k-step PAIR
+// (32 deep) of the existing fragments is one MFMA k-step; lane l (i = l % 16,
+// q = l / 16) takes the 16 bytes of fragment k-step 2 ks + q / 2 at lane position
+// 16 (row block % 2) + i + 32 (q % 2) -- its 8 elements are 8 of the 32 m of the pair,
+// the same 8 for the A operand (L_k^T, rows m') and the B operand (A, columns n), so
+// the contraction is unchanged.  Wave w: 128 rows x 64 columns = 8 x 4 blocks of
+// 16 x 16; per pair the L fragments of the item's 4 row sub-tiles (16 KiB) are staged
+// in LDS (double buffered, one barrier per pair), the wave's B fragments go global ->
+// registers one pair ahead; 96 MFMAs per wave and pair.
+typedef float floatx4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ floatx4v mfma16_f16(bf16x8 a, bf16x8 b, floatx4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c,
+                                                0, 0, 0);
+}
+
+__global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __restrict__ Afr,
+                                                               const bf16x8* __restrict__ Lfr, uint32_t afr_bytes,
+                                                               uint32_t lfr_bytes, int nmk, int nmb, int nTn, int K,
+                                                               int64_t N, float* __restrict__ part, int64_t ldp,
+                                                               const float* __restrict__ a_bound,
+                                                               const float* __restrict__ l_bound) {
+  __shared__ bf16x8 sL[2][4 * 2 * 2 * 64];  // 2 x 16 KiB: [row sub-tile][k-step of pair][plane][lane position]
+  int t, tn, k;
+  x6_item<false>(blockIdx.x, nTn, K, t, tn, k);
+  const int nTp = nmb / 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rT = img_rsrc(Lfr, lfr_bytes), rB = img_rsrc(Afr, afr_bytes);
+  const uint32_t tbase = (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes;
+  // L staging: unit e = tid + 256 s -> sub-tile i = e / 256, k-step kk = (e / 128) % 2,
+  // plane p = (e / 64) % 2, position e % 64
+  uint32_t vT[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int e = tid + 256 * s, i = e >> 8, kk = (e >> 7) & 1, p = (e >> 6) & 1;
+    vT[s] = (uint32_t)((((i * nmk + kk) * 3 + p) * 64 + (e & 63)) * 16);
+  }
+  // B (A image): column block cb of this wave, plane p, pair ks: fragment nb = 8 tn + 2 w + cb / 2,
+  // k-step 2 ks + q / 2, position 16 (cb % 2) + li + 32 (q % 2)
+  const uint32_t sB0 = (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes;
+  const uint32_t vB = (uint32_t)((((q >> 1) * 3) * 64 + li + 32 * (q & 1)) * 16);
+  auto boff = [&](int cb, int p, int ks) {
+    return sB0 + (uint32_t)(cb >> 1) * (uint32_t)nmk * 3u * kFragBytes + (uint32_t)((2 * ks) * 3 + p) * kFragBytes +
+           (uint32_t)(16 * (cb & 1)) * 16u;
+  };
+  floatx4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[i][c] = floatx4v{0.f, 0.f, 0.f, 0.f};
+  auto load_b = [&](bf16x8 (&b)[4][2], int ks) {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) b[cb][p] = ld_frag(rB, vB, boff(cb, p, ks));
+  };
+  auto load_t = [&](u32x4v (&st)[4], int ks) {
+    const uint32_t o = tbase + (uint32_t)(2 * ks) * 3u * kFragBytes;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s], o, 0);
+  };
+  auto store_t = [&](int buf, const u32x4v (&st)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
+  };
+  // A operand of row block ib, plane p: sub-tile ib / 2, k-step q / 2, position 16 (ib % 2) + li + 32 (q % 2)
+  const int aoff = (q >> 1) * 128 + li + 32 * (q & 1);
+  auto compute = [&](int buf, const bf16x8 (&b)[4][2], auto ihi) {
+    constexpr int IHI = decltype(ihi)::value;
+#pragma unroll
+    for (int ib = 0; ib < IHI; ++ib) {
+      const int base = (ib >> 1) * 256 + 16 * (ib & 1) + aoff;
+      const bf16x8 a0 = sL[buf][base], a1 = sL[buf][base + 64];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        acc[ib][cb] = mfma16_f16(a1, b[cb][0], acc[ib][cb]);
+        acc[ib][cb] = mfma16_f16(a0, b[cb][1], acc[ib][cb]);
+        acc[ib][cb] = mfma16_f16(a0, b[cb][0], acc[ib][cb]);
+      }
+    }
+  };
+  const int ks0 = 4 * t, nks = nmk / 2;
+  bf16x8 b0[4][2], b1[4][2];
+  u32x4v st[4];
+  load_t(st, ks0);
+  load_b(b0, ks0);
+  store_t(0, st);
+  __syncthreads();
+  // two pairs per iteration (buffers and register sets alternate); the first four pairs
+  // meet the diagonal: pair p has row blocks ib <= 2 p + 1
+  auto two = [&](int ks, auto ihi0, auto ihi1) {
+    load_t(st, ks + 1);
+    load_b(b1, ks + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0, b0, ihi0);
+    __builtin_amdgcn_sched_barrier(0);
+    store_t(1, st);
+    __syncthreads();
+    const int k2 = ks + 2 < nks ? ks + 2 : nks - 1;
+    load_t(st, k2);
+    load_b(b0, k2);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1, b1, ihi1);
+    __builtin_amdgcn_sched_barrier(0);
+    store_t(0, st);
+    __syncthreads();
+  };
+  two(ks0, ic<2>{}, ic<4>{});
+  two(ks0 + 2, ic<6>{}, ic<8>{});
+#pragma nounroll
+  for (int ks = ks0 + 4; ks < nks; ks += 2) two(ks, ic<8>{}, ic<8>{});
+
+  // sum over the 128 rows of C^2 per column: 8 blocks x 4 registers, then the 4 lane groups
+  const float unscale = ldexpf(1.f, -2 * (img_exp(*a_bound) + img_exp(*l_bound)));
+  float* dst = part + ((int64_t)k * nTp + t) * ldp;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    float s = 0.f;
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s = fmaf(acc[ib][cb][r], acc[ib][cb][r], s);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const int64_t n = (int64_t)tn * kX6BN + 64 * w + 16 * cb + li;
+    if (lane < 16 && n < N) dst[n] = s * unscale;
   }
 }
 
@@ -1392,6 +1528,14 @@ extern "C" size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K)
 }
 
 // Argument checks report the index in mgp_expert_conditional_x6's signature.
+// K5 (split-f16, forward) on 16x16x32 MFMAs (expert_cond16_kernel) unless
+// MGP_K5_SHAPE=32 (read per call).  c3, one launch: 1.196 vs 1.322 ms for the 32x32x16
+// kernel, same operands and MFMA cycles (tools/k5_probe.py, profiles/r03_k5_shape.json).
+static bool k5_shape16() {
+  const char* e = getenv("MGP_K5_SHAPE");
+  return !(e && atoi(e) == 32);
+}
+
 static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
                               const float* stats, int64_t lds, const float* variance, int64_t M, int64_t N,
                               int32_t K, int planes, float* fmean, float* fvar, int64_t ldf, void* workspace,
@@ -1439,6 +1583,10 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
     hipLaunchKernelGGL((expert_cond_x6_kernel<2, true, false, true>), grid, dim3(256), 0, s, (const bf16x8*)Afr,
                        (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk,
                        nmb, nTn, K, N, part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
+  } else if (planes == 2 && f16 && !x8 && k5_shape16()) {  // the default split-f16 forward K5
+    hipLaunchKernelGGL(expert_cond16_kernel, grid, dim3(256), 0, s, (const bf16x8*)Afr, (const bf16x8*)Lfr,
+                       (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N,
+                       part, ldp, a_bound, l_bound);
   } else {
   MGP_K5_CASE(3, false, false)
   MGP_K5_CASE(2, false, false)
