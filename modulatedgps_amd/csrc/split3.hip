@@ -166,6 +166,14 @@ __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t vof
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+// The 16x16x32-MFMA K5 (expert_cond16_kernel, forward and training) unless
+// MGP_K5_SHAPE=32 (read per call).  c3, one launch: 1.196 vs 1.322 ms for the 32x32x16
+// kernel, same operands and MFMA cycles (tools/k5_probe.py, profiles/r03_k5_shape.json).
+static bool k5_shape16() {
+  const char* e = getenv("MGP_K5_SHAPE");
+  return !(e && atoi(e) == 32);
+}
+
 // Item b -> (row tile t heavy-first, column tile tn, expert k); the K experts of
 // a column tile are 8 block ids apart (one XCD) when nTn % 8 == 0.
 // TN_OUTER (K5 writing the C_k images, training): per XCD, one column tile at a
@@ -466,105 +474,189 @@ __device__ __forceinline__ floatx4v mfma16_f16(bf16x8 a, bf16x8 b, floatx4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c,
                                                 0, 0, 0);
 }
+__device__ __forceinline__ floatx4v mfma16_bf16(bf16x8 a, bf16x8 b, floatx4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// one 16x16 block: the plane products of mfma_fmt (x6: six bf16, split-f16: three f16)
+template <int NPL, bool F16>
+__device__ __forceinline__ floatx4v mfma16_fmt(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4v acc) {
+  if constexpr (F16) {
+    acc = mfma16_f16(a[1], b[0], acc);
+    acc = mfma16_f16(a[0], b[1], acc);
+    return mfma16_f16(a[0], b[0], acc);
+  } else if constexpr (NPL == 3) {
+    acc = mfma16_bf16(a[2], b[0], acc);
+    acc = mfma16_bf16(a[1], b[1], acc);
+    acc = mfma16_bf16(a[0], b[2], acc);
+    acc = mfma16_bf16(a[1], b[0], acc);
+    acc = mfma16_bf16(a[0], b[1], acc);
+    return mfma16_bf16(a[0], b[0], acc);
+  } else if constexpr (NPL == 2) {
+    acc = mfma16_bf16(a[1], b[0], acc);
+    acc = mfma16_bf16(a[0], b[1], acc);
+    return mfma16_bf16(a[0], b[0], acc);
+  } else {
+    return mfma16_bf16(a[0], b[0], acc);
+  }
+}
 
-__global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __restrict__ Afr,
-                                                               const bf16x8* __restrict__ Lfr, uint32_t afr_bytes,
-                                                               uint32_t lfr_bytes, int nmk, int nmb, int nTn, int K,
-                                                               int64_t N, float* __restrict__ part, int64_t ldp,
-                                                               const float* __restrict__ a_bound,
-                                                               const float* __restrict__ l_bound) {
-  __shared__ bf16x8 sL[2][4 * 2 * 2 * 64];  // 2 x 16 KiB: [row sub-tile][k-step of pair][plane][lane position]
-  int t, tn, k;
-  x6_item<false>(blockIdx.x, nTn, K, t, tn, k);
-  const int nTp = nmb / 4;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 15, q = lane >> 4;
-  const __amdgpu_buffer_rsrc_t rT = img_rsrc(Lfr, lfr_bytes), rB = img_rsrc(Afr, afr_bytes);
-  const uint32_t tbase = (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes;
-  // L staging: unit e = tid + 256 s -> sub-tile i = e / 256, k-step kk = (e / 128) % 2,
-  // plane p = (e / 64) % 2, position e % 64
-  uint32_t vT[4];
+// Main loop of the 16x16x32 kernels: acc[ib][cb] (16-row block ib = 0..7 of the 128-row
+// item, 16-column block cb = 0..3 of this wave's 64 columns) += sum over k-step PAIRS
+// ks in [ks_begin, ks_end) (even count) of T-image rows x B-image columns.  T fragments
+// of the item's 4 row sub-tiles, both k-steps of a pair and NPL planes are staged in LDS
+// (double buffered, one barrier per pair); B fragments go global -> registers one pair
+// ahead.  DIAG = 1: T lower (K5): the first 4 pairs meet the diagonal, pair p has row
+// blocks ib <= 2 p + 1; DIAG = 2: T upper (K4): the last 4 pairs do, pair p of them has
+// ib >= 2 p; 0: full.  (The zero sub-blocks inside come from the images' zero fill.)
+//   tbase: byte offset of T fragment (mb = 4 t, mk = 0); sB0: of B fragment (nb0, mk = 0)
+template <int DIAG, int NPL, bool F16>
+__device__ __forceinline__ void x6_mainloop16(floatx4v (&acc)[8][4], bf16x8 (*sL)[4 * 2 * 3 * 64],
+                                              __amdgpu_buffer_rsrc_t rT, uint32_t tbase, __amdgpu_buffer_rsrc_t rB,
+                                              uint32_t sB0, int ks_begin, int ks_end, int nmk) {
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, q = lane >> 4;
+  // T staging: unit e = tid + 256 s (NPL 2: 4 units, 3: 6 units per thread): sub-tile
+  // i = e / (128 NPL), k-step kk = (e / (64 NPL)) % 2, plane p = (e / 64) % NPL, position e % 64
+  constexpr int NU = 2 * NPL;
+  uint32_t vT[NU];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int e = tid + 256 * s, i = e >> 8, kk = (e >> 7) & 1, p = (e >> 6) & 1;
+  for (int s = 0; s < NU; ++s) {
+    const int e = tid + 256 * s, i = e / (128 * NPL), kk = (e / (64 * NPL)) % 2, p = (e / 64) % NPL;
     vT[s] = (uint32_t)((((i * nmk + kk) * 3 + p) * 64 + (e & 63)) * 16);
   }
-  // B (A image): column block cb of this wave, plane p, pair ks: fragment nb = 8 tn + 2 w + cb / 2,
-  // k-step 2 ks + q / 2, position 16 (cb % 2) + li + 32 (q % 2)
-  const uint32_t sB0 = (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes;
+  // B: column block cb, plane p, pair ks: fragment nb0 + cb / 2, k-step 2 ks + q / 2,
+  // position 16 (cb % 2) + li + 32 (q % 2)
   const uint32_t vB = (uint32_t)((((q >> 1) * 3) * 64 + li + 32 * (q & 1)) * 16);
   auto boff = [&](int cb, int p, int ks) {
     return sB0 + (uint32_t)(cb >> 1) * (uint32_t)nmk * 3u * kFragBytes + (uint32_t)((2 * ks) * 3 + p) * kFragBytes +
            (uint32_t)(16 * (cb & 1)) * 16u;
   };
-  floatx4v acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[i][c] = floatx4v{0.f, 0.f, 0.f, 0.f};
-  auto load_b = [&](bf16x8 (&b)[4][2], int ks) {
+  auto load_b = [&](bf16x8 (&b)[4][3], int ks) {
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-      for (int p = 0; p < 2; ++p) b[cb][p] = ld_frag(rB, vB, boff(cb, p, ks));
+      for (int p = 0; p < NPL; ++p) b[cb][p] = ld_frag(rB, vB, boff(cb, p, ks));
   };
-  auto load_t = [&](u32x4v (&st)[4], int ks) {
+  auto load_t = [&](u32x4v (&st)[NU], int ks) {
     const uint32_t o = tbase + (uint32_t)(2 * ks) * 3u * kFragBytes;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s], o, 0);
+    for (int s = 0; s < NU; ++s) st[s] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT[s], o, 0);
   };
-  auto store_t = [&](int buf, const u32x4v (&st)[4]) {
+  auto store_t = [&](int buf, const u32x4v (&st)[NU]) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
+    for (int s = 0; s < NU; ++s) reinterpret_cast<u32x4v*>(sL[buf])[tid + 256 * s] = st[s];
   };
   // A operand of row block ib, plane p: sub-tile ib / 2, k-step q / 2, position 16 (ib % 2) + li + 32 (q % 2)
-  const int aoff = (q >> 1) * 128 + li + 32 * (q & 1);
-  auto compute = [&](int buf, const bf16x8 (&b)[4][2], auto ihi) {
-    constexpr int IHI = decltype(ihi)::value;
+  const int aoff = (q >> 1) * 64 * NPL + li + 32 * (q & 1);
+  auto compute = [&](int buf, const bf16x8 (&b)[4][3], auto ilo, auto ihi) {
+    constexpr int ILO = decltype(ilo)::value, IHI = decltype(ihi)::value;
 #pragma unroll
-    for (int ib = 0; ib < IHI; ++ib) {
-      const int base = (ib >> 1) * 256 + 16 * (ib & 1) + aoff;
-      const bf16x8 a0 = sL[buf][base], a1 = sL[buf][base + 64];
+    for (int ib = ILO; ib < IHI; ++ib) {
+      const int base = (ib >> 1) * 128 * NPL + 16 * (ib & 1) + aoff;
+      bf16x8 a[3];
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        acc[ib][cb] = mfma16_f16(a1, b[cb][0], acc[ib][cb]);
-        acc[ib][cb] = mfma16_f16(a0, b[cb][1], acc[ib][cb]);
-        acc[ib][cb] = mfma16_f16(a0, b[cb][0], acc[ib][cb]);
-      }
+      for (int p = 0; p < NPL; ++p) a[p] = sL[buf][base + 64 * p];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[ib][cb] = mfma16_fmt<NPL, F16>(a, b[cb], acc[ib][cb]);
     }
   };
-  const int ks0 = 4 * t, nks = nmk / 2;
-  bf16x8 b0[4][2], b1[4][2];
-  u32x4v st[4];
-  load_t(st, ks0);
-  load_b(b0, ks0);
+  bf16x8 b0[4][3], b1[4][3];
+  u32x4v st[NU];
+  load_t(st, ks_begin);
+  load_b(b0, ks_begin);
   store_t(0, st);
   __syncthreads();
-  // two pairs per iteration (buffers and register sets alternate); the first four pairs
-  // meet the diagonal: pair p has row blocks ib <= 2 p + 1
-  auto two = [&](int ks, auto ihi0, auto ihi1) {
+  auto two = [&](int ks, auto ilo0, auto ihi0, auto ilo1, auto ihi1) {
     load_t(st, ks + 1);
     load_b(b1, ks + 1);
     __builtin_amdgcn_sched_barrier(0);
-    compute(0, b0, ihi0);
+    compute(0, b0, ilo0, ihi0);
     __builtin_amdgcn_sched_barrier(0);
     store_t(1, st);
     __syncthreads();
-    const int k2 = ks + 2 < nks ? ks + 2 : nks - 1;
+    const int k2 = ks + 2 < ks_end ? ks + 2 : ks_end - 1;  // after the last pair: harmless reload
     load_t(st, k2);
     load_b(b0, k2);
     __builtin_amdgcn_sched_barrier(0);
-    compute(1, b1, ihi1);
+    compute(1, b1, ilo1, ihi1);
     __builtin_amdgcn_sched_barrier(0);
     store_t(0, st);
     __syncthreads();
   };
-  two(ks0, ic<2>{}, ic<4>{});
-  two(ks0 + 2, ic<6>{}, ic<8>{});
+  if constexpr (DIAG == 1) {
+    two(ks_begin, ic<0>{}, ic<2>{}, ic<0>{}, ic<4>{});
+    two(ks_begin + 2, ic<0>{}, ic<6>{}, ic<0>{}, ic<8>{});
 #pragma nounroll
-  for (int ks = ks0 + 4; ks < nks; ks += 2) two(ks, ic<8>{}, ic<8>{});
+    for (int ks = ks_begin + 4; ks < ks_end; ks += 2) two(ks, ic<0>{}, ic<8>{}, ic<0>{}, ic<8>{});
+  } else if constexpr (DIAG == 0) {
+#pragma nounroll
+    for (int ks = ks_begin; ks < ks_end; ks += 2) two(ks, ic<0>{}, ic<8>{}, ic<0>{}, ic<8>{});
+  } else {
+#pragma nounroll
+    for (int ks = ks_begin; ks < ks_end - 4; ks += 2) two(ks, ic<0>{}, ic<8>{}, ic<0>{}, ic<8>{});
+    two(ks_end - 4, ic<0>{}, ic<8>{}, ic<2>{}, ic<8>{});
+    two(ks_end - 2, ic<4>{}, ic<8>{}, ic<6>{}, ic<8>{});
+  }
+}
 
+// ------------------------------------------------------------------ K5 (split-f16) on 16x16x32 MFMAs
+// The same contraction, items and split-f16 images as expert_cond_x6_kernel<2, true>,
+// on v_mfma_f32_16x16x32_f16 (16 cycles per 16x16x32 block: the same cycles per flop
+// as 32x32x16; the chip can hold a different clock per shape under load,
+// MI355X_MICROARCH.md, DVFS give-back item 7).  No new image format: one k-step PAIR
+// (32 deep) of the existing fragments is one MFMA k-step; lane l (i = l % 16,
+// q = l / 16) takes the 16 bytes of fragment k-step 2 ks + q / 2 at lane position
+// 16 (row block % 2) + i + 32 (q % 2) -- its 8 elements are 8 of the 32 m of the pair,
+// the same 8 for the A operand (L_k^T, rows m') and the B operand (A, columns n), so
+// the contraction is unchanged (x6_mainloop16).  Wave w: 128 rows x 64 columns =
+// 8 x 4 blocks of 16 x 16; 96 MFMAs per wave and pair.
+// COUT (training): C_k = L_k^T A is also written as a split-f16 B-layout image per expert,
+// as expert_cond_x6_kernel<2, true, false, true> does; a fragment's lane position takes
+// 8 rows from two lanes of the 16x16 accumulator layout (one exchange across the lane halves).
+template <bool COUT = false>
+__global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __restrict__ Afr,
+                                                               const bf16x8* __restrict__ Lfr, uint32_t afr_bytes,
+                                                               uint32_t lfr_bytes, int nmk, int nmb, int nTn, int K,
+                                                               int64_t N, float* __restrict__ part, int64_t ldp,
+                                                               const float* __restrict__ a_bound,
+                                                               const float* __restrict__ l_bound,
+                                                               bf16x8* __restrict__ Cfr = nullptr, int64_t cexp = 0,
+                                                               const float* __restrict__ colmax = nullptr) {
+  __shared__ bf16x8 sL[2][4 * 2 * 3 * 64];  // [row sub-tile][k-step of pair][plane][lane position] (2 planes used)
+  int t, tn, k;
+  x6_item<COUT>(blockIdx.x, nTn, K, t, tn, k);
+  const int nTp = nmb / 4;
+  const int lane = threadIdx.x & 63, li = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  floatx4v acc[8][4];
+  x6_mainloop16<1, 2, true>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
+                            img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 4 * t,
+                            nmk / 2, nmk);
+  if constexpr (COUT) {
+    const float cmul = ldexpf(1.f, img_exp(*colmax * *a_bound * 1.0009765625f) -
+                                       (img_exp(*a_bound) + img_exp(*l_bound)));
+    bf16x8* Ck = Cfr + (int64_t)k * cexp;
+    const bool lo_half = lane < 32;
+    const int pos = lo_half ? li + 32 * q : 16 + li + 32 * (q - 2);
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const floatx4v send = lo_half ? acc[ib][2 * c + 1] : acc[ib][2 * c];
+        float y[4], v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(send[r], 32, 64);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = (lo_half ? acc[ib][2 * c][r] : y[r]) * cmul;
+          v[4 + r] = (lo_half ? y[r] : acc[ib][2 * c + 1][r]) * cmul;
+        }
+        store_split_f16(Ck + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, 1.f);
+      }
+  }
   // sum over the 128 rows of C^2 per column: 8 blocks x 4 registers, then the 4 lane groups
   const float unscale = ldexpf(1.f, -2 * (img_exp(*a_bound) + img_exp(*l_bound)));
   float* dst = part + ((int64_t)k * nTp + t) * ldp;
@@ -1528,14 +1620,6 @@ extern "C" size_t mgp_expert_x6_workspace_bytes(int64_t M, int64_t N, int32_t K)
 }
 
 // Argument checks report the index in mgp_expert_conditional_x6's signature.
-// K5 (split-f16, forward) on 16x16x32 MFMAs (expert_cond16_kernel) unless
-// MGP_K5_SHAPE=32 (read per call).  c3, one launch: 1.196 vs 1.322 ms for the 32x32x16
-// kernel, same operands and MFMA cycles (tools/k5_probe.py, profiles/r03_k5_shape.json).
-static bool k5_shape16() {
-  const char* e = getenv("MGP_K5_SHAPE");
-  return !(e && atoi(e) == 32);
-}
-
 static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr, size_t lfr_bytes,
                               const float* stats, int64_t lds, const float* variance, int64_t M, int64_t N,
                               int32_t K, int planes, float* fmean, float* fvar, int64_t ldf, void* workspace,
@@ -1580,11 +1664,16 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
     const size_t cexp = cols_planes(M, N);
     if (cfr_bytes < (size_t)K * cexp) return -17;
     if (!aligned16(Cfr)) return MGP_ERR_ALIGN;
-    hipLaunchKernelGGL((expert_cond_x6_kernel<2, true, false, true>), grid, dim3(256), 0, s, (const bf16x8*)Afr,
-                       (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk,
-                       nmb, nTn, K, N, part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
+    if (k5_shape16())
+      hipLaunchKernelGGL((expert_cond16_kernel<true>), grid, dim3(256), 0, s, (const bf16x8*)Afr, (const bf16x8*)Lfr,
+                         (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N,
+                         part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
+    else
+      hipLaunchKernelGGL((expert_cond_x6_kernel<2, true, false, true>), grid, dim3(256), 0, s, (const bf16x8*)Afr,
+                         (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K),
+                         nmk, nmb, nTn, K, N, part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
   } else if (planes == 2 && f16 && !x8 && k5_shape16()) {  // the default split-f16 forward K5
-    hipLaunchKernelGGL(expert_cond16_kernel, grid, dim3(256), 0, s, (const bf16x8*)Afr, (const bf16x8*)Lfr,
+    hipLaunchKernelGGL((expert_cond16_kernel<false>), grid, dim3(256), 0, s, (const bf16x8*)Afr, (const bf16x8*)Lfr,
                        (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N,
                        part, ldp, a_bound, l_bound);
   } else {
