@@ -44,8 +44,12 @@ def kernel_key(name):
         return "gram_f16_kernel"
     if base == "grad_a_s_kernel" and flags[:1] == ["true"]:
         return "grad_a_s_f16_kernel"
-    if base == "expert_cond_x6_kernel" and flags[1:] == ["true", "true"]:
+    if base == "expert_cond_x6_kernel" and flags[1:3] == ["true", "true"]:
         return "expert_cond_f16x8_kernel"       # split-f16 hi products + e4m3 cross terms
+    if base == "expert_cond_x6_kernel" and flags[1:4] == ["true", "false", "true"]:
+        return "expert_cond_f16c_kernel"        # split-f16, also writing the C_k images (training)
+    if base == "expert_cond16_kernel" and flags[:1] == ["true"]:
+        return "expert_cond16c_kernel"          # 16x16x32, also writing the C_k images (training)
     if base in ("expert_cond_x6_kernel", "rbf_kuf_x6_kernel") and "true" in flags:
         return base.replace("_x6_", "_f16_")
     return base
