@@ -154,7 +154,22 @@ __device__ __forceinline__ void load_latents(const float* __restrict__ mu_f, con
 // the same W, with its own logsumexp over S: lse_S(sum_k W ve_a) + lse_S(sum_k W ve_f) - 2 log S.
 // MC: the pred likelihood is MultiClass/RobustMax (mc_a = log(1 - eps),
 // mc_b = log(eps / (K - 1)); lik_var unused): ve_k = the point's RobustMax var-exp.
-template <int KMAX, bool MOD, bool MC>
+// LANES consecutive lanes share a point: lane `sub` takes the samples s = sub (mod
+// LANES) and the lanes' running (max, sum) pairs are merged by shuffles (a point per
+// thread left 65536 threads -- one wave per SIMD -- for the latency-bound Philox /
+// transcendental chain at c3).
+template <int LANES>
+__device__ __forceinline__ void lse_merge(float& run_max, float& run_sum) {
+#pragma unroll
+  for (int off = 1; off < LANES; off <<= 1) {
+    const float om = __shfl_xor(run_max, off, 64), os = __shfl_xor(run_sum, off, 64);
+    const float m = fmaxf(run_max, om);
+    if (m != -INFINITY) run_sum = run_sum * __expf(run_max - m) + os * __expf(om - m);
+    run_max = m;
+  }
+}
+
+template <int KMAX, bool MOD, bool MC, int LANES>
 __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
@@ -163,8 +178,11 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
     const float* __restrict__ noise_z, const float* __restrict__ noise_u, uint32_t key0,
     uint32_t key1, int64_t n_offset, double* __restrict__ partials, float mc_a, float mc_b) {
   __shared__ double scratch[16];
-  const int64_t n = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
+  const int64_t gt = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
+  const int64_t n = gt / LANES;
+  const int sub = (int)(gt % LANES);
   float val = 0.f;
+  float run_max = -INFINITY, run_sum = 0.f, run_max_a = -INFINITY, run_sum_a = 0.f;
   if (n < N) {
     const float kHalfLog2Pi = 0.91893853320467274f;
     float ve[KMAX], ma[KMAX], sa[KMAX], vea[MOD ? KMAX : 1];
@@ -203,8 +221,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
       }
     }
     const uint32_t ng = (uint32_t)(n + n_offset);
-    float run_max = -INFINITY, run_sum = 0.f, run_max_a = -INFINITY, run_sum_a = 0.f;
-    for (int s = 0; s < S; ++s) {
+    for (int s = sub; s < S; s += LANES) {
       float z[KMAX], u[KMAX];
       draw_noise<KMAX>(z, u, noise_z, noise_u, N, K, n, s, ng, key0, key1);
       float x[KMAX], xm = -INFINITY;
@@ -243,6 +260,12 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
         }
       }
     }
+  }
+  if constexpr (LANES > 1) {  // every lane of the wave takes part (points beyond N included)
+    lse_merge<LANES>(run_max, run_sum);
+    if constexpr (MOD) lse_merge<LANES>(run_max_a, run_sum_a);
+  }
+  if (n < N && sub == 0) {
     val = run_max + logf(run_sum) - logf((float)S);
     if constexpr (MOD) val += run_max_a + logf(run_sum_a) - logf((float)S);
   }
@@ -265,7 +288,17 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_kernel(
 // multiplied by `scale` (1 / N_total for the ELBO's batch mean).
 // MC: dDT/dve_mc = sum_k om_k, chained through robustmax_p's gradient; no
 // likelihood-variance gradient (MultiClass has no trainable parameter).
-template <int KMAX, bool MOD, bool MC>
+// LANES lanes per point as the forward: the lanes split the samples of both passes,
+// merge the log-sum-exp pairs after pass 1 and sum the per-sample accumulators after
+// pass 2 (butterfly shuffles, so every lane ends with the totals); lane 0 writes.
+template <int LANES>
+__device__ __forceinline__ float lanes_sum(float v) {
+#pragma unroll
+  for (int off = 1; off < LANES; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int KMAX, bool MOD, bool MC, int LANES>
 __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     const float* __restrict__ mu_f, const float* __restrict__ var_f, const float* __restrict__ mu_a,
     const float* __restrict__ var_a, int64_t ldf, const float* __restrict__ Y,
@@ -274,7 +307,9 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     uint32_t key0, uint32_t key1, int64_t n_offset, float scale, float* __restrict__ G, int64_t ldg,
     double* __restrict__ partials, float mc_a, float mc_b) {
   __shared__ double scratch[16];
-  const int64_t n = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
+  const int64_t gt = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
+  const int64_t n = gt / LANES;
+  const int sub = (int)(gt % LANES);
   float glv[KMAX], glva[MOD ? KMAX : 1];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) glv[k] = 0.f;
@@ -282,7 +317,10 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) glva[k] = 0.f;
   }
-  if (n < N) {
+  // (LANES > 1: a point beyond N is computed for the last valid one, so that all lanes
+  // of the wave take part in the shuffles, and not written)
+  if (LANES > 1 || n < N) {
+    const int64_t n = (gt / LANES < N) ? gt / LANES : N - 1;
     const float kHalfLog2Pi = 0.91893853320467274f;
     const float y = Y[n];
     float ve[KMAX], ma[KMAX], sa[KMAX], vea[MOD ? KMAX : 1];
@@ -351,13 +389,17 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     };
     // pass 1: log-sum-exp over the samples
     float mx = -INFINITY, sm = 0.f, mxa = -INFINITY, sma = 0.f;
-    for (int s = 0; s < S; ++s) {
+    for (int s = sub; s < S; s += LANES) {
       float z[KMAX], W[KMAX], l, la;
       sample(s, z, W, l, la);
       if (l > mx) { sm = sm * __expf(mx - l) + 1.f; mx = l; } else { sm += __expf(l - mx); }
       if constexpr (MOD) {
         if (la > mxa) { sma = sma * __expf(mxa - la) + 1.f; mxa = la; } else { sma += __expf(la - mxa); }
       }
+    }
+    if constexpr (LANES > 1) {
+      lse_merge<LANES>(mx, sm);
+      if constexpr (MOD) lse_merge<LANES>(mxa, sma);
     }
     const float lse = mx + logf(sm), lsea = MOD ? mxa + logf(sma) : 0.f;
     // pass 2: accumulate
@@ -367,7 +409,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
       om[k] = 0.f; gx[k] = 0.f; gxz[k] = 0.f;
       if constexpr (MOD) oma[k] = 0.f;
     }
-    for (int s = 0; s < S; ++s) {
+    for (int s = sub; s < S; s += LANES) {
       float z[KMAX], W[KMAX], l, la;
       sample(s, z, W, l, la);
       const float pi = __expf(l - lse);
@@ -386,6 +428,16 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
         gxz[k] = fmaf(t, z[k], gxz[k]);
       }
     }
+    if constexpr (LANES > 1) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        om[k] = lanes_sum<LANES>(om[k]);
+        gx[k] = lanes_sum<LANES>(gx[k]);
+        gxz[k] = lanes_sum<LANES>(gxz[k]);
+        if constexpr (MOD) oma[k] = lanes_sum<LANES>(oma[k]);
+      }
+    }
+    const bool writer = sub == 0 && gt / LANES < N;
     float gve_mc = 0.f;
     if constexpr (MC) {
 #pragma unroll
@@ -394,7 +446,7 @@ __global__ __launch_bounds__(kElboThreads) void elbo_terms_bwd_kernel(
     }
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
-      if (k < K) {
+      if (k < K && writer) {
         float gma = gx[k] * inv_tau;
         float gva = (var_a[(int64_t)k * ldf + n] + jitter > 0.f) ? gxz[k] * inv_tau * 0.5f / sa[k] : 0.f;
         float gmf, gvf;
@@ -1033,10 +1085,20 @@ extern "C" int mgp_philox_normal2(uint64_t seed, int64_t n_offset, int64_t N, in
   return launch_status();
 }
 
-static int64_t elbo_blocks(int64_t N) { return (N + kElboThreads - 1) / kElboThreads; }
+// K6 and its backward: kElboLanes lanes per point (MultiClass: one -- its per-point
+// Gauss-Hermite var-exp and its gradient would be repeated by every lane)
+constexpr int kElboLanes = 4;
+// The backward keeps one lane per point: its lane-split form (LANES = 4, the samples'
+// accumulators summed by shuffles) reorders the float32 sums of G, and the kernel
+// variance gradients, differences of large Kuf / Kuu terms through the Cholesky
+// backward, amplify that reordering past their test bound at small M (measured:
+// assign.variance 9.6e-4 vs 6.8e-4 at N = 1000, M = 25, K = 3, D = 1).
+constexpr int kElboBwdLanes = 1;
+static int64_t elbo_fwd_blocks(int64_t N, int lanes) { return (N * lanes + kElboThreads - 1) / kElboThreads; }
 
 extern "C" size_t mgp_elbo_workspace_bytes(int64_t N) {
-  return (size_t)(elbo_blocks(N) > 0 ? elbo_blocks(N) : 1) * sizeof(double);
+  const int64_t nb = elbo_fwd_blocks(N, kElboLanes);
+  return (size_t)(nb > 0 ? nb : 1) * sizeof(double);
 }
 
 template <int KM, bool MOD, bool MC>
@@ -1045,8 +1107,9 @@ static void launch_elbo_terms(int nb, hipStream_t s, const float* mu_f, const fl
                               const float* lik_var_a, int64_t N, int K, int S, float inv_tau, float jitter,
                               const float* noise_z, const float* noise_u, uint32_t k0, uint32_t k1,
                               int64_t n_offset, double* partials, float mc_a, float mc_b) {
-  hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a, var_a,
-                     ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1, n_offset,
+  constexpr int L = MC ? 1 : kElboLanes;
+  hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC, L>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
+                     var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1, n_offset,
                      partials, mc_a, mc_b);
 }
 
@@ -1060,7 +1123,7 @@ static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu
                           float mc_a = 0.f, float mc_b = 0.f) {
   if (!workspace || workspace_bytes < mgp_elbo_workspace_bytes(N)) return MGP_ERR_WORKSPACE;
   double* partials = (double*)workspace;
-  const int nb = (int)elbo_blocks(N);
+  const int nb = (int)elbo_fwd_blocks(N, mc ? 1 : kElboLanes);
   const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
   if (nb > 0) {
 #define MGP_ELBO_CASE(KM)                                                                               \
@@ -1227,7 +1290,7 @@ extern "C" const char* mgp_status_string(int status) {
 static int elbo_kmax(int K) { return K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32; }
 
 extern "C" size_t mgp_elbo_backward_workspace_bytes(int64_t N, int32_t K) {
-  const int64_t nb = elbo_blocks(N) > 0 ? elbo_blocks(N) : 1;
+  const int64_t nb = N > 0 ? elbo_fwd_blocks(N, kElboLanes) : 1;
   return (size_t)nb * 2 * (size_t)elbo_kmax(K) * sizeof(double);
 }
 
@@ -1237,7 +1300,8 @@ static void launch_elbo_bwd(int nb, hipStream_t s, const float* mu_f, const floa
                             const float* lik_var_a, int64_t N, int K, int S, float inv_tau, float jitter,
                             const float* noise_z, const float* noise_u, uint32_t k0, uint32_t k1, int64_t n_offset, float scale,
                             float* G, int64_t ldg, double* partials, float mc_a, float mc_b) {
-  hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, MOD, MC>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
+  constexpr int L = MC ? 1 : kElboBwdLanes;
+  hipLaunchKernelGGL((elbo_terms_bwd_kernel<KM, MOD, MC, L>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
                      var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1, n_offset,
                      scale, G, ldg, partials, mc_a, mc_b);
 }
@@ -1250,7 +1314,7 @@ static int elbo_bwd_run(const float* mu_f, const float* var_f, const float* mu_a
                         float mc_a, float mc_b) {
   if (!workspace || workspace_bytes < mgp_elbo_backward_workspace_bytes(N, K)) return MGP_ERR_WORKSPACE;
   double* partials = (double*)workspace;
-  const int nb = (int)elbo_blocks(N);
+  const int nb = (int)elbo_fwd_blocks(N, mc ? 1 : kElboBwdLanes);
   const int km = elbo_kmax(K);
   const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
   if (nb == 0) {

@@ -173,6 +173,11 @@ static bool k5_shape16() {
   const char* e = getenv("MGP_K5_SHAPE");
   return !(e && atoi(e) == 32);
 }
+// K4 (split-f16 in and out, f16 cross terms) likewise: trsm_stats16_kernel unless MGP_K4_SHAPE=32
+static bool k4_shape16() {
+  const char* e = getenv("MGP_K4_SHAPE");
+  return !(e && atoi(e) == 32);
+}
 
 // Item b -> (row tile t heavy-first, column tile tn, expert k); the K experts of
 // a column tile are 8 block ids apart (one XCD) when nTn % 8 == 0.
@@ -1532,6 +1537,192 @@ __global__ __launch_bounds__(256, 2) void trsm_stats_x6_kernel(
                                           Afr, stats, lds_, Af32, lda, a_var, t_bound, k_bound);
 }
 
+// ------------------------------------------------------------------ K4 (split-f16) on 16x16x32 MFMAs
+// trsm_stats_x6_item<KMAX, true, true> on x6_mainloop16 (as expert_cond16_kernel is K5 on
+// it): the same items, images, outputs and bounds.  Epilogue per 16-row block ib (k-step
+// 8 t + ib of A's image): the image fragment of each 32-column block from two lanes of the
+// 16x16 accumulator layout (one exchange across the lane halves, as K5's C_k images);
+// sum A^2 straight from the accumulators; the q_mu^T A stats of each 64-row stats tile on
+// 16x16x32 f16 MFMAs whose B operand is the accumulators themselves: lane (i, q) slot j
+// holds row 4q + j (j < 4) of block ib and row 4q + j - 4 of block ib + 1 -- any k order
+// shared by both operands is the same sum, so the split q_mu operand (from LDS) is built
+// in that order and no exchange is needed.  Rows kk of the 16 x 16 stats block are q_mu's
+// columns (KMAX <= 16).
+__device__ __forceinline__ void store_acc16_f32(const floatx4v (&acc)[8][4], float* __restrict__ out, int64_t ld,
+                                                int64_t i0, int64_t n0, int64_t M, int64_t N) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, (int)(uint32_t)(M * ld * 4), 0x00020000);
+  const uint32_t soff = (uint32_t)((i0 * ld + n0) * 4);
+  const uint32_t ld32 = (uint32_t)ld;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int nl = 64 * w + 16 * cb + li;
+    if (n0 + nl < N) {
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t rl = (uint32_t)(16 * ib + 4 * q + e);
+          // (through a float: __builtin_bit_cast of the vector element lvalue itself
+          // reads element 0 with this compiler)
+          const float x = acc[ib][cb][e];
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, (rl * ld32 + (uint32_t)nl) * 4u,
+                                                soff, 0);
+        }
+    }
+  }
+}
+
+template <int KMAX>
+__device__ __forceinline__ void trsm_stats16_item(
+    bf16x8 (*sL)[4 * 2 * 3 * 64], float* __restrict__ sQ, int t, int tn, const bf16x8* __restrict__ Tfr,
+    uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
+    const float* __restrict__ q_mu, int64_t ldq, int K, bf16x8* __restrict__ Afr, float* __restrict__ stats,
+    int64_t lds_, float* __restrict__ Af32, int64_t lda, const float* __restrict__ a_var,
+    const float* __restrict__ t_bound, const float* __restrict__ k_bound) {
+  static_assert(KMAX <= 16, "the stats block has 16 rows");
+  const int lane = threadIdx.x & 63, li = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t i0 = 128 * (int64_t)t;
+  const float a_scale = ldexpf(1.f, img_exp(sqrtf(*a_var)));
+  // q_mu rows of the tile -> LDS [128][KMAX] and max |q_mu| (published by the main loop's barriers)
+  if (stats) {
+    float qmax = 0.f;
+    for (int idx = threadIdx.x; idx < 128 * KMAX; idx += 256) {
+      const int r = idx / KMAX, kk = idx % KMAX;
+      const float qv = (i0 + r < M && kk < K) ? q_mu[(i0 + r) * ldq + kk] : 0.f;
+      sQ[idx] = qv;
+      qmax = fmaxf(qmax, fabsf(qv));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(sQ + 128 * KMAX), __float_as_uint(qmax));
+  }
+  floatx4v acc[8][4];
+  x6_mainloop16<2, 2, true>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
+                            img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0,
+                            4 * t + 4, nmk);
+  {
+    const float unscale = ldexpf(1.f, -(img_exp(*t_bound) + img_exp(*k_bound)));
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[ib][cb][e] *= unscale;
+  }
+  if (Af32) store_acc16_f32(acc, Af32, lda, i0, (int64_t)tn * kX6BN, M, N);
+  // A's image: fragment (column block 8 tn + 2 w + c, k-step 8 t + ib), lane position pos
+  const bool lo_half = lane < 32;
+  const int pos = lo_half ? li + 32 * q : 16 + li + 32 * (q - 2);
+#pragma unroll
+  for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const floatx4v send = lo_half ? acc[ib][2 * c + 1] : acc[ib][2 * c];
+      float y[4], v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(send[r], 32, 64);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = lo_half ? acc[ib][2 * c][r] : y[r];
+        v[4 + r] = lo_half ? y[r] : acc[ib][2 * c + 1][r];
+      }
+      store_split_f16(Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, a_scale);
+    }
+  if (!stats) return;
+  const int qe = img_exp(__uint_as_float(reinterpret_cast<const unsigned int*>(sQ)[128 * KMAX]));
+  const float q_scale = ldexpf(1.f, qe), s_unscale = ldexpf(1.f, -(qe + img_exp(sqrtf(*a_var))));
+#pragma unroll
+  for (int st2 = 0; st2 < 2; ++st2) {  // 64-row stats tile 2 t + st2 = row blocks 4 st2 .. 4 st2 + 3
+    floatx4v sq[4];
+    float a2[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      sq[cb] = floatx4v{0.f, 0.f, 0.f, 0.f};
+      a2[cb] = 0.f;
+    }
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {  // row blocks ib0 = 4 st2 + 2 pr and ib0 + 1 (32 rows)
+      const int ib0 = 4 * st2 + 2 * pr;
+      bf16x8 qf[3];
+      {
+        halfx8 qh, ql;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int row = 16 * ib0 + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4);
+          const float x = (li < K ? sQ[row * KMAX + (li < KMAX ? li : 0)] : 0.f) * q_scale;
+          const _Float16 xh = (_Float16)x;
+          qh[j] = xh;
+          ql[j] = (_Float16)(x - (float)xh);
+        }
+        qf[0] = __builtin_bit_cast(bf16x8, qh);
+        qf[1] = __builtin_bit_cast(bf16x8, ql);
+      }
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        halfx8 vh, vl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = j < 4 ? acc[ib0][cb][j] : acc[ib0 + 1][cb][j - 4];
+          a2[cb] = fmaf(a, a, a2[cb]);
+          const float x = a * a_scale;
+          const _Float16 xh = (_Float16)x;
+          vh[j] = xh;
+          vl[j] = (_Float16)(x - (float)xh);
+        }
+        const bf16x8 bf[3] = {__builtin_bit_cast(bf16x8, vh), __builtin_bit_cast(bf16x8, vl), bf16x8{}};
+        sq[cb] = mfma16_fmt<2, true>(qf, bf, sq[cb]);
+      }
+    }
+    const int64_t st = 2 * (int64_t)t + st2;
+    if (64 * st < M) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int64_t n = (int64_t)tn * kX6BN + 64 * w + 16 * cb + li;
+        float s_a2 = a2[cb] + __shfl_xor(a2[cb], 16, 64);
+        s_a2 += __shfl_xor(s_a2, 32, 64);
+        if (n < N) {
+          float* dst = stats + st * (K + 1) * lds_ + n;
+          if (lane < 16) dst[0] = s_a2;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int kk = 4 * q + e;
+            if (kk < K) dst[(int64_t)(1 + kk) * lds_] = sq[cb][e] * s_unscale;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Row-tile pairs as trsm_stats_x6_kernel (equal work per workgroup).
+template <int KMAX>
+__global__ __launch_bounds__(256, 2) void trsm_stats16_kernel(
+    const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
+    int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
+    bf16x8* __restrict__ Afr, float* __restrict__ stats, int64_t lds_, float* __restrict__ Af32, int64_t lda,
+    const float* __restrict__ a_var, float* __restrict__ a_bound, const float* __restrict__ t_bound,
+    const float* __restrict__ k_bound) {
+  __shared__ bf16x8 sL[2][4 * 2 * 3 * 64];
+  __shared__ float sQ[128 * KMAX + 1];
+  const int nT = nmk / 8, nP = (nT + 1) / 2;
+  int p, tn;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a_bound = sqrtf(*a_var);
+  col_major_item(blockIdx.x, nP, nTn, p, tn);
+  if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
+  __syncthreads();
+  trsm_stats16_item<KMAX>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
+                          lds_, Af32, lda, a_var, t_bound, k_bound);
+  if (nT - 1 - p == p) return;
+  __syncthreads();
+  if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
+  __syncthreads();
+  trsm_stats16_item<KMAX>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats, lds_,
+                          Af32, lda, a_var, t_bound, k_bound);
+}
+
 }  // namespace mgp
 
 using namespace mgp;
@@ -1725,6 +1916,10 @@ static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb
       hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                          (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
                          (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
+    else if (k4_shape16())
+      hipLaunchKernelGGL((trsm_stats16_kernel<KMAX>), grid, dim3(256), 0, s, (const bf16x8*)Tfr, (uint32_t)tb,
+                         (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K, (bf16x8*)Afr, stats, lds, A,
+                         lda, a_var, a_bound, t_bound, k_bound);
     else
       hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                          (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,

@@ -108,7 +108,9 @@ def test_expert_conditional_f16_accuracy(device):
     assert errs["f16"][1] < 1.5 * errs["x6"][1]        # measured 7.34e-7 vs x6 7.31e-7
     assert errs["f16 chain"][0] < 1e-4 and errs["f16 chain"][1] < 1e-4
     assert errs["f16 chain"][0] < 8 * errs["x6"][0] and errs["f16 chain"][1] < 8 * errs["x6"][1]
-    assert errs["f16x8 chain"][0] == errs["f16 chain"][0]  # fmean from K4's stats
+    # fmean from K4's stats: the f16x8 chain's K4 is the 32x32x16 kernel, the f16 chain's
+    # the 16x16x32 one (trsm_stats16_kernel) -- the same products in another summation order
+    assert errs["f16x8 chain"][0] == pytest.approx(errs["f16 chain"][0], rel=0.05)
     assert errs["f16x8 chain"][1] < 1e-4
 
 
