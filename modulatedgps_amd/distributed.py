@@ -50,24 +50,49 @@ def allreduce_data_term(t, group=None):
     return t
 
 
-def allreduce_gradients(tensors, group=None):
-    """Sum a list of gradient tensors over the group with one collective per dtype:
-    the tensors are packed into a flat bucket (float32 / float64), all-reduced and
-    unpacked in place.  The training step's only data-path exchange (the gradients
-    of the per-shard data terms; the KL part is added after it on every rank)."""
+class PendingBucket:
+    """An all-reduce of one gradient bucket in flight (allreduce_gradients_async);
+    wait() orders the current stream after it and unpacks the sums in place."""
+
+    def __init__(self, works, packs):
+        self._works, self._packs = works, packs
+
+    def wait(self):
+        for w in self._works:
+            w.wait()
+        for flat, ts in self._packs:
+            o = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[o:o + n].view_as(t))
+                o += n
+        self._works, self._packs = [], []
+
+
+def allreduce_gradients_async(tensors, group=None):
+    """Start the sum of a list of gradient tensors over the group, one collective per
+    dtype: the tensors are packed into a flat bucket (float32 / float64) on the
+    current stream and all-reduced asynchronously (RCCL runs it on its own stream,
+    after the bucket is packed), so the caller's next kernels -- the other layer's
+    backward -- overlap it.  The tensors must not change until wait()."""
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):
-        return tensors
+        return PendingBucket([], [])
     by_dtype = {}
     for t in tensors:
         by_dtype.setdefault(t.dtype, []).append(t)
+    works, packs = [], []
     for ts in by_dtype.values():
         flat = torch.cat([t.reshape(-1) for t in ts])
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-        o = 0
-        for t in ts:
-            n = t.numel()
-            t.copy_(flat[o:o + n].view_as(t))
-            o += n
+        works.append(dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True))
+        packs.append((flat, ts))
+    return PendingBucket(works, packs)
+
+
+def allreduce_gradients(tensors, group=None):
+    """Sum a list of gradient tensors over the group (allreduce_gradients_async, then
+    wait).  The training step's only data-path exchange: the gradients of the
+    per-shard data terms (the KL part is added after it on every rank)."""
+    allreduce_gradients_async(tensors, group).wait()
     return tensors
 
 

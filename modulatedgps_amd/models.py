@@ -751,6 +751,7 @@ class SMGP(SGP):
         grads = {"lik_variance": glv} if mc is None else {}
         if alv is not None:
             grads["assign_lik_variance"] = glva
+        pending = []
         for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
             M = layer.num_inducing
             with _Stage(timing, "conditional_bwd"):
@@ -773,12 +774,21 @@ class SMGP(SGP):
                                                                   device=self.device))
                 ops.rbf_backward(layer.Z, layer.Z, k.variance, k.lengthscales, gKuu, symmetric=True,
                                  accumulate=True, gZ=gZ, g_var=gvar, g_ls=gls)
-            grads.update({name + ".Z": gZ, name + ".variance": gvar, name + ".lengthscales": gls,
-                          name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]})
+            layer_grads = {name + ".Z": gZ, name + ".variance": gvar, name + ".lengthscales": gls,
+                           name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]}
+            if process_group is not None:
+                # one bucket per layer, all-reduced while the next layer's backward runs
+                # (the first also carries the data-term sum and the likelihood gradients)
+                from .distributed import allreduce_gradients_async
+                bucket = list(layer_grads.values())
+                if not pending:
+                    bucket = [b["data_sum"]] + list(grads.values()) + bucket
+                pending.append(allreduce_gradients_async(bucket, group=process_group))
+            grads.update(layer_grads)
         if process_group is not None:
-            from .distributed import allreduce_gradients
             with _Stage(timing, "allreduce"):
-                allreduce_gradients([b["data_sum"]] + list(grads.values()), group=process_group)
+                for pb in pending:
+                    pb.wait()
         num_data = self.num_data if self.num_data is not None else n_batch
         for name, layer in (("pred", self.pred_layer), ("assign", self.assign_layer)):
             ops.kl_grad(layer.q_mu, layer.q_sqrt, num_data, grads[name + ".q_mu"], grads[name + ".q_sqrt"])

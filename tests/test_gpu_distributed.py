@@ -163,17 +163,25 @@ def _rccl_worker(rank, world, port, q):
     plain = float(model._build_likelihood(Xd, Y, noise=noise).cpu())
     via = float(model._build_likelihood(Xd, Y, noise=noise, process_group=dist.group.WORLD).cpu())
     expert = float(expert_parallel_elbo(model, Xd, Y, noise=noise).cpu())
-    q.put((dist.get_backend(), plain, via, expert, R.smgp_elbo(X, Y, p, z, u)))
+    # the training step's per-layer gradient buckets through RCCL (async, overlapped
+    # with the next layer's backward) against the step without a process group
+    e0, g0 = model.elbo_and_grad(Xd, Y, noise=noise)
+    g0 = {k: v.double().cpu() for k, v in g0.items()}
+    e1, g1 = model.elbo_and_grad(Xd, Y, noise=noise, process_group=dist.group.WORLD)
+    gdiff = max(float((v.double().cpu() - g0[k]).abs().max() / (g0[k].abs().max() + 1e-30)) for k, v in g1.items())
+    q.put((dist.get_backend(), plain, via, expert, R.smgp_elbo(X, Y, p, z, u), float(e0.cpu()), float(e1.cpu()),
+           gdiff))
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
 def test_rccl_collectives_on_device(device):
-    """The ELBO's all-reduce and the expert layout's all_to_all through RCCL
-    (backend "nccl") on device tensors, one rank."""
+    """The ELBO's all-reduce, the expert layout's all_to_all and the training step's
+    gradient buckets through RCCL (backend "nccl") on device tensors, one rank."""
     procs, q = _spawn(_rccl_worker, 1)
-    backend, plain, via, expert, ref = q.get(timeout=280)
+    backend, plain, via, expert, ref, e0, e1, gdiff = q.get(timeout=280)
     _join(procs)
     assert backend == "nccl"
+    assert e1 == pytest.approx(e0, rel=1e-7) and gdiff < 1e-6
     assert via == pytest.approx(plain, rel=1e-7) and expert == pytest.approx(plain, rel=1e-6)
     assert plain == pytest.approx(ref, rel=1e-4)
