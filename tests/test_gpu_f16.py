@@ -148,3 +148,33 @@ def test_elbo_configs_formats(device, fmt_mode, N, M, K, D, ls, S):
     assert normwise(to_np(var_f).T, parts["var_f"]) < 1e-4
     assert normwise(to_np(mu_a).T, parts["mu_a"]) < 1e-4
     assert normwise(to_np(var_a).T, parts["var_a"]) < 1e-4
+
+
+@pytest.mark.parametrize("k4_shape,k5_shape", [("16", "16"), ("32", "32"), ("32", "16"), ("16", "32")])
+def test_mfma_shape_switches(device, monkeypatch, k4_shape, k5_shape):
+    """The split-f16 K4 and K5 on 16x16x32 MFMAs (trsm_stats16_kernel,
+    expert_cond16_kernel: the defaults) and on 32x32x16 (MGP_K4_SHAPE / MGP_K5_SHAPE
+    = 32, read per call): every combination against the float64 oracle at config-3
+    shapes (ragged N), the forward and the training K5 that also writes the C_k images."""
+    from modulatedgps_amd import ops
+    monkeypatch.setenv("MGP_K4_SHAPE", k4_shape)
+    monkeypatch.setenv("MGP_K5_SHAPE", k5_shape)
+    N, M, K, D, ls = 3001, 1024, 8, 8, 1.0
+    X, _, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
+    L = p.pred
+    mu_ref, var_ref = R.svgp_predict_f_dedup(X, L["Z"], L["variance"], L["lengthscales"], L["q_mu"], L["q_sqrt"])
+    var, lsc, Zt = _t([L["variance"]], device), _t([ls], device), _t(L["Z"], device)
+    _, LinvT, _ = ops.kuu_potrf_trtri([Zt], [var], [lsc], 1e-6)
+    qm, qs = _t(L["q_mu"], device), ops.as_padded(_t(L["q_sqrt"], device))
+    Khr = ops.rbf_kuf_x6(_t(X, device), Zt, var, lsc, fmt="f16")
+    Thr = ops.split_upper_x6(LinvT[0], fmt="f16")
+    A32 = ops.padded(M, N, device)
+    Afr, stats = ops.trsm_stats_x6(Thr, Khr, qm, M, N, A=A32, f16_variance=var, in_fmt="f16", cross="f16")
+    Lfr = ops.split_lower_x6(qs, fmt="f16")
+    fm, fv = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmt="f16", cross="f16")
+    assert normwise(to_np(fm).T, mu_ref) < 1e-4 and normwise(to_np(fv).T, var_ref) < 1e-4
+    Cfr = torch.empty(ops.c_images_bytes(M, N, K), dtype=torch.uint8, device=device)
+    fmc, fvc = ops.expert_conditional_x6(Afr, Lfr, stats, var, M, N, K, fmt="f16", cross="f16",
+                                         c_out=(Cfr, ops.colnorm_max(qs)))
+    assert normwise(to_np(fvc).T, var_ref) < 1e-4
+    assert normwise(to_np(fvc), to_np(fv)) < 1e-6
