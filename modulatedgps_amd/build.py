@@ -73,5 +73,27 @@ def build(verbose=False, extra_flags=()):
     return LIB
 
 
+C_ABI_SRC = os.path.join(ROOT, "tests", "c_abi", "elbo_c.cpp")
+C_ABI_BIN = os.path.join(ROOT, "tests", "c_abi", "elbo_c")
+
+
+def build_c_abi_test(verbose=False):
+    """tests/c_abi/elbo_c: a host program that runs one ELBO through the C-ABI of
+    libmgp_hip.so alone (no torch), for tests/test_gpu_c_abi.py.  Linked against the
+    in-tree library by a relative rpath, so it runs from the snapshot on the GPU box."""
+    lib = build(verbose)
+    if _mtime(C_ABI_BIN) >= max(_mtime(C_ABI_SRC), _mtime(lib), _mtime(os.path.join(INCLUDE, "mgp_hip.h"))):
+        return C_ABI_BIN
+    cmd = [HIPCC, "-O2", "-std=c++17", "-I", INCLUDE, C_ABI_SRC, "-o", C_ABI_BIN, "-L", PKG, "-lmgp_hip",
+           "-Wl,-rpath,$ORIGIN/../../modulatedgps_amd"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"C-ABI test program failed to build:\n{r.stdout}\n{r.stderr}")
+    return C_ABI_BIN
+
+
 if __name__ == "__main__":
     print(build(verbose="-v" in sys.argv))
+    print(build_c_abi_test(verbose="-v" in sys.argv))
