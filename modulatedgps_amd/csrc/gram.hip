@@ -15,6 +15,7 @@
 // parallelism; partial tiles go to a workspace and gram_reduce_kernel sums
 // them in a fixed order (deterministic), applies alpha and the triangle.
 // Roofline: f32 MFMA (2 MI MJ N flops, half for the triangular outputs).
+#include <atomic>
 #include "mgp_common.hpp"
 
 namespace mgp {
@@ -667,46 +668,67 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
 
 // out[b][i][j] = alpha * sum_z ws[z][b][i][j]; mode 0 full, 1 lower triangle
 // (zero above), 2 symmetric (the upper triangle mirrors the lower).  Grid
-// (32-column tile, 32-row tile, batch), 256 threads: the source tile (the
-// mirrored one above the diagonal in mode 2) is summed with row-contiguous
-// loads into LDS and written out transposed where needed -- coalesced both ways,
-// no index divisions.
+// (32-column tile, 32-row tile, batch), 256 threads = 32 rows x 8 four-column
+// groups: the source tile (the mirrored one above the diagonal in mode 2) is
+// summed with 16-B row-contiguous loads, four splits in flight per thread (fixed
+// order: split z into partial z % 4, then (p0 + p1) + (p2 + p3)), into LDS and
+// written out transposed where needed -- coalesced both ways, no index divisions.
 __global__ __launch_bounds__(256) void gram_x6_reduce_kernel(const float* __restrict__ ws, int64_t bstride,
                                                              int64_t zstride, int nsplit, int64_t MI, int64_t MJ,
                                                              float alpha, int mode, float* __restrict__ out,
                                                              int64_t ldo, int64_t so) {
   __shared__ float sT[32][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
   const int64_t bi = blockIdx.y, bj = blockIdx.x, b = blockIdx.z;
   const bool mirror = mode == 2 && bj > bi;
   const bool skip = mode == 1 && bj > bi;  // a zero tile
   const int64_t ti = mirror ? bj : bi, tj = mirror ? bi : bj;
   if (!skip) {
+    const int64_t r = 32 * ti + ty, c = 32 * tj + 4 * tx;
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r < MI && c < MJ) {
+      const float* src = ws + b * bstride + r * MJ + c;
+      if (c + 4 <= MJ && (MJ & 3) == 0) {  // 16-B aligned rows (zstride, bstride are multiples of MJ)
+        floatx4 p[4] = {v, v, v, v};
+        int z = 0;
+        for (; z + 4 <= nsplit; z += 4) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t r = 32 * ti + ty + 8 * k, c = 32 * tj + tx;
-      float v = 0.f;
-      if (r < MI && c < MJ) {
-        const float* src = ws + b * bstride + r * MJ + c;
-        for (int z = 0; z < nsplit; ++z) v += src[(int64_t)z * zstride];
+          for (int u = 0; u < 4; ++u) p[u] += *reinterpret_cast<const floatx4*>(src + (int64_t)(z + u) * zstride);
+        }
+        for (; z < nsplit; ++z) p[z & 3] += *reinterpret_cast<const floatx4*>(src + (int64_t)z * zstride);
+        v = (p[0] + p[1]) + (p[2] + p[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c + e < MJ)
+            for (int z = 0; z < nsplit; ++z) v[e] += src[(int64_t)z * zstride + e];
       }
-      sT[ty + 8 * k][tx] = v * alpha;
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sT[ty][4 * tx + e] = v[e] * alpha;
   }
   __syncthreads();
+  const int64_t i = 32 * bi + ty, j0 = 32 * bj + 4 * tx;
+  if (i >= MI || j0 >= MJ) return;
+  floatx4 o;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int li = ty + 8 * k;
-    const int64_t i = 32 * bi + li, j = 32 * bj + tx;
-    if (i >= MI || j >= MJ) continue;
-    float v;
+  for (int e = 0; e < 4; ++e) {
+    const int lj = 4 * tx + e;
+    const int64_t j = j0 + e;
     if (skip || (mode == 1 && j > i))
-      v = 0.f;
+      o[e] = 0.f;
     else if (mirror || (mode == 2 && bi == bj && j > i))
-      v = sT[tx][li];
+      o[e] = sT[lj][ty];
     else
-      v = sT[li][tx];
-    out[b * so + i * ldo + j] = v;
+      o[e] = sT[ty][lj];
+  }
+  float* dst = out + b * so + i * ldo + j0;
+  if (j0 + 4 <= MJ && ((ldo | so) & 3) == 0 && ((uintptr_t)out & 15) == 0) {
+    *reinterpret_cast<floatx4*>(dst) = o;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (j0 + e < MJ) dst[e] = o[e];
   }
 }
 
@@ -847,11 +869,44 @@ extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y,
   return launch_status();
 }
 
-static int gram_x6_splits(int64_t N, int64_t wgs) {
-  // aim for >= 2048 workgroups, each with >= 2048 points
-  int s = 1;
-  while (wgs * s < 2048 && N / (2 * s) >= 2048) s *= 2;
-  return s;
+// CUs of the current device (the 768-thread grams run one workgroup per CU).
+static int device_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
+
+// Split-K count of the 768-thread grams (items = workgroups per split, out_tiles =
+// 128 x 128 output tiles the reduction sums): every workgroup of a launch holds
+// the same n-count, so the launch lasts (workgroup rounds) x (chunks per workgroup
+// + ~4 chunks of pipeline fill and store); the reduction reads one more tile set
+// per split (~0.009 chunk times per tile, measured at c3).  Among 1, 2, 4 and the multiples
+// of 8 up to 64 (one n-slab per XCD), with >= 512 points per workgroup, the
+// cheapest count wins (a larger count only when >= 1 % cheaper).  The earlier
+// rule (double until 2048 workgroups) left c3's P_k gram 4.5 rounds deep: 16
+// splits instead of 8 take it from 2.28 to 2.12 ms (profiles/r03_gram_splits_probe.log).
+static int gram_x6_splits(int64_t N, int64_t items, int64_t out_tiles) {
+  const int cus = device_cus();
+  int best = 1;
+  double best_cost = 1e300;
+  static const int cand[] = {1, 2, 4, 8, 16, 24, 32, 40, 48, 56, 64};
+  for (int s : cand) {
+    if (s > 1 && N / s < 512) break;
+    const int64_t rounds = (items * s + cus - 1) / cus;
+    const int64_t nch = (N + (int64_t)s * kXC - 1) / ((int64_t)s * kXC);
+    const double cost = (double)rounds * (double)(nch + 4) + 0.009 * (double)out_tiles * s;
+    if (cost < best_cost * 0.99) {
+      best_cost = cost;
+      best = s;
+    }
+  }
+  return best;
 }
 
 static int gram_x6_tiles(int64_t MI, int64_t MJ, int tri) {
@@ -861,8 +916,11 @@ static int gram_x6_tiles(int64_t MI, int64_t MJ, int tri) {
 
 extern "C" size_t mgp_gram_x6_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t batch, int32_t mode) {
   if (MI <= 0 || MJ <= 0 || N <= 0 || batch <= 0) return 16;
-  const int tiles = gram_x6_tiles(MI, MJ, mode != 0);
-  return (size_t)gram_x6_splits(N, (int64_t)tiles * batch) * (size_t)batch * (size_t)MI * (size_t)MJ * sizeof(float);
+  const int64_t tiles = gram_x6_tiles(MI, MJ, mode != 0);
+  // the larger of the x6 kernel's count and the row-image kernel's (entry pairs)
+  const int s1 = gram_x6_splits(N, tiles * batch, tiles * batch);
+  const int s2 = gram_x6_splits(N, tiles * ((batch + 1) / 2), tiles * batch);
+  return (size_t)(s1 > s2 ? s1 : s2) * (size_t)batch * (size_t)MI * (size_t)MJ * sizeof(float);
 }
 
 static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, const float* Y, int64_t ldy,
@@ -896,7 +954,7 @@ static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, c
   hipStream_t s = (hipStream_t)stream;
   const int tiles = gram_x6_tiles(MI, MJ, mode != 0);
   const int nbj = (int)((MJ + kGT - 1) / kGT);
-  const int nsplit = N > 0 ? gram_x6_splits(N, (int64_t)tiles * batch) : 1;
+  const int nsplit = N > 0 ? gram_x6_splits(N, (int64_t)tiles * batch, (int64_t)tiles * batch) : 1;
   int64_t nper = (N + nsplit - 1) / nsplit;
   nper = (nper + kXC - 1) / kXC * kXC;
   float* ws = (float*)workspace;
@@ -974,12 +1032,12 @@ extern "C" int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI
   hipStream_t s = (hipStream_t)stream;
   const int tiles = gram_x6_tiles(MI, MJ, mode != 0);
   const int nbj = (int)((MJ + kGT - 1) / kGT);
-  const int nsplit = N > 0 ? gram_x6_splits(N, (int64_t)tiles * batch) : 1;  // the x6 gram's workspace
+  const int pairs = (batch + 1) / 2;
+  const int nsplit = N > 0 ? gram_x6_splits(N, (int64_t)tiles * pairs, (int64_t)tiles * batch) : 1;
   int64_t nper = (N + nsplit - 1) / nsplit;
   nper = (nper + kXC - 1) / kXC * kXC;
   float* ws = (float*)workspace;
   const int64_t bstride = MI * MJ, zstride = (int64_t)batch * MI * MJ;
-  const int pairs = (batch + 1) / 2;
   const dim3 grid((unsigned)(tiles * pairs * nsplit));
   if (mode != 0)
     hipLaunchKernelGGL(gram_rows2_kernel<true>, grid, dim3(768), 0, s, (const char*)ximg, nns, MI, Y, ldy, MJ, W, sw,
