@@ -771,6 +771,196 @@ __global__ __launch_bounds__(256) void grad_a_base_kernel(const float* __restric
   }
 }
 
+// Steps 2, 5 (A's row image) and 6 (g_q_mu) of the split-f16 conditional backward
+// in ONE pass over A (three kernels read A before: grad_a_base, split_rows_f16,
+// gram_narrow).  Workgroup: one slab of 8 k-steps (128 n) x kPrepRB 32-row blocks;
+// G_mu and sum_k Gv over the slab's columns are staged in LDS once.  Per row block:
+//   (1) coalesced: thread t takes rows t / 32 + 8 i (i < 4), columns 4 (t % 32) + e
+//       of A (16-B loads, two 512-B rows per wave instruction) and writes
+//       gA0[m][n] = sum_k q_mu[m][k] G_mu[k][n] - 2 A[m][n] sum_k Gv[k][n] the same
+//       way, and puts the tile into LDS (pitch 132 floats: conflict-free reads below);
+//   (2) fragments: lane (r, h) of wave w takes row r, k-steps w and w + 4
+//       (n = 16 ns + 8 h + j), stores split_rows_f16(A)'s image (same layout and
+//       scale 2^img_exp(*bound)) and sums A[m][n] G_mu[k][n] for g_q_mu:
+//       part[slab][m][k] (f32 per slab; folded in float64 by prep_fold_kernel).
+// The tile and the row sums are double-buffered: one barrier per row block.
+// c3 (MI355X, rocprofv3): 205 us per layer against 126 + 90 + 111 + 12 us for
+// grad_a_base, split_rows_f16, gram_narrow and its fold (profiles/r03_grad_a_prep_probe.log).
+// Measured, not kept: the next row block's A loads issued before (2) (287 vs 248 us),
+// 4 instead of 8 row blocks per workgroup (same).
+constexpr int kPrepRB = 8, kPrepPitch = 132;
+template <int KMAX>
+__global__ __launch_bounds__(256) void grad_a_prep_kernel(const float* __restrict__ A, int64_t lda,
+                                                          const float* __restrict__ q_mu, int64_t ldq,
+                                                          const float* __restrict__ Gmu,
+                                                          const float* __restrict__ Gv, int64_t ldg, int64_t M,
+                                                          int64_t N, int K, int nns, const float* __restrict__ bound,
+                                                          float* __restrict__ gA0, int64_t ldo,
+                                                          bf16x8* __restrict__ img, float* __restrict__ part, int rbs, int qvec) {
+  __shared__ __attribute__((aligned(16))) float sg[KMAX + 1][128];  // G_mu rows, then sum_k Gv
+  __shared__ __attribute__((aligned(16))) float sA[2][32][kPrepPitch];
+  __shared__ float sp[2][4][32][KMAX];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int64_t nsb = 8 * (int64_t)blockIdx.x, n0 = 16 * nsb;
+  const int64_t rb0 = (int64_t)blockIdx.y * rbs;
+  const int nblk = (int)((M + 31) / 32);
+  const int nit = nblk - rb0 < rbs ? (int)(nblk - rb0) : rbs;
+  for (int i = tid; i < (KMAX + 1) * 32; i += 256) {  // 4 columns per item
+    const int k = i >> 5, c = 4 * (i & 31);
+    const int64_t n = n0 + c;
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (k < KMAX) {
+      if (k < K) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = n + e < N ? Gmu[(int64_t)k * ldg + n + e] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KMAX; ++kk)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (kk < K && n + e < N) ? Gv[(int64_t)kk * ldg + n + e] : 0.f;
+    }
+    *reinterpret_cast<floatx4*>(&sg[k][c]) = v;
+  }
+  __syncthreads();
+  const float scale = ldexpf(1.f, img_exp(*bound));
+  const int ct_r = tid >> 5, ct_c = 4 * (tid & 31);
+  const int64_t nc = n0 + ct_c;
+  const bool colvec = nc + 3 < N;
+  floatx4 gmu4[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) gmu4[k] = *reinterpret_cast<const floatx4*>(&sg[k][ct_c]);
+  const floatx4 gvs4 = *reinterpret_cast<const floatx4*>(&sg[KMAX][ct_c]);
+  auto flush = [&](int it, int b) {
+    for (int i = tid; i < 32 * KMAX; i += 256) {
+      const int rr = i / KMAX, k = i % KMAX;
+      const int64_t m = 32 * (rb0 + it) + rr;
+      if (m < M && k < K)
+        part[((int64_t)blockIdx.x * M + m) * K + k] = (sp[b][0][rr][k] + sp[b][1][rr][k]) + (sp[b][2][rr][k] + sp[b][3][rr][k]);
+    }
+  };
+  auto load_rows = [&](floatx4 (&a)[4], int64_t rb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = 32 * rb + ct_r + 8 * i;
+      a[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (row < M) {
+        if (colvec) {
+          a[i] = *reinterpret_cast<const floatx4*>(A + row * lda + nc);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[i][e] = nc + e < N ? A[row * lda + nc + e] : 0.f;
+        }
+      }
+    }
+  };
+  floatx4 a[4];
+  for (int it = 0; it < nit; ++it) {
+    const int64_t rb = rb0 + it;
+    const int b = it & 1;
+    load_rows(a, rb);
+    // (1) coalesced rows: gA0, the LDS tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = 32 * rb + ct_r + 8 * i;
+      if (row < M) {
+        floatx4 g = -2.f * a[i] * gvs4;
+        if (qvec) {  // q_mu's row in 16-B loads (ldq % 4 == 0, K a multiple of 4)
+#pragma unroll
+          for (int k4 = 0; k4 < KMAX / 4; ++k4) {
+            if (4 * k4 < K) {
+              const floatx4 q = *reinterpret_cast<const floatx4*>(q_mu + row * ldq + 4 * k4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) g += q[e] * gmu4[4 * k4 + e];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k)
+            if (k < K) g += q_mu[row * ldq + k] * gmu4[k];
+        }
+        float* dst = gA0 + row * ldo + nc;
+        if (colvec) {
+          *reinterpret_cast<floatx4*>(dst) = g;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (nc + e < N) dst[e] = g[e];
+        }
+      }
+      *reinterpret_cast<floatx4*>(&sA[b][ct_r + 8 * i][ct_c]) = a[i];
+    }
+    __syncthreads();
+    if (it > 0) flush(it - 1, b ^ 1);
+    // (2) fragments: the image and the g_q_mu row sums
+    float pf[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) pf[k] = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int st = w + 4 * s2;
+      const int64_t ns = nsb + st;
+      if (ns >= nns) continue;
+      const int c = 16 * st + 8 * h;
+      const floatx4 lo = *reinterpret_cast<const floatx4*>(&sA[b][r][c]);
+      const floatx4 hi = *reinterpret_cast<const floatx4*>(&sA[b][r][c + 4]);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+      }
+      store_split_f16(img + (rb * nns + ns) * 128 + lane, v, scale);
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[k] = fmaf(v[j], sg[k][c + j], pf[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) pf[k] += __shfl_xor(pf[k], 32, 64);
+    if (h == 0) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) sp[b][w][r][k] = pf[k];
+    }
+  }
+  __syncthreads();
+  if (nit > 0) flush(nit - 1, (nit - 1) & 1);
+}
+
+// out[m][k] = sum over the slabs of part[slab][m][k] in float64, fixed order:
+// 16 outputs per workgroup, thread (o, g) sums slabs g, g + 16, ... (four running
+// sums, slab c into sum (c / 16) % 4), then the 16 groups in order.
+__global__ __launch_bounds__(256) void prep_fold_kernel(const float* __restrict__ part, int slabs, int64_t M, int K,
+                                                        float* __restrict__ out, int64_t ldo) {
+  __shared__ double sred[16][17];
+  const int o = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t MK = M * K, idx = (int64_t)blockIdx.x * 16 + o;
+  double v = 0.0;
+  if (idx < MK) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int c = g;
+    for (; c + 48 < slabs; c += 64) {
+      a0 += (double)part[(int64_t)c * MK + idx];
+      a1 += (double)part[(int64_t)(c + 16) * MK + idx];
+      a2 += (double)part[(int64_t)(c + 32) * MK + idx];
+      a3 += (double)part[(int64_t)(c + 48) * MK + idx];
+    }
+    for (int u = 0; c < slabs; c += 16, ++u) {
+      const double x = (double)part[(int64_t)c * MK + idx];
+      if (u == 0) a0 += x; else if (u == 1) a1 += x; else a2 += x;
+    }
+    v = (a0 + a1) + (a2 + a3);
+  }
+  sred[g][o] = v;
+  __syncthreads();
+  if (threadIdx.x < 16 && idx < MK) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += sred[q][o];
+    out[(idx / K) * ldo + idx % K] = (float)t;
+  }
+}
+
 // B-b: gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0 with S_k = L_k L_k^T
 // (full split images): item = (row tile t of 128 rows, column tile tn of
 // 128), wave w owns the 32 columns of B block 4 tn + w.  Each expert's
@@ -2188,6 +2378,7 @@ extern "C" int mgp_expert_conditional_f16x8(const void* Afr, size_t afr_bytes, c
 // ------------------------------------------------------------------ conditional backward (x6)
 extern "C" size_t mgp_gram_workspace_bytes(int64_t MI, int64_t MJ, int64_t N, int32_t tri);
 extern "C" size_t mgp_rows_f16_bytes(int64_t M, int64_t N);
+extern "C" int64_t mgp_rows_f16_ksteps(int64_t N);
 extern "C" int mgp_split_rows_f16(const float* X, int64_t ldx, int64_t M, int64_t N, const float* bound, void* img,
                                   size_t img_bytes, mgp_stream_t stream);
 extern "C" int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI, const float* Y, int64_t ldy,
@@ -2214,7 +2405,7 @@ constexpr int kRowSumChunks = 32;  // column chunks of row_sums_kernel
 
 namespace {
 struct CondBwdWs {  // workspace carve-up (256-B aligned pieces)
-  size_t sfr, ga0, gafr, lifr, P, LT, part, bnd, gram, total;
+  size_t sfr, ga0, rimg, qpart, gafr, lifr, P, LT, part, bnd, gram, total;
 };
 size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
@@ -2225,6 +2416,9 @@ CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
   w.sfr = o;  o += al256(mgp_x6_lower_bytes(M, K));
   // gA0 (read last by step 3), then A's row image for the P_k gram (step 5)
   w.ga0 = o;  o += al256(std::max((size_t)M * ldn * 4, mgp_rows_f16_bytes(M, N)));
+  // A's row image written beside gA0 by grad_a_prep_kernel (split-f16), its g_q_mu partials
+  w.rimg = o; o += al256(mgp_rows_f16_bytes(M, N));
+  w.qpart = o; o += al256((size_t)((mgp_rows_f16_ksteps(N) + 7) / 8) * M * K * 4);
   w.gafr = o; o += al256(mgp_x6_cols_bytes(M, N));
   w.lifr = o; o += al256(mgp_x6_lower_bytes(M, 1));
   w.P = o;    o += al256((size_t)K * M * ldm * 4);
@@ -2388,8 +2582,29 @@ static int conditional_backward(
     if ((st = launch_status())) return st;
   }
   }
-  // 2. gA0 = q_mu G_mu - 2 A sum_k Gv_k
-  {
+  // 2. gA0 = q_mu G_mu - 2 A sum_k Gv_k; split-f16: with A's row image (step 5) and
+  //    g_q_mu's partials (step 6) in the same pass over A
+  const float* a_bound = trailer(const_cast<void*>(Afr), cols_planes(M, N));
+  bf16x8* rimg = (bf16x8*)(ws + L.rimg);
+  float* qpart = (float*)(ws + L.qpart);
+  const int nns = (int)mgp_rows_f16_ksteps(N);
+  const int slabs = (nns + 7) / 8;
+  const bool prep = f16 && lda % 4 == 0 && aligned16(A);  // else grad_a_base, split_rows_f16, gram_narrow
+  if (prep) {
+    const int rbs = kPrepRB;
+    const dim3 grid((unsigned)slabs, (unsigned)((M + 32 * rbs - 1) / (32 * rbs)));
+    const int qvec = (ldq % 4 == 0 && K % 4 == 0 && aligned16(q_mu)) ? 1 : 0;
+    if (K <= 4)
+      hipLaunchKernelGGL(grad_a_prep_kernel<4>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, nns,
+                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec);
+    else if (K <= 8)
+      hipLaunchKernelGGL(grad_a_prep_kernel<8>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, nns,
+                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec);
+    else
+      hipLaunchKernelGGL(grad_a_prep_kernel<16>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, nns,
+                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec);
+    if ((st = launch_status())) return st;
+  } else {
     const int rows = 128;
     const dim3 grid((unsigned)((N + 255) / 256), (unsigned)((M + rows - 1) / rows));
     if (K <= 4)
@@ -2433,17 +2648,14 @@ static int conditional_backward(
   //    (x6 grams over N, then over M with the transposed triangle of L_k); f16: the
   //    grams over N on f16 products, bounds |A| <= sqrt(var) (Afr's trailer), max |Gv|
   float* bnd = (float*)(ws + L.bnd);
-  const float* a_bound = trailer(const_cast<void*>(Afr), cols_planes(M, N));
   if (f16) {
     if ((st = hip_status(hipMemsetAsync(bnd, 0, sizeof(float), s)))) return st;
     launch_absmax<0>(Gv, ldg, (int64_t)0, (int64_t)K, N, (int64_t)K, bnd, s);
     if ((st = launch_status())) return st;
-    // A's row image (split once; gA0's space is free after step 3) as the grams'
-    // unweighted side
-    const size_t rimg = mgp_rows_f16_bytes(M, N);
-    if ((st = mgp_split_rows_f16(A, lda, M, N, a_bound, gA0, rimg, stream))) return st;
-    st = mgp_gram_f16_rows(gA0, rimg, M, A, lda, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, a_bound, a_bound, bnd,
-                           gws, gwsb, stream);
+    // A's row image (step 2) as the grams' unweighted side
+    if (!prep && (st = mgp_split_rows_f16(A, lda, M, N, a_bound, rimg, mgp_rows_f16_bytes(M, N), stream))) return st;
+    st = mgp_gram_f16_rows(rimg, mgp_rows_f16_bytes(M, N), M, A, lda, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm,
+                           a_bound, a_bound, bnd, gws, gwsb, stream);
   } else {
     st = mgp_gram_x6(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, gws, gwsb, stream);
   }
@@ -2461,8 +2673,13 @@ static int conditional_backward(
   st = mgp_gram_x6(g_Kuf, ldk, 0, M, A, lda, 0, M, nullptr, 0, N, 1, -1.f, 1, g_Lm, ldgl, M * ldgl, gws, gwsb,
                    stream);
   if (st) return st;
-  st = mgp_gram(A, lda, M, Gmu, ldg, K, N, 1.f, 0, g_q_mu, ldgq, gws, gwsb, stream);
-  if (st) return st;
+  if (prep) {  // g_q_mu from step 2's partials
+    hipLaunchKernelGGL(prep_fold_kernel, dim3((unsigned)((M * K + 15) / 16)), dim3(256), 0, s, qpart, slabs, M, K,
+                       g_q_mu, ldgq);
+  } else {
+    st = mgp_gram(A, lda, M, Gmu, ldg, K, N, 1.f, 0, g_q_mu, ldgq, gws, gwsb, stream);
+    if (st) return st;
+  }
   hipLaunchKernelGGL(row_sums_kernel, dim3((unsigned)K, kRowSumChunks), dim3(256), 0, s, Gv, N, ldg, part);
   hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1), 0, s, part, (int)K * kRowSumChunks, g_var);
   return launch_status();
