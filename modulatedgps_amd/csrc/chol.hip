@@ -1399,17 +1399,27 @@ __global__ __launch_bounds__(kCholThreads) void chol_persist(CholArgs a) {
 //   gKuu = (S + S^T) / 2,
 // all in float64 (M^3 work; Kuu is badly conditioned).  dgemm: C = op(A) op(B)
 // on v_mfma_f64_16x16x4_f64: 64 x 64 tile per workgroup (4 waves x 32 x 32 =
-// 2 x 2 MFMA blocks each), 16-deep LDS chunks.
+// 2 x 2 MFMA blocks each), 16-deep LDS chunks.  tri (the triangular operands of
+// the three products; every term outside the range is an exact zero):
+//   kTriNone: k over [0, M);
+//   kTriUpperK: k over [max(i0, j0), M)  (op(A) upper, op(B) lower: L^T gL, Linv^T G);
+//   kTriBand: k over [j0, i0 + 64)       (A lower, B lower: P Linv);
+//   | kTriLowerOut: tiles wholly above the diagonal are not computed (their
+//     consumer reads only the lower triangle / never reaches them).
+constexpr int kTriNone = 0, kTriUpperK = 1, kTriBand = 2, kTriLowerOut = 4;
 template <bool TA, bool TB, int BN = 64>
 __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A, int64_t lda,
                                                     const double* __restrict__ B, int64_t ldb,
-                                                    double* __restrict__ C, int64_t ldc, int64_t M) {
+                                                    double* __restrict__ C, int64_t ldc, int64_t M, int tri) {
   // 64 x BN tile; wave w: rows wi .. wi + 31, columns wj .. wj + BN / 2 - 1 (NB 16-wide blocks)
   constexpr int NB = BN / 32, LB = BN / 16;  // MFMA column blocks per wave, B loads per thread
   __shared__ double sa[64][17], sb[16][BN + 1];  // sa[i][k] = op(A), sb[k][j] = op(B)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wi = (w >> 1) * 32, wj = (w & 1) * (BN / 2);
   const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * BN;
+  if ((tri & kTriLowerOut) && j0 > i0 + 63) return;
+  const int64_t klo = (tri & kTriUpperK) ? (i0 > j0 ? i0 : j0) : (tri & kTriBand) ? j0 : 0;
+  const int64_t khi = (tri & kTriBand) ? (i0 + 64 < M ? i0 + 64 : M) : M;
   doublex4 acc[2][NB];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1446,11 +1456,11 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A
       sb[TB ? idx % 16 : idx / BN][TB ? idx / 16 : idx % BN] = rb[q];
     }
   };
-  load(0);
-  for (int64_t k0 = 0; k0 < M; k0 += 16) {
+  if (klo < khi) load(klo);
+  for (int64_t k0 = klo; k0 < khi; k0 += 16) {
     store();
     __syncthreads();
-    if (k0 + 16 < M) load(k0 + 16);
+    if (k0 + 16 < khi) load(k0 + 16);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       double av[2], bv[NB];
@@ -1693,10 +1703,15 @@ extern "C" int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, L, ldl, Ld, M, nullptr, (int64_t)0);
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 1, LinvT, ldli, Li, M, nullptr, (int64_t)0);
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, gL, ldg, G, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M);      // L^T gL
+  // L, gL, Linv are lower triangular (exact zeros above), so are P and P Linv: the
+  // products skip the zero terms and the tiles Phi / the next product never read
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M,
+                     kTriUpperK | kTriLowerOut);                                                      // L^T gL
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 2, nullptr, (int64_t)0, T, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL((dgemm_kernel<false, false, 32>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M);     // P Linv
-  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M);      // Linv^T (.)
+  hipLaunchKernelGGL((dgemm_kernel<false, false, 32>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M,
+                     kTriBand | kTriLowerOut);                                                        // P Linv
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M,
+                     kTriUpperK);                                                                     // Linv^T (.)
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 3, nullptr, (int64_t)0, T, M, gKuu, ldo);
   return launch_status();
 }
