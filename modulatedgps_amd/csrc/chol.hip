@@ -1407,13 +1407,14 @@ __global__ __launch_bounds__(kCholThreads) void chol_persist(CholArgs a) {
 //   | kTriLowerOut: tiles wholly above the diagonal are not computed (their
 //     consumer reads only the lower triangle / never reaches them).
 constexpr int kTriNone = 0, kTriUpperK = 1, kTriBand = 2, kTriLowerOut = 4;
-template <bool TA, bool TB, int BN = 64>
+template <bool TA, bool TB, int BN = 64, int KC = 16>
 __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A, int64_t lda,
                                                     const double* __restrict__ B, int64_t ldb,
                                                     double* __restrict__ C, int64_t ldc, int64_t M, int tri) {
-  // 64 x BN tile; wave w: rows wi .. wi + 31, columns wj .. wj + BN / 2 - 1 (NB 16-wide blocks)
-  constexpr int NB = BN / 32, LB = BN / 16;  // MFMA column blocks per wave, B loads per thread
-  __shared__ double sa[64][17], sb[16][BN + 1];  // sa[i][k] = op(A), sb[k][j] = op(B)
+  // 64 x BN tile; wave w: rows wi .. wi + 31, columns wj .. wj + BN / 2 - 1 (NB 16-wide blocks);
+  // KC-deep chunks (KC / 4 MFMA k-steps per barrier pair)
+  constexpr int NB = BN / 32, LA = 64 * KC / 256, LB = KC * BN / 256;  // loads per thread
+  __shared__ double sa[64][KC + 1], sb[KC][BN + 1];  // sa[i][k] = op(A), sb[k][j] = op(B)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wi = (w >> 1) * 32, wj = (w & 1) * (BN / 2);
   const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * BN;
@@ -1425,44 +1426,44 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[a][b] = doublex4{0.0, 0.0, 0.0, 0.0};
-  // chunk k0 .. k0 + 15: thread loads 4 elements of op(A) and LB of op(B) (coalesced
-  // along the contiguous index), one chunk ahead in registers
-  double ra[4], rb[LB];
+  // chunk k0 .. k0 + KC - 1: thread loads LA elements of op(A) and LB of op(B)
+  // (coalesced along the contiguous index), one chunk ahead in registers
+  double ra[LA], rb[LB];
   auto load = [&](int64_t k0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < LA; ++q) {
       const int idx = tid + 256 * q;
-      const int r_a = TA ? idx % 64 : idx / 16, k_a = TA ? idx / 64 : idx % 16;
+      const int r_a = TA ? idx % 64 : idx / KC, k_a = TA ? idx / 64 : idx % KC;
       const int64_t ia = i0 + r_a, kA = k0 + k_a;
       ra[q] = (ia < M && kA < M) ? (TA ? A[kA * lda + ia] : A[ia * lda + kA]) : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < LB; ++q) {
       const int idx = tid + 256 * q;
-      const int c_b = TB ? idx / 16 : idx % BN, k_b = TB ? idx % 16 : idx / BN;
+      const int c_b = TB ? idx / KC : idx % BN, k_b = TB ? idx % KC : idx / BN;
       const int64_t jb = j0 + c_b, kB = k0 + k_b;
       rb[q] = (jb < M && kB < M) ? (TB ? B[jb * ldb + kB] : B[kB * ldb + jb]) : 0.0;
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < LA; ++q) {
       const int idx = tid + 256 * q;
-      sa[TA ? idx % 64 : idx / 16][TA ? idx / 64 : idx % 16] = ra[q];
+      sa[TA ? idx % 64 : idx / KC][TA ? idx / 64 : idx % KC] = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < LB; ++q) {
       const int idx = tid + 256 * q;
-      sb[TB ? idx % 16 : idx / BN][TB ? idx / 16 : idx % BN] = rb[q];
+      sb[TB ? idx % KC : idx / BN][TB ? idx / KC : idx % BN] = rb[q];
     }
   };
   if (klo < khi) load(klo);
-  for (int64_t k0 = klo; k0 < khi; k0 += 16) {
+  for (int64_t k0 = klo; k0 < khi; k0 += KC) {
     store();
     __syncthreads();
-    if (k0 + 16 < khi) load(k0 + 16);
+    if (k0 + KC < khi) load(k0 + KC);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < KC / 4; ++ks) {
       double av[2], bv[NB];
 #pragma unroll
       for (int t = 0; t < 2; ++t) av[t] = sa[wi + 16 * t + (lane & 15)][4 * ks + (lane >> 4)];
@@ -1695,6 +1696,7 @@ extern "C" int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT
   if (M == 0) return MGP_OK;
   if (!workspace || workspace_bytes < mgp_chol_backward_workspace_bytes(M)) return MGP_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
+  constexpr int KCB = 32;  // chunk depth of the products (32: half the barriers of 16)
   double* Ld = (double*)workspace;
   double* Li = Ld + M * M;   // Linv = LinvT^T
   double* G = Li + M * M;
@@ -1705,12 +1707,12 @@ extern "C" int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, gL, ldg, G, M, nullptr, (int64_t)0);
   // L, gL, Linv are lower triangular (exact zeros above), so are P and P Linv: the
   // products skip the zero terms and the tiles Phi / the next product never read
-  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M,
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32, KCB>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M,
                      kTriUpperK | kTriLowerOut);                                                      // L^T gL
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 2, nullptr, (int64_t)0, T, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL((dgemm_kernel<false, false, 32>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M,
+  hipLaunchKernelGGL((dgemm_kernel<false, false, 32, KCB>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M,
                      kTriBand | kTriLowerOut);                                                        // P Linv
-  hipLaunchKernelGGL((dgemm_kernel<true, false, 32>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M,
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32, KCB>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M,
                      kTriUpperK);                                                                     // Linv^T (.)
   hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 3, nullptr, (int64_t)0, T, M, gKuu, ldo);
   return launch_status();
