@@ -42,17 +42,22 @@ constexpr int LDT = CB + 2;   // LDS leading dimension (doubles): conflict-free 
 constexpr int kCholThreads = 256;
 constexpr int kMaxBatch = 8;
 
+// Thread index within a 256-thread tile group: the tile helpers below work on one
+// 64x64 tile with 4 waves; chol_step_pair runs two such groups per workgroup (512
+// threads), every other kernel here is one group (threadIdx.x < 256).
+__device__ __forceinline__ int ctid() { return (int)(threadIdx.x & (kCholThreads - 1)); }
+
 #ifdef MGP_DBG_STAMPS
 __device__ unsigned long long g_stamps[64 * 16];
 // persistent path: chain stamps [batch 2][step 128][8]; worker phase totals [batch 2][wg 128][8]
 __device__ unsigned long long g_pchain[2 * 128 * 8];
 __device__ unsigned long long g_pwork[2 * 128 * 8];
-#define PSTAMP(b, j, k) do { if (threadIdx.x == 0 && (b) < 2 && (j) < 128) g_pchain[((b) * 128 + (j)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-#define PWACC(b, w, k, v) do { if (threadIdx.x == 0 && (b) < 2 && (w) < 128) g_pwork[((b) * 128 + (w)) * 8 + (k)] += (v); } while (0)
+#define PSTAMP(b, j, k) do { if (ctid() == 0 && (b) < 2 && (j) < 128) g_pchain[((b) * 128 + (j)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define PWACC(b, w, k, v) do { if (ctid() == 0 && (b) < 2 && (w) < 128) g_pwork[((b) * 128 + (w)) * 8 + (k)] += (v); } while (0)
 #define PNOW() __builtin_amdgcn_s_memtime()
-#define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP(j, k) do { if (ctid() == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 // 100 MHz reference clock (one time base for every CU): slots 14 / 15
-#define RSTAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RSTAMP(j, k) do { if (ctid() == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(j, k) do {} while (0)
 #define RSTAMP(j, k) do {} while (0)
@@ -129,14 +134,14 @@ struct TileRegs {
 __device__ __forceinline__ void tile_fetch(TileRegs& t, const double* __restrict__ g, int64_t ld) {
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
-    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
+    const int idx = ctid() + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
     t.v[it] = *reinterpret_cast<const double2*>(g + (int64_t)r * ld + c);
   }
 }
 __device__ __forceinline__ void tile_put(double* __restrict__ s, const TileRegs& t) {
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
-    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
+    const int idx = ctid() + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
     s[r * LDT + c] = t.v[it].x;
     s[r * LDT + c + 1] = t.v[it].y;
   }
@@ -151,7 +156,7 @@ __device__ __forceinline__ void tile_load(double* __restrict__ s, const double* 
 // guarded to rows < nr, cols < nc of the destination block.
 __device__ __forceinline__ void tile_store_f32(float* __restrict__ g, int64_t ld, const double* __restrict__ s,
                                                bool transpose, int nr, int nc) {
-  for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+  for (int idx = ctid(); idx < CB * CB; idx += kCholThreads) {
     const int r = idx >> 6, c = idx & 63;
     if (r < nr && c < nc) g[(int64_t)r * ld + c] = (float)(transpose ? s[c * LDT + r] : s[r * LDT + c]);
   }
@@ -161,7 +166,7 @@ __device__ __forceinline__ void tile_store_f32(float* __restrict__ g, int64_t ld
 __device__ __forceinline__ float tile_store_f32_max(float* __restrict__ g, int64_t ld, const double* __restrict__ s,
                                                     bool transpose, int nr, int nc) {
   float m = 0.f;
-  for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+  for (int idx = ctid(); idx < CB * CB; idx += kCholThreads) {
     const int r = idx >> 6, c = idx & 63;
     if (r < nr && c < nc) {
       const float v = (float)(transpose ? s[c * LDT + r] : s[r * LDT + c]);
@@ -181,7 +186,7 @@ __device__ __forceinline__ float tile_store_f32_v4(float* __restrict__ g, int64_
   float m = 0.f;
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
-    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 4, c = (idx & 15) * 4;
+    const int idx = ctid() + kCholThreads * it, r = idx >> 4, c = (idx & 15) * 4;
     float v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -198,11 +203,11 @@ __device__ __forceinline__ float tile_store_f32_v4(float* __restrict__ g, int64_
 __device__ __forceinline__ void wave_absmax_atomic(float m, float* out) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
+  if ((ctid() & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
 }
 
 __device__ __forceinline__ void tile_store_f64(double* __restrict__ g, int64_t ld, const double* __restrict__ s) {
-  for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+  for (int idx = ctid(); idx < CB * CB; idx += kCholThreads) {
     const int r = idx >> 6, c = idx & 63;
     g[(int64_t)r * ld + c] = s[r * LDT + c];
   }
@@ -228,7 +233,7 @@ __device__ __forceinline__ Quad quad_zero() {
 template <bool TA, bool TB>
 __device__ __forceinline__ void tile_mma(Quad& q, const double* __restrict__ sa, const double* __restrict__ sb,
                                          double sign) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = ctid() & 63, w = ctid() >> 6;
   const int qi = (w >> 1) * 32, qj = (w & 1) * 32;
   const int l16 = lane & 15, kq = lane >> 4;
 #pragma unroll 4
@@ -251,7 +256,7 @@ __device__ __forceinline__ void tile_mma(Quad& q, const double* __restrict__ sa,
 
 template <typename F>
 __device__ __forceinline__ void quad_foreach(F f) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = ctid() & 63, w = ctid() >> 6;
   const int qi = (w >> 1) * 32, qj = (w & 1) * 32;
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
@@ -288,17 +293,18 @@ __device__ __forceinline__ Blk4 blk4_zero() {
 // Row stripe: C[16w + i][16tj + j] += sign * sum_k A(i, k) B(k, j), A = sa[16w + i][k],
 // B(k, j) = TB ? sb[16tj + j][k] : sb[k][16tj + j].  TRI = 0: every k; TRI = 1:
 // k < 16 (tj + 1) (B = D^T, D lower triangular: 40 of 64 MFMAs); TRI = 2:
-// k >= 16 tj (B = D, lower triangular).
-template <bool TB, int TRI>
+// k >= 16 tj (B = D, lower triangular).  BLK: the column blocks tj formed (bit tj).
+template <bool TB, int TRI, int BLK = 0xF>
 __device__ __forceinline__ void row_mma(Blk4& r, const double* __restrict__ sa, const double* __restrict__ sb,
                                         double sign) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+  const int lane = ctid() & 63, w = ctid() >> 6, l16 = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int k0 = 0; k0 < CB; k0 += 4) {
     const int k = k0 + kq;
     const double av = sign * sa[(16 * w + l16) * LDT + k];
 #pragma unroll
     for (int tj = 0; tj < 4; ++tj) {
+      if (!((BLK >> tj) & 1)) continue;
       if (TRI == 1 && k0 >= 16 * (tj + 1)) continue;
       if (TRI == 2 && k0 < 16 * tj) continue;
       const double bv = TB ? sb[(16 * tj + l16) * LDT + k] : sb[k * LDT + 16 * tj + l16];
@@ -310,7 +316,7 @@ __device__ __forceinline__ void row_mma(Blk4& r, const double* __restrict__ sa, 
 // Column stripe: C[16ti + i][16w + j] += sum_k D[16ti + i][k] sb[k][16w + j] with
 // D lower triangular (k < 16 (ti + 1)): X_jc = D_j B_jc.
 __device__ __forceinline__ void col_mma_lower(Blk4& r, const double* __restrict__ sD, const double* __restrict__ sb) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, kq = lane >> 4;
+  const int lane = ctid() & 63, w = ctid() >> 6, l16 = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int k0 = 0; k0 < CB; k0 += 4) {
     const int k = k0 + kq;
@@ -324,21 +330,23 @@ __device__ __forceinline__ void col_mma_lower(Blk4& r, const double* __restrict_
   }
 }
 
-template <bool ROW, typename F>
+template <bool ROW, typename F, int BLK = 0xF>
 __device__ __forceinline__ void blk4_foreach(F f) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = ctid() & 63, w = ctid() >> 6;
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      if (!((BLK >> t) & 1)) continue;
       const int rr = (lane >> 4) + 4 * q, cc = lane & 15;
       if (ROW) f(t, q, 16 * w + rr, 16 * t + cc);
       else f(t, q, 16 * t + rr, 16 * w + cc);
     }
 }
-template <bool ROW>
+template <bool ROW, int BLK = 0xF>
 __device__ __forceinline__ void blk4_to_lds(double* __restrict__ s, const Blk4& r) {
-  blk4_foreach<ROW>([&](int t, int q, int row, int col) { s[row * LDT + col] = r.c[t][q]; });
+  auto put = [&](int t, int q, int row, int col) { s[row * LDT + col] = r.c[t][q]; };
+  blk4_foreach<ROW, decltype(put), BLK>(put);
 }
 __device__ __forceinline__ void row_from_global(Blk4& r, const double* __restrict__ g, int64_t ld) {
   blk4_foreach<true>([&](int t, int q, int row, int col) { r.c[t][q] = g[(int64_t)row * ld + col]; });
@@ -387,7 +395,7 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 template <bool TB>
 __device__ __forceinline__ void blk_mma(doublex4& acc, const double* __restrict__ sa,
                                         const double* __restrict__ sb, double sign) {
-  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+  const int lane = ctid() & 63, i = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int k0 = 0; k0 < 16; k0 += 4) {
     const double av = sign * sa[i * LDT + k0 + kq];
@@ -397,7 +405,7 @@ __device__ __forceinline__ void blk_mma(doublex4& acc, const double* __restrict_
 }
 
 __device__ __forceinline__ doublex4 blk_load(const double* __restrict__ s) {
-  const int lane = threadIdx.x & 63;
+  const int lane = ctid() & 63;
   doublex4 v;
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = s[((lane >> 4) + 4 * r) * LDT + (lane & 15)];
@@ -405,7 +413,7 @@ __device__ __forceinline__ doublex4 blk_load(const double* __restrict__ s) {
 }
 
 __device__ __forceinline__ void blk_store(double* __restrict__ s, const doublex4& v) {
-  const int lane = threadIdx.x & 63;
+  const int lane = ctid() & 63;
 #pragma unroll
   for (int r = 0; r < 4; ++r) s[((lane >> 4) + 4 * r) * LDT + (lane & 15)] = v[r];
 }
@@ -413,13 +421,13 @@ __device__ __forceinline__ void blk_store(double* __restrict__ s, const doublex4
 // Lower 16x16 blocks (bi >= bj) of the diagonal tile s -= P P^T, in place in LDS;
 // the 10 blocks dealt 3/3/2/2 over the waves (48 MFMAs at most per wave).
 __device__ __forceinline__ void diag_lower_update(double* __restrict__ s, const double* __restrict__ sP) {
-  const int w = threadIdx.x >> 6;
+  const int w = ctid() >> 6;
   for (int q = w; q < 10; q += 4) {
     int bi = 0;
     while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
     const int bj = q - bi * (bi + 1) / 2;
     doublex4 acc = blk_load(s + 16 * bi * LDT + 16 * bj);
-    const int lane = threadIdx.x & 63, l16 = lane & 15, kq = lane >> 4;
+    const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
 #pragma unroll
     for (int k0 = 0; k0 < CB; k0 += 4) {
       const double av = -sP[(16 * bi + l16) * LDT + k0 + kq];
@@ -586,7 +594,7 @@ __device__ __forceinline__ doublex4 neg_x_times(const double* __restrict__ Xii, 
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0,
                                                  const double* sPend = nullptr) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = ctid() >> 6, lane = ctid() & 63;
   int bad = 0;
   const int js = (int)(gcol0 / CB) - 1;
   if (w == 0) {
@@ -707,7 +715,7 @@ __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, cons
     if (nr == CB) {
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
-        const int idx = threadIdx.x + kCholThreads * it, r = idx >> 4, c = (idx & 15) * 4;
+        const int idx = ctid() + kCholThreads * it, r = idx >> 4, c = (idx & 15) * 4;
         const double* sr = sF + r * LDT + c;
         *reinterpret_cast<float4*>(g + (int64_t)r * a.ldl + c) =
             make_float4((float)sr[0], (float)sr[1], (float)sr[2], (float)sr[3]);
@@ -719,7 +727,7 @@ __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, cons
   double* d = ws_D(a, b, j);
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
-    const int idx = threadIdx.x + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
+    const int idx = ctid() + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
     *reinterpret_cast<double2*>(d + r * CB + c) = make_double2(sX[r * LDT + c], sX[r * LDT + c + 1]);
   }
 }
@@ -804,14 +812,14 @@ __device__ __forceinline__ void prep_persist_state(const CholArgs& a, int b) {
   const int nb = a.nb;
   int* s = a.sync + (int64_t)b * a.strideSync;
   const int64_t nw = chol_sync_words(nb), d0 = (int64_t)2 * nb * nb;
-  for (int64_t w = (int64_t)blockIdx.x * kCholThreads + threadIdx.x; w < nw; w += (int64_t)gridDim.x * kCholThreads)
+  for (int64_t w = (int64_t)blockIdx.x * kCholThreads + ctid(); w < nw; w += (int64_t)gridDim.x * kCholThreads)
     s[w] = (w == d0) ? 1 : 0;
   const int q = blockIdx.x;
   if (b != 0 || q >= task_block_count(nb)) return;
   int start = 0;
   for (int r = 0; r < q; ++r) start += task_block_size(r, nb);
   const int n = task_block_size(q, nb);
-  for (int e = threadIdx.x; e < n; e += kCholThreads) a.tasks[start + e] = task_entry(q, e, nb);
+  for (int e = ctid(); e < n; e += kCholThreads) a.tasks[start + e] = task_entry(q, e, nb);
 }
 
 // ------------------------------------------------------------------ prep launch
@@ -875,6 +883,25 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
 }
 
 // ------------------------------------------------------------------ step launch j
+// The look-ahead's factorisation of tile (j+1, j+1): s1 holds P = L_{j+1,j}, s2 the
+// tile with column block 0 of -P P^T still to apply.
+__device__ __forceinline__ void lookahead_factor(const CholArgs& a, int b, int j, double* s1, double* s2,
+                                                 double* col) {
+  // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
+  // lower blocks are applied beside the first panel sweep
+  sub_outer_blk<4>(s2, 16 * (threadIdx.x >> 6), 0, s1, s1);
+  __syncthreads();
+  STAMP(j, 3);
+  STAMP(j, 4);
+  factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1);
+  STAMP(j, 6);
+  __syncthreads();
+  write_diag(a, b, j + 1, s2, s1);
+  __syncthreads();
+  STAMP(j, 7);
+  RSTAMP(j, 15);
+}
+
 __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
   __shared__ double s1[CB * LDT], s2[CB * LDT], sD[CB * LDT], col[CB];
   const int b = blockIdx.y;
@@ -953,19 +980,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
       return;
     }
     if (la) {  // look-ahead: factor the next diagonal tile
-      // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
-      // lower blocks are applied beside the first panel sweep
-      sub_outer_blk<4>(s2, 16 * (threadIdx.x >> 6), 0, s1, s1);
-      __syncthreads();
-      STAMP(j, 3);
-      STAMP(j, 4);
-      factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1);
-      STAMP(j, 6);
-      __syncthreads();
-      write_diag(a, b, j + 1, s2, s1);
-      __syncthreads();
-      STAMP(j, 7);
-      RSTAMP(j, 15);
+      lookahead_factor(a, b, j, s1, s2, col);
     } else {
       // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T in place in LDS (s2)
       diag_lower_update(s2, s1);
@@ -1010,6 +1025,148 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
     row_mma<false, 2>(u, s1, sD, -1.0);
   }
   row_to_global(Bt(i, c), Mp, u);
+}
+
+// ------------------------------------------------------------------ step launch j, tile pairs
+// chol_step with the trailing-update and forward-substitution tiles of step j taken two
+// at a time along a tile row i, one 256-thread group per tile in a 512-thread
+// workgroup (workgroup 0 is the look-ahead, on its first group).  chol_step's tile
+// workgroups each form P_i = W_ij D_j^T for themselves and run their three products
+// with one wave per SIMD; here the pair loads W_ij and D_j once, each group forms half
+// of P_i's column blocks and then its tile's own first product (P_l or X_jc), and the
+// two groups' MFMAs share every SIMD (two waves each), so a step's tiles take half the
+// workgroups for about the time of one.  Per tile the products are chol_step's, on the same
+// operands in the same order: L and L^-T are bit-identical.
+// Row i's tiles in order: the update tiles (i, l), l = j + 1 .. i (rows i > j + 1;
+// l = i is the diagonal tile), then the forward-substitution tiles (i, c), c = 0 .. j.
+constexpr int kPairThreads = 2 * kCholThreads;
+__host__ __device__ inline int step_row_tiles(int i, int j) { return i == j + 1 ? j + 1 : i + 1; }
+__host__ __device__ inline int step_pair_count(int nb, int j) {
+  int n = 0;
+  for (int i = j + 1; i < nb; ++i) n += (step_row_tiles(i, j) + 1) / 2;
+  return n;
+}
+
+__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j) {
+  __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB];
+  const int b = blockIdx.y;
+  const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));  // tile group
+  double* W = ws_W(a, b);
+  double* Bm = ws_B(a, b);
+  float* LinvT = a.LinvT + (int64_t)b * a.strideL;
+  const int64_t Mp = a.Mp;
+  auto Wt = [&](int bi, int bl) { return W + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
+  auto Bt = [&](int bi, int bl) { return Bm + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
+  float* lt_max = a.lt_absmax[0];
+#pragma unroll
+  for (int q = 1; q < kMaxBatch; ++q)
+    if (b == q) lt_max = a.lt_absmax[q];
+  auto store_linvT = [&](int c, const double* sx) {  // X_jc -> LinvT block (c, j)
+    const int64_t gr = (int64_t)c * CB, gc = (int64_t)j * CB;
+    const float m = tile_store_f32_max(LinvT + gr * a.ldl + gc, a.ldl, sx, true, (int)min<int64_t>(CB, a.M - gr),
+                                       (int)min<int64_t>(CB, a.M - gc));
+    if (lt_max) wave_absmax_atomic(m, lt_max);
+  };
+  int i = j + 1;
+  if (blockIdx.x == 0) {  // look-ahead: tile (j+1, j+1), group 0 (group 1's waves end here:
+    if (g != 0) return;   // a barrier waits only for the waves that have not terminated)
+    RSTAMP(j, 14);
+    STAMP(j, 0);
+    TileRegs r1, rD, r2;
+    tile_fetch(r1, Wt(i, j), Mp);
+    tile_fetch(rD, ws_D(a, b, j), CB);
+    tile_fetch(r2, Wt(i, i), Mp);
+    tile_put(s1, r1);
+    tile_put(sD, rD);
+    tile_put(s2[0], r2);
+    __syncthreads();
+    STAMP(j, 1);
+    Blk4 pi = blk4_zero();
+    row_mma<true, 1>(pi, s1, sD, 1.0);
+    __syncthreads();
+    blk4_to_lds<true>(s1, pi);
+    __syncthreads();
+    STAMP(j, 2);
+    lookahead_factor(a, b, j, s1, s2[0], col);
+    return;
+  }
+  // pair -> (row i, tile e of the row)
+  int q = blockIdx.x - 1, nt = 0;
+  for (; i < a.nb; ++i) {
+    nt = step_row_tiles(i, j);
+    const int np = (nt + 1) / 2;
+    if (q < np) break;
+    q -= np;
+  }
+  const int e = 2 * q + g;
+  const bool has = e < nt;  // an odd row's last pair: group 1 has no tile (it forms its half of P_i)
+  const int nupd = (i == j + 1) ? 0 : i - j;
+  const bool upd = has && e < nupd;
+  const int l = j + 1 + e, c = e - nupd;
+  const bool fwd = has && !upd && c < j;  // forward-substitution tile reading B_jc
+  const bool first = (upd && l != i) || fwd;  // P_l / X_jc before the update
+  double* sT = s2[g];
+  // this tile's operands: sT's tile (when it reads one) and the updated tile (u)
+  TileRegs r1, rD, r2;
+  Blk4 u = blk4_zero();  // B_ij is zero before step j
+  if (g == 0) {
+    tile_fetch(r1, Wt(i, j), Mp);
+    tile_fetch(rD, ws_D(a, b, j), CB);
+  }
+  if (upd) {
+    if (l != i) {
+      tile_fetch(r2, Wt(l, j), Mp);
+      row_from_global(u, Wt(i, l), Mp);
+    } else {
+      tile_fetch(r2, Wt(i, i), Mp);
+    }
+  } else if (fwd) {
+    tile_fetch(r2, Bt(j, c), Mp);
+    row_from_global(u, Bt(i, c), Mp);
+  }
+  if (g == 0) {
+    tile_put(s1, r1);
+    tile_put(sD, rD);
+  }
+  if (upd || fwd) tile_put(sT, r2);
+  __syncthreads();
+  // P_i's column blocks split over the groups with equal MFMA counts (D_j^T upper:
+  // block tj takes 4 (tj + 1) k-steps): group 0 blocks 0 and 3, group 1 blocks 1 and 2;
+  // each group then forms its tile's own first product
+  Blk4 pi = blk4_zero(), t = blk4_zero();
+  if (g == 0) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);  // P_i = W_ij D_j^T = L_ij
+  else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
+  if (first) {
+    if (upd) row_mma<true, 1>(t, sT, sD, 1.0);   // P_l = W_lj D_j^T
+    else col_mma_lower(t, sD, sT);               // X_jc = D_j B_jc
+  }
+  __syncthreads();
+  if (g == 0) blk4_to_lds<true, 0x9>(s1, pi);
+  else blk4_to_lds<true, 0x6>(s1, pi);
+  if (first) upd ? blk4_to_lds<true>(sT, t) : blk4_to_lds<false>(sT, t);
+  __syncthreads();
+  if (g == 0 && q == 0 && a.L) {  // L_ij, once per row
+    const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
+    tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
+                   (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
+  }
+  if (!has) return;
+  if (upd && l != i) {
+    row_mma<true, 0>(u, s1, sT, -1.0);    // W_il -= P_i P_l^T
+    row_to_global(Wt(i, l), Mp, u);
+  } else if (upd) {                        // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T
+    diag_lower_update(sT, s1);
+    __syncthreads();
+    tile_store_f64(Wt(i, i), Mp, sT);
+  } else if (fwd) {
+    if (i == j + 1) store_linvT(c, sT);
+    row_mma<false, 0>(u, s1, sT, -1.0);    // B_ic -= P_i X_jc
+    row_to_global(Bt(i, c), Mp, u);
+  } else {                                 // X_jj = D_j (lower triangular)
+    if (i == j + 1) store_linvT(c, sD);
+    row_mma<false, 2>(u, s1, sD, -1.0);
+    row_to_global(Bt(i, c), Mp, u);
+  }
 }
 
 // ------------------------------------------------------------------ persistent launch
@@ -1555,6 +1712,13 @@ static int chol_persist_workers(int nb) {
   return std::min(48, std::max(2, 2 * nb));
 }
 
+// Per-step launches on tile pairs (chol_step_pair, default) or one tile per workgroup
+// (chol_step, MGP_CHOL_PAIR=0; read per call).
+static bool chol_pair_enabled() {
+  const char* e = getenv("MGP_CHOL_PAIR");
+  return e ? atoi(e) != 0 : true;
+}
+
 static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s,
                     hipEvent_t prep_done = nullptr) {
   if (!workspace || workspace_bytes < mgp_chol_workspace_bytes(a.M, batch)) return MGP_ERR_WORKSPACE;
@@ -1585,8 +1749,15 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
     hipLaunchKernelGGL(chol_persist, dim3(1 + chol_persist_workers(a.nb), batch), block, 0, s, a);
     return launch_status();
   }
+  const bool pair = chol_pair_enabled();
   for (int j = 0; j < a.nb; ++j) {
     const int T = a.nb - j - 1;
+    if (pair && T > 0) {
+      hipLaunchKernelGGL(chol_step_pair, dim3(1 + step_pair_count(a.nb, j), batch), dim3(kPairThreads), 0, s, a, j);
+      st = launch_status();
+      if (st) return st;
+      continue;
+    }
     const int n = (T == 0) ? a.nb : T * (T + 1) / 2 + T * (j + 1);
     hipLaunchKernelGGL(chol_step, dim3(n, batch), block, 0, s, a, j);
     st = launch_status();

@@ -38,11 +38,14 @@ def test_rbf_kuf_kuu(device, N, M, D, ard):
     assert np.array_equal(Kuu, Kuu.T)
 
 
-@pytest.fixture(params=["steps", "persist"])
+@pytest.fixture(params=["steps", "tiles", "persist"])
 def chol_path(request, monkeypatch):
-    """K3's two launch structures: one launch per panel step (default) and the single
-    persistent launch (chol_persist, MGP_CHOL_PERSIST=1; the library reads it per call)."""
+    """K3's launch structures: one launch per panel step with two tiles per workgroup
+    (default, chol_step_pair), the same with one tile per workgroup (chol_step,
+    MGP_CHOL_PAIR=0), and the single persistent launch (chol_persist, MGP_CHOL_PERSIST=1);
+    the library reads both switches per call."""
     monkeypatch.setenv("MGP_CHOL_PERSIST", "1" if request.param == "persist" else "0")
+    monkeypatch.setenv("MGP_CHOL_PAIR", "0" if request.param == "tiles" else "1")
     return request.param
 
 

@@ -1,6 +1,7 @@
-"""K3 variants in one process (interleaved rounds): the per-step launches against the
-persistent launch at several worker counts, c3 shapes (two layers, M = 1024), plus a
-float64 check of the persistent result.  Usage: python tools/chol_probe.py"""
+"""K3 variants in one process (interleaved rounds): the per-step launches with one tile
+per workgroup (chol_step, MGP_CHOL_PAIR=0), with two tiles of a row per 512-thread
+workgroup (chol_step_pair, the default) and the persistent launch, c3 shapes (two layers, M = 1024), plus the
+largest difference of each variant's L / L^-T to the first.  Usage: python tools/chol_probe.py"""
 import json
 import os
 import sys
@@ -18,15 +19,16 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     Z = torch.randn(M, 8, device=dev, generator=g)
     var, ls = torch.tensor([0.5], device=dev), torch.tensor([1.0], device=dev)
-    variants = [("steps", {"MGP_CHOL_PERSIST": "0"})] + [
-        (f"persist_w{w}", {"MGP_CHOL_PERSIST": "1", "MGP_CHOL_WORKERS": str(w)}) for w in (16, 24, 32, 48, 64, 96)]
+    variants = [("tiles", {"MGP_CHOL_PERSIST": "0", "MGP_CHOL_PAIR": "0"}),
+                ("pairs", {"MGP_CHOL_PERSIST": "0", "MGP_CHOL_PAIR": "1"}),
+                ("persist_w48", {"MGP_CHOL_PERSIST": "1", "MGP_CHOL_WORKERS": "48"})]
     outs = {}
     for name, env in variants:
         os.environ.update(env)
         L, LinvT, info = ops.kuu_potrf_trtri([Z, Z], [var, var], [ls, ls], 1e-6, want_L=True)
         torch.cuda.synchronize()
         outs[name] = (L.clone(), LinvT.clone(), info.clone())
-    ref = outs["steps"]
+    ref = outs["tiles"]
     check = {n: {"info": o[2].tolist(), "dL": float((o[0] - ref[0]).abs().max()),
                  "dLinvT": float((o[1] - ref[1]).abs().max())} for n, o in outs.items()}
     print(json.dumps({"check": check}), flush=True)
