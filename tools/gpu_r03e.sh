@@ -9,4 +9,5 @@ tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 tail -c 400 gpurun_out/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
+timeout -k 10 60 tools/f64_mfma_probe > gpurun_out/f64_mfma_probe.log 2>&1 && cat gpurun_out/f64_mfma_probe.log
 echo round-ok
