@@ -178,6 +178,12 @@ static bool k4_shape16() {
   const char* e = getenv("MGP_K4_SHAPE");
   return !(e && atoi(e) == 32);
 }
+// K4 (16x16x32) epilogue: split each accumulator once for both the A image and the
+// stats products (default), or once per use (MGP_K4_SPLIT_ONCE=0); same bits either way.
+static bool k4_split_once() {
+  const char* e = getenv("MGP_K4_SPLIT_ONCE");
+  return !(e && atoi(e) == 0);
+}
 
 // Item b -> (row tile t heavy-first, column tile tn, expert k); the K experts of
 // a column tile are 8 block ids apart (one XCD) when nTn % 8 == 0.
@@ -475,6 +481,7 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
 // in LDS (double buffered, one barrier per pair), the wave's B fragments go global ->
 // registers one pair ahead; 96 MFMAs per wave and pair.
 typedef float floatx4v __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ floatx4v mfma16_f16(bf16x8 a, bf16x8 b, floatx4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c,
                                                 0, 0, 0);
@@ -1764,7 +1771,7 @@ __device__ __forceinline__ void store_acc16_f32(const floatx4v (&acc)[8][4], flo
   }
 }
 
-template <int KMAX>
+template <int KMAX, bool ONCE>
 __device__ __forceinline__ void trsm_stats16_item(
     bf16x8 (*sL)[4 * 2 * 3 * 64], float* __restrict__ sQ, int t, int tn, const bf16x8* __restrict__ Tfr,
     uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
@@ -1806,22 +1813,24 @@ __device__ __forceinline__ void trsm_stats16_item(
   // A's image: fragment (column block 8 tn + 2 w + c, k-step 8 t + ib), lane position pos
   const bool lo_half = lane < 32;
   const int pos = lo_half ? li + 32 * q : 16 + li + 32 * (q - 2);
+  if (!stats || !ONCE) {
 #pragma unroll
-  for (int ib = 0; ib < 8; ++ib)
+    for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const floatx4v send = lo_half ? acc[ib][2 * c + 1] : acc[ib][2 * c];
-      float y[4], v[8];
+      for (int c = 0; c < 2; ++c) {
+        const floatx4v send = lo_half ? acc[ib][2 * c + 1] : acc[ib][2 * c];
+        float y[4], v[8];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(send[r], 32, 64);
+        for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(send[r], 32, 64);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = lo_half ? acc[ib][2 * c][r] : y[r];
-        v[4 + r] = lo_half ? y[r] : acc[ib][2 * c + 1][r];
+        for (int r = 0; r < 4; ++r) {
+          v[r] = lo_half ? acc[ib][2 * c][r] : y[r];
+          v[4 + r] = lo_half ? y[r] : acc[ib][2 * c + 1][r];
+        }
+        store_split_f16(Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, a_scale);
       }
-      store_split_f16(Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, a_scale);
-    }
-  if (!stats) return;
+    if (!stats) return;
+    // (ONCE = false: the stats products split the accumulators a second time)
   const int qe = img_exp(__uint_as_float(reinterpret_cast<const unsigned int*>(sQ)[128 * KMAX]));
   const float q_scale = ldexpf(1.f, qe), s_unscale = ldexpf(1.f, -(qe + img_exp(sqrtf(*a_var))));
 #pragma unroll
@@ -1885,10 +1894,109 @@ __device__ __forceinline__ void trsm_stats16_item(
       }
     }
   }
+    return;
+  }
+  // With the stats: every accumulator value is split once (x = a 2^e -> f16 hi, f16 lo,
+  // packed two per dword) and both the image fragments and the stats products' B
+  // operand are assembled from the packed halves (the image's lane-half exchange moves
+  // packed halves); row-block pairs (ib0, ib0 + 1) = 64-row stats tile ib0 / 4.
+  const int qe = img_exp(__uint_as_float(reinterpret_cast<const unsigned int*>(sQ)[128 * KMAX]));
+  const float q_scale = ldexpf(1.f, qe), s_unscale = ldexpf(1.f, -(qe + img_exp(sqrtf(*a_var))));
+  floatx4v sq[4];
+  float a2[4];
+#pragma unroll
+  for (int pr4 = 0; pr4 < 4; ++pr4) {  // row blocks ib0 = 2 pr4, ib0 + 1
+    const int ib0 = 2 * pr4, st2 = pr4 >> 1;
+    if ((pr4 & 1) == 0) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        sq[cb] = floatx4v{0.f, 0.f, 0.f, 0.f};
+        a2[cb] = 0.f;
+      }
+    }
+    uint32_t hp[2][4][2], lp[2][4][2];  // [row block of the pair][column block][dword]
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const float a0 = acc[ib0 + d][cb][2 * h2], a1 = acc[ib0 + d][cb][2 * h2 + 1];
+          a2[cb] = fmaf(a1, a1, fmaf(a0, a0, a2[cb]));
+          const float x0 = a0 * a_scale, x1 = a1 * a_scale;
+          const _Float16 h0 = (_Float16)x0, h1 = (_Float16)x1;
+          const halfx2 hh = {h0, h1}, ll = {(_Float16)(x0 - (float)h0), (_Float16)(x1 - (float)h1)};
+          hp[d][cb][h2] = __builtin_bit_cast(uint32_t, hh);
+          lp[d][cb][h2] = __builtin_bit_cast(uint32_t, ll);
+        }
+    // the image fragments of row blocks ib0, ib0 + 1
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int cs = lo_half ? 2 * c + 1 : 2 * c, co = lo_half ? 2 * c : 2 * c + 1;
+        uint32_t yh[2], yl[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          yh[h2] = (uint32_t)__shfl_xor((int)hp[d][cs][h2], 32, 64);
+          yl[h2] = (uint32_t)__shfl_xor((int)lp[d][cs][h2], 32, 64);
+        }
+        const u32x4v fh = lo_half ? u32x4v{hp[d][co][0], hp[d][co][1], yh[0], yh[1]}
+                                  : u32x4v{yh[0], yh[1], hp[d][co][0], hp[d][co][1]};
+        const u32x4v fl = lo_half ? u32x4v{lp[d][co][0], lp[d][co][1], yl[0], yl[1]}
+                                  : u32x4v{yl[0], yl[1], lp[d][co][0], lp[d][co][1]};
+        bf16x8* dst = Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib0 + d) * 3) * 64 + pos;
+        dst[0] = __builtin_bit_cast(bf16x8, fh);
+        dst[64] = __builtin_bit_cast(bf16x8, fl);
+      }
+    // q_mu^T A of this row-block pair: B operand slot j = row 4q + j of block ib0 (j < 4),
+    // row 4q + j - 4 of block ib0 + 1
+    bf16x8 qf[3];
+    {
+      halfx8 qh, ql;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = 16 * ib0 + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4);
+        const float x = (li < K ? sQ[row * KMAX + (li < KMAX ? li : 0)] : 0.f) * q_scale;
+        const _Float16 xh = (_Float16)x;
+        qh[j] = xh;
+        ql[j] = (_Float16)(x - (float)xh);
+      }
+      qf[0] = __builtin_bit_cast(bf16x8, qh);
+      qf[1] = __builtin_bit_cast(bf16x8, ql);
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const bf16x8 bf[3] = {__builtin_bit_cast(bf16x8, u32x4v{hp[0][cb][0], hp[0][cb][1], hp[1][cb][0], hp[1][cb][1]}),
+                            __builtin_bit_cast(bf16x8, u32x4v{lp[0][cb][0], lp[0][cb][1], lp[1][cb][0], lp[1][cb][1]}),
+                            bf16x8{}};
+      sq[cb] = mfma16_fmt<2, true>(qf, bf, sq[cb]);
+    }
+    if ((pr4 & 1) == 1) {  // 64-row stats tile 2 t + st2 done
+      const int64_t st = 2 * (int64_t)t + st2;
+      if (64 * st < M) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int64_t n = (int64_t)tn * kX6BN + 64 * w + 16 * cb + li;
+          float s_a2 = a2[cb] + __shfl_xor(a2[cb], 16, 64);
+          s_a2 += __shfl_xor(s_a2, 32, 64);
+          if (n < N) {
+            float* dst = stats + st * (K + 1) * lds_ + n;
+            if (lane < 16) dst[0] = s_a2;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int kk = 4 * q + e;
+              if (kk < K) dst[(int64_t)(1 + kk) * lds_] = sq[cb][e] * s_unscale;
+            }
+          }
+        }
+      }
+    }
+  }
 }
 
 // Row-tile pairs as trsm_stats_x6_kernel (equal work per workgroup).
-template <int KMAX>
+template <int KMAX, bool ONCE = true>
 __global__ __launch_bounds__(256, 2) void trsm_stats16_kernel(
     const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
     int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
@@ -1903,13 +2011,13 @@ __global__ __launch_bounds__(256, 2) void trsm_stats16_kernel(
   col_major_item(blockIdx.x, nP, nTn, p, tn);
   if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
   __syncthreads();
-  trsm_stats16_item<KMAX>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
+  trsm_stats16_item<KMAX, ONCE>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
                           lds_, Af32, lda, a_var, t_bound, k_bound);
   if (nT - 1 - p == p) return;
   __syncthreads();
   if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
   __syncthreads();
-  trsm_stats16_item<KMAX>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats, lds_,
+  trsm_stats16_item<KMAX, ONCE>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats, lds_,
                           Af32, lda, a_var, t_bound, k_bound);
 }
 
@@ -2106,8 +2214,12 @@ static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb
       hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                          (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
                          (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
+    else if (k4_shape16() && k4_split_once())
+      hipLaunchKernelGGL((trsm_stats16_kernel<KMAX, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr, (uint32_t)tb,
+                         (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K, (bf16x8*)Afr, stats, lds, A,
+                         lda, a_var, a_bound, t_bound, k_bound);
     else if (k4_shape16())
-      hipLaunchKernelGGL((trsm_stats16_kernel<KMAX>), grid, dim3(256), 0, s, (const bf16x8*)Tfr, (uint32_t)tb,
+      hipLaunchKernelGGL((trsm_stats16_kernel<KMAX, false>), grid, dim3(256), 0, s, (const bf16x8*)Tfr, (uint32_t)tb,
                          (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K, (bf16x8*)Afr, stats, lds, A,
                          lda, a_var, a_bound, t_bound, k_bound);
     else
