@@ -490,9 +490,10 @@ def main():
                       if f16 else {3: "f32 (split-bf16 x6, f32-exact operands)", 2: "f32/bf16x3 mixed",
                                    1: "f32/bf16 mixed"}[args.planes]) if x6 else "f32",
             "data": "synthetic",
-            "dtype_note": (("f32 operands and accumulation; K1/K4 products on bf16 MFMA via an exact 3-plane "
-                            "split (6 products) in training; the forward chain K1 -> K4 -> K5 on f16 MFMA via "
-                            "power-of-two-scaled 2-plane fp16 splits (22-bit operands, 3 products); K3 in f64")
+            "dtype_note": (("f32 operands and accumulation; the forward chain K1 -> K4 -> K5 on f16 MFMA via "
+                            "power-of-two-scaled 2-plane fp16 splits (22-bit operands, 3 products), in the ELBO "
+                            "and the training step alike; the training backward's g_Lm gram (g_Kuf A^T) and its "
+                            "M x M products on bf16 MFMA via an exact 3-plane split (6 products); K3 in f64")
                            + ("; K5's two cross terms (2^-11 of the leading product) on the e4m3 MFMA"
                               if f16x8 else "")
                            if f16 else
