@@ -1037,6 +1037,10 @@ __global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
 // two groups' MFMAs share every SIMD (two waves each), so a step's tiles take half the
 // workgroups for about the time of one.  Per tile the products are chol_step's, on the same
 // operands in the same order: L and L^-T are bit-identical.
+// After P_i the groups take their tiles' own paths: a __syncthreads on one path waits
+// for the live waves of both groups wherever they are, so it still orders that group's
+// own LDS hand-off (and a group that has ended is not waited for: a barrier counts only
+// the waves that have not terminated).
 // Row i's tiles in order: the update tiles (i, l), l = j + 1 .. i (rows i > j + 1;
 // l = i is the diagonal tile), then the forward-substitution tiles (i, c), c = 0 .. j.
 constexpr int kPairThreads = 2 * kCholThreads;
