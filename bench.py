@@ -445,13 +445,10 @@ def main():
             kernels[name] = {"avg_us": st[name][0] * 1e3}
 
     ek = kernels.get("expert_cond", {})
-    shape32 = os.environ.get("MGP_K5_SHAPE") == "32"
-    kname = (("expert_cond_f16x8_kernel" if f16x8 else
-              ("expert_cond_f16_kernel" if shape32 else "expert_cond16_kernel")) if f16 else
+    kname = (("expert_cond_f16x8_kernel" if f16x8 else "expert_cond16_kernel") if f16 else
              "expert_cond_x6_kernel") if x6 else "expert_cond_kernel"
     traffic, traffic_src = load_traffic(kname)
-    klabel = {"expert_cond_f16_kernel": "expert_cond_x6_kernel<2, true, false> (split-f16, 32x32x16 MFMA)",
-              "expert_cond16_kernel": "expert_cond16_kernel<false> (split-f16, 16x16x32 MFMA)",
+    klabel = {"expert_cond16_kernel": "expert_cond16_kernel<false> (split-f16, 16x16x32 MFMA)",
               "expert_cond_f16x8_kernel": "expert_cond_x6_kernel<2, true, true> (split-f16 + e4m3 cross terms)"
               }.get(kname, kname)
     roofline = {"kernel": f"{klabel} (K5, L_k^T A + sum of squares, + cond_finalize)", "bound": "mfma",

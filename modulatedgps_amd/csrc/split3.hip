@@ -166,25 +166,6 @@ __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t vof
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-// The 16x16x32-MFMA K5 (expert_cond16_kernel, forward and training) unless
-// MGP_K5_SHAPE=32 (read per call).  c3, one launch: 1.196 vs 1.322 ms for the 32x32x16
-// kernel, same operands and MFMA cycles (tools/k5_probe.py, profiles/r03_k5_shape.json).
-static bool k5_shape16() {
-  const char* e = getenv("MGP_K5_SHAPE");
-  return !(e && atoi(e) == 32);
-}
-// K4 (split-f16 in and out, f16 cross terms) likewise: trsm_stats16_kernel unless MGP_K4_SHAPE=32
-static bool k4_shape16() {
-  const char* e = getenv("MGP_K4_SHAPE");
-  return !(e && atoi(e) == 32);
-}
-// K4 (16x16x32) epilogue: split each accumulator once for both the A image and the
-// stats products (default), or once per use (MGP_K4_SPLIT_ONCE=0); same bits either way.
-static bool k4_split_once() {
-  const char* e = getenv("MGP_K4_SPLIT_ONCE");
-  return !(e && atoi(e) == 0);
-}
-
 // Item b -> (row tile t heavy-first, column tile tn, expert k); the K experts of
 // a column tile are 8 block ids apart (one XCD) when nTn % 8 == 0.
 // TN_OUTER (K5 writing the C_k images, training): per XCD, one column tile at a
@@ -408,23 +389,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const void* p, uint32
 // ------------------------------------------------------------------ K5 (x6)
 // F16: split-f16 images (NPL = 2) scaled by 2^img_exp(*a_bound), 2^img_exp(*l_bound).
 // X8: their hi planes on f16 MFMA and cross terms on e4m3 MFMA (mfma_f8x).
-// COUT (training, split-f16): C_k = L_k^T A itself is also written, as a split-f16
-// B-layout image per expert (Cfr + k cexp, scale 2^img_exp(bound), bound =
-// *colmax *a_bound (1 + 2^-10) >= |C|: |C[m'][n]| <= ||L_k[:, m']|| ||A[:, n]|| and
-// ||A[:, n]||^2 <= variance), for the backward's gA = 2 sum_k L_k (C_k diag(Gv_k)).
-template <int NPL, bool F16 = false, bool X8 = false, bool COUT = false>
+template <int NPL, bool F16 = false, bool X8 = false>
 __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __restrict__ Afr,
                                                                 const bf16x8* __restrict__ Lfr,
                                                                 uint32_t afr_bytes, uint32_t lfr_bytes,
                                                                 int nmk, int nmb, int nTn, int K,
                                                                 int64_t N, float* __restrict__ part,
                                                                 int64_t ldp, const float* __restrict__ a_bound,
-                                                                const float* __restrict__ l_bound,
-                                                                bf16x8* __restrict__ Cfr = nullptr, int64_t cexp = 0,
-                                                                const float* __restrict__ colmax = nullptr) {
+                                                                const float* __restrict__ l_bound) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];  // 2 x 12 KiB: [row sub-tile][plane][lane]
   int t, tn, k;
-  x6_item<COUT>(blockIdx.x, nTn, K, t, tn, k);
+  x6_item(blockIdx.x, nTn, K, t, tn, k);
   const int nTp = nmb / 4;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -432,22 +407,6 @@ __global__ __launch_bounds__(256, 2) void expert_cond_x6_kernel(const bf16x8* __
   x6_mainloop<1, 2, NPL, F16, X8>(acc, sL, img_rsrc(Lfr, lfr_bytes), (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk) * 3u * kFragBytes,
               img_rsrc(Afr, afr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
 
-  if constexpr (COUT) {
-    const float cmul = ldexpf(1.f, img_exp(*colmax * *a_bound * 1.0009765625f) -
-                                       (img_exp(*a_bound) + img_exp(*l_bound)));
-    bf16x8* Ck = Cfr + (int64_t)k * cexp;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = acc[i][c][8 * s2 + j] * cmul;
-          store_split_f16(Ck + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + 2 * i + s2) * 3) * 64 + lane, v, 1.f);
-        }
-  }
   // sum over the 128 rows of C^2 per column: 4 sub-tiles x 16 registers, then the lane halves
   const int64_t nbase = (int64_t)tn * kX6BN + 64 * w + (lane & 31);
   float* dst = part + ((int64_t)k * nTp + t) * ldp;
@@ -626,7 +585,7 @@ __device__ __forceinline__ void x6_mainloop16(floatx4v (&acc)[8][4], bf16x8 (*sL
 // the contraction is unchanged (x6_mainloop16).  Wave w: 128 rows x 64 columns =
 // 8 x 4 blocks of 16 x 16; 96 MFMAs per wave and pair.
 // COUT (training): C_k = L_k^T A is also written as a split-f16 B-layout image per expert,
-// as expert_cond_x6_kernel<2, true, false, true> does; a fragment's lane position takes
+// (the B-layout of the images K4 writes); a fragment's lane position takes
 // 8 rows from two lanes of the 16x16 accumulator layout (one exchange across the lane halves).
 template <bool COUT = false>
 __global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __restrict__ Afr,
@@ -1771,7 +1730,7 @@ __device__ __forceinline__ void store_acc16_f32(const floatx4v (&acc)[8][4], flo
   }
 }
 
-template <int KMAX, bool ONCE>
+template <int KMAX>
 __device__ __forceinline__ void trsm_stats16_item(
     bf16x8 (*sL)[4 * 2 * 3 * 64], float* __restrict__ sQ, int t, int tn, const bf16x8* __restrict__ Tfr,
     uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
@@ -1813,7 +1772,7 @@ __device__ __forceinline__ void trsm_stats16_item(
   // A's image: fragment (column block 8 tn + 2 w + c, k-step 8 t + ib), lane position pos
   const bool lo_half = lane < 32;
   const int pos = lo_half ? li + 32 * q : 16 + li + 32 * (q - 2);
-  if (!stats || !ONCE) {
+  if (!stats) {  // no stats: the image alone
 #pragma unroll
     for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
@@ -1829,71 +1788,6 @@ __device__ __forceinline__ void trsm_stats16_item(
         }
         store_split_f16(Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, a_scale);
       }
-    if (!stats) return;
-    // (ONCE = false: the stats products split the accumulators a second time)
-  const int qe = img_exp(__uint_as_float(reinterpret_cast<const unsigned int*>(sQ)[128 * KMAX]));
-  const float q_scale = ldexpf(1.f, qe), s_unscale = ldexpf(1.f, -(qe + img_exp(sqrtf(*a_var))));
-#pragma unroll
-  for (int st2 = 0; st2 < 2; ++st2) {  // 64-row stats tile 2 t + st2 = row blocks 4 st2 .. 4 st2 + 3
-    floatx4v sq[4];
-    float a2[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      sq[cb] = floatx4v{0.f, 0.f, 0.f, 0.f};
-      a2[cb] = 0.f;
-    }
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {  // row blocks ib0 = 4 st2 + 2 pr and ib0 + 1 (32 rows)
-      const int ib0 = 4 * st2 + 2 * pr;
-      bf16x8 qf[3];
-      {
-        halfx8 qh, ql;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int row = 16 * ib0 + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4);
-          const float x = (li < K ? sQ[row * KMAX + (li < KMAX ? li : 0)] : 0.f) * q_scale;
-          const _Float16 xh = (_Float16)x;
-          qh[j] = xh;
-          ql[j] = (_Float16)(x - (float)xh);
-        }
-        qf[0] = __builtin_bit_cast(bf16x8, qh);
-        qf[1] = __builtin_bit_cast(bf16x8, ql);
-      }
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        halfx8 vh, vl;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float a = j < 4 ? acc[ib0][cb][j] : acc[ib0 + 1][cb][j - 4];
-          a2[cb] = fmaf(a, a, a2[cb]);
-          const float x = a * a_scale;
-          const _Float16 xh = (_Float16)x;
-          vh[j] = xh;
-          vl[j] = (_Float16)(x - (float)xh);
-        }
-        const bf16x8 bf[3] = {__builtin_bit_cast(bf16x8, vh), __builtin_bit_cast(bf16x8, vl), bf16x8{}};
-        sq[cb] = mfma16_fmt<2, true>(qf, bf, sq[cb]);
-      }
-    }
-    const int64_t st = 2 * (int64_t)t + st2;
-    if (64 * st < M) {
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        const int64_t n = (int64_t)tn * kX6BN + 64 * w + 16 * cb + li;
-        float s_a2 = a2[cb] + __shfl_xor(a2[cb], 16, 64);
-        s_a2 += __shfl_xor(s_a2, 32, 64);
-        if (n < N) {
-          float* dst = stats + st * (K + 1) * lds_ + n;
-          if (lane < 16) dst[0] = s_a2;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int kk = 4 * q + e;
-            if (kk < K) dst[(int64_t)(1 + kk) * lds_] = sq[cb][e] * s_unscale;
-          }
-        }
-      }
-    }
-  }
     return;
   }
   // With the stats: every accumulator value is split once (x = a 2^e -> f16 hi, f16 lo,
@@ -1996,7 +1890,7 @@ __device__ __forceinline__ void trsm_stats16_item(
 }
 
 // Row-tile pairs as trsm_stats_x6_kernel (equal work per workgroup).
-template <int KMAX, bool ONCE = true>
+template <int KMAX>
 __global__ __launch_bounds__(256, 2) void trsm_stats16_kernel(
     const bf16x8* __restrict__ Tfr, uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes,
     int nmk, int nTn, int64_t M, int64_t N, const float* __restrict__ q_mu, int64_t ldq, int K,
@@ -2011,13 +1905,13 @@ __global__ __launch_bounds__(256, 2) void trsm_stats16_kernel(
   col_major_item(blockIdx.x, nP, nTn, p, tn);
   if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
   __syncthreads();
-  trsm_stats16_item<KMAX, ONCE>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
+  trsm_stats16_item<KMAX>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
                           lds_, Af32, lda, a_var, t_bound, k_bound);
   if (nT - 1 - p == p) return;
   __syncthreads();
   if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
   __syncthreads();
-  trsm_stats16_item<KMAX, ONCE>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats, lds_,
+  trsm_stats16_item<KMAX>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats, lds_,
                           Af32, lda, a_var, t_bound, k_bound);
 }
 
@@ -2153,15 +2047,10 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
     const size_t cexp = cols_planes(M, N);
     if (cfr_bytes < (size_t)K * cexp) return -17;
     if (!aligned16(Cfr)) return MGP_ERR_ALIGN;
-    if (k5_shape16())
-      hipLaunchKernelGGL((expert_cond16_kernel<true>), grid, dim3(256), 0, s, (const bf16x8*)Afr, (const bf16x8*)Lfr,
-                         (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N,
-                         part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
-    else
-      hipLaunchKernelGGL((expert_cond_x6_kernel<2, true, false, true>), grid, dim3(256), 0, s, (const bf16x8*)Afr,
-                         (const bf16x8*)Lfr, (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K),
-                         nmk, nmb, nTn, K, N, part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
-  } else if (planes == 2 && f16 && !x8 && k5_shape16()) {  // the default split-f16 forward K5
+    hipLaunchKernelGGL((expert_cond16_kernel<true>), grid, dim3(256), 0, s, (const bf16x8*)Afr, (const bf16x8*)Lfr,
+                       (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N,
+                       part, ldp, a_bound, l_bound, (bf16x8*)Cfr, (int64_t)(cexp / 16), colmax);
+  } else if (planes == 2 && f16 && !x8) {  // the split-f16 forward K5 (16x16x32 MFMA)
     hipLaunchKernelGGL((expert_cond16_kernel<false>), grid, dim3(256), 0, s, (const bf16x8*)Afr, (const bf16x8*)Lfr,
                        (uint32_t)mgp_x6_cols_bytes(M, N), (uint32_t)mgp_x6_lower_bytes(M, K), nmk, nmb, nTn, K, N,
                        part, ldp, a_bound, l_bound);
@@ -2169,7 +2058,6 @@ static int expert_cond_planes(const void* Afr, size_t afr_bytes, const void* Lfr
   MGP_K5_CASE(3, false, false)
   MGP_K5_CASE(2, false, false)
   MGP_K5_CASE(1, false, false)
-  MGP_K5_CASE(2, true, false)
   MGP_K5_CASE(2, true, true)
   }
 #undef MGP_K5_CASE
@@ -2214,18 +2102,10 @@ static int launch_trsm_x6(const void* Tfr, size_t tb, const void* Kfr, size_t kb
       hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                          (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
                          (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
-    else if (k4_shape16() && k4_split_once())
-      hipLaunchKernelGGL((trsm_stats16_kernel<KMAX, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr, (uint32_t)tb,
-                         (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K, (bf16x8*)Afr, stats, lds, A,
-                         lda, a_var, a_bound, t_bound, k_bound);
-    else if (k4_shape16())
-      hipLaunchKernelGGL((trsm_stats16_kernel<KMAX, false>), grid, dim3(256), 0, s, (const bf16x8*)Tfr, (uint32_t)tb,
-                         (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K, (bf16x8*)Afr, stats, lds, A,
-                         lda, a_var, a_bound, t_bound, k_bound);
     else
-      hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
-                         (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,
-                         (bf16x8*)Afr, stats, lds, A, lda, a_var, a_bound, t_bound, k_bound);
+      hipLaunchKernelGGL((trsm_stats16_kernel<KMAX>), grid, dim3(256), 0, s, (const bf16x8*)Tfr, (uint32_t)tb,
+                         (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K, (bf16x8*)Afr, stats, lds, A,
+                         lda, a_var, a_bound, t_bound, k_bound);
   } else if (a_var)
     hipLaunchKernelGGL((trsm_stats_x6_kernel<KMAX, true>), grid, dim3(256), 0, s, (const bf16x8*)Tfr,
                        (uint32_t)tb, (const bf16x8*)Kfr, (uint32_t)kb, nmk, nTn, M, N, q_mu, ldq, K,

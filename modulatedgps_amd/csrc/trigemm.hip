@@ -371,13 +371,6 @@ __global__ __launch_bounds__(256) void cond_finalize_kernel(const float* __restr
 
 using namespace mgp;
 
-#include <stdlib.h>
-static bool force_guard() {  // experiment switch: MGP_FORCE_GUARD=1 selects the guarded path
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("MGP_FORCE_GUARD"); v = (e && e[0] == '1') ? 1 : 0; }
-  return v == 1;
-}
-
 // Tile choice shared by K4 and K5: row tile BM = kTgBM always (the stats tiling
 // depends on it: T = ceil(M / BM)); column tile 256 for large N, else 128.
 #ifndef MGP_TG_BM
@@ -398,7 +391,7 @@ static int launch_trsm(const float* LinvT, int64_t ldl, const float* Kuf, int64_
   const size_t shm2 = (size_t)(BM * KMAX + 2 * (KMAX + 1) * BN) * sizeof(float);
   const size_t sh = shm > shm2 ? shm : shm2;
   const dim3 grid(nTm * nTn), block(TgCfg<BM, BN>::THREADS);
-  if ((M % BM == 0) && (N % BN == 0) && !force_guard())
+  if ((M % BM == 0) && (N % BN == 0))
     hipLaunchKernelGGL((trsm_stats_kernel<BM, BN, KMAX, false>), grid, block, sh, s, LinvT, ldl, Kuf, ldk,
                        M, N, q_mu, ldq, K, A, lda, stats, lds);
   else
@@ -469,7 +462,7 @@ static int launch_expert(const float* A, int64_t lda, const float* q_sqrt, int64
   const int64_t ldp = expert_ldp(N);
   const size_t shm = (size_t)TriGemm<BM, BN, true, false>::LDS_FLOATS * sizeof(float);
   const dim3 grid(K * nTn * nTm), block(TgCfg<BM, BN>::THREADS);
-  if (M % BM == 0 && N % BN == 0 && !force_guard())
+  if (M % BM == 0 && N % BN == 0)
     hipLaunchKernelGGL((expert_cond_kernel<BM, BN, false>), grid, block, shm, s, A, lda, q_sqrt, ldqs,
                        strideq, M, N, K, part, ldp);
   else

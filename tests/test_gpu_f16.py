@@ -150,15 +150,13 @@ def test_elbo_configs_formats(device, fmt_mode, N, M, K, D, ls, S):
     assert normwise(to_np(var_a).T, parts["var_a"]) < 1e-4
 
 
-@pytest.mark.parametrize("k4_shape,k5_shape", [("16", "16"), ("32", "32"), ("32", "16"), ("16", "32")])
-def test_mfma_shape_switches(device, monkeypatch, k4_shape, k5_shape):
+def test_mfma_shape_switches(device):
     """The split-f16 K4 and K5 on 16x16x32 MFMAs (trsm_stats16_kernel,
-    expert_cond16_kernel: the defaults) and on 32x32x16 (MGP_K4_SHAPE / MGP_K5_SHAPE
-    = 32, read per call): every combination against the float64 oracle at config-3
-    shapes (ragged N), the forward and the training K5 that also writes the C_k images."""
+    expert_cond16_kernel: the only split-f16 f16x3 kernels since round 4, when the
+    32x32x16 environment switches were removed from the library) against the float64
+    oracle at config-3 shapes (ragged N): the forward and the training K5 that also
+    writes the C_k images."""
     from modulatedgps_amd import ops
-    monkeypatch.setenv("MGP_K4_SHAPE", k4_shape)
-    monkeypatch.setenv("MGP_K5_SHAPE", k5_shape)
     N, M, K, D, ls = 3001, 1024, 8, 8, 1.0
     X, _, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=2)
     L = p.pred
