@@ -21,7 +21,7 @@ import torch
 #              work.  The training step follows it (A's image, S_k A in the
 #              backward); the reduced-plane modes use "x6".
 _CFG = {"jitter": 1e-6, "device": None, "conditional": "x6", "expert_planes": 3, "expert_format": "f16",
-        "expert_cross": "f16"}
+        "expert_cross": "f16", "step_schedule": "overlap"}
 # expert_cross (f16 images): the precision of K5's two cross-term products
 #              a_hi b_lo + a_lo b_hi -- "f16" (three f16 products) or "f8" (one
 #              e4m3 MFMA per two k-steps for both, mgp_expert_conditional_f16x8:
@@ -93,6 +93,29 @@ def set_expert_cross(cross):
     _CFG["expert_cross"] = cross
 
 
+# step_schedule (x6 mode): where the Cholesky-independent work of an ELBO step runs
+#              relative to the latency-bound K3 chain (host-side launch order only;
+#              every schedule computes the same bits):
+#   "overlap"  K1 and the tril(q_sqrt) images of both layers and the KL on a side
+#              stream beside K3 (round 1-3 default);
+#   "k1a_late" the assign layer's K1 on the side stream after K3, beside the pred
+#              layer's K4 (one K1 beside the chain instead of two);
+#   "k1_main"  both K1 on the main stream after K3 (only the small images and
+#              the KL beside the chain);
+#   "serial"   everything on the main stream, K3 alone on the chip.
+STEP_SCHEDULES = ("overlap", "k1a_late", "k1_main", "serial")
+
+
+def step_schedule():
+    return _CFG["step_schedule"]
+
+
+def set_step_schedule(name):
+    if name not in STEP_SCHEDULES:
+        raise ValueError(f"step schedule must be one of {STEP_SCHEDULES}")
+    _CFG["step_schedule"] = name
+
+
 def forward_image_format(train=False):
     """Image format of the K1 -> K4 -> K5 chain (and of the training step's A
     image): expert_format() at full planes, "x6" for the reduced-plane modes."""
@@ -116,6 +139,8 @@ def _from_env():
         set_expert_format(env["MGP_K5_FORMAT"])
     if "MGP_K5_CROSS" in env:
         set_expert_cross(env["MGP_K5_CROSS"])
+    if "MGP_STEP_SCHEDULE" in env:
+        set_step_schedule(env["MGP_STEP_SCHEDULE"])
 
 
 _from_env()

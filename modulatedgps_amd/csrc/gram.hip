@@ -15,7 +15,6 @@
 // parallelism; partial tiles go to a workspace and gram_reduce_kernel sums
 // them in a fixed order (deterministic), applies alpha and the triangle.
 // Roofline: f32 MFMA (2 MI MJ N flops, half for the triangular outputs).
-#include <atomic>
 #include "mgp_common.hpp"
 
 namespace mgp {
@@ -869,18 +868,11 @@ extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y,
   return launch_status();
 }
 
-// CUs of the current device (the 768-thread grams run one workgroup per CU).
-static int device_cus() {
-  static std::atomic<int> cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  int n = cache[dev].load(std::memory_order_relaxed);
-  if (n <= 0) {
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cache[dev].store(n, std::memory_order_relaxed);
-  }
-  return n;
-}
+// The split-K count is costed for the MI355X's 256 CUs whatever device is current:
+// a fixed count keeps the workspace size (mgp_*_workspace_bytes) and the fixed-order
+// split reduction -- so the result bits -- the same on every device and CU partition
+// mode (round 4; the count used to follow hipDeviceAttributeMultiprocessorCount).
+constexpr int kGramCUs = 256;
 
 // Split-K count of the 768-thread grams (items = workgroups per split, out_tiles =
 // 128 x 128 output tiles the reduction sums): every workgroup of a launch holds
@@ -892,7 +884,7 @@ static int device_cus() {
 // rule (double until 2048 workgroups) left c3's P_k gram 4.5 rounds deep: 16
 // splits instead of 8 take it from 2.28 to 2.12 ms (profiles/r03_gram_splits_probe.log).
 static int gram_x6_splits(int64_t N, int64_t items, int64_t out_tiles) {
-  const int cus = device_cus();
+  const int cus = kGramCUs;
   int best = 1;
   double best_cost = 1e300;
   static const int cand[] = {1, 2, 4, 8, 16, 24, 32, 40, 48, 56, 64};

@@ -131,6 +131,7 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
     }
     if (TRI != 2 && (ld & 3) == 0 && ((uintptr_t)row & 15) == 0) {  // float4 loads (c0 % 4 == 0), scalar tail
       const int64_t c4 = c0 + ((c1 - c0) & ~(int64_t)3);
+#pragma unroll 4
       for (int64_t c = c0 + 4 * lane; c < c4; c += 256) {
         const float4 v = *reinterpret_cast<const float4*>(row + c);
         m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
@@ -151,12 +152,13 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
   if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
-// Launch shape of absmax_kernel<TRI>: <= 256 row groups (one atomic per workgroup);
+// Launch shape of absmax_kernel<TRI>: <= 1024 row groups (one atomic per workgroup; 256
+// left the reduction of K q_sqrt triangles latency-bound at 34 us for 32 MB, round 4);
 // TRI 0 adds column chunks so a few long rows still fill the chip.
 template <int TRI>
 static void launch_absmax(const float* src, int64_t ld, int64_t stride, int64_t rows, int64_t cols,
                           int64_t nrows_total, float* out, hipStream_t s) {
-  const int64_t gx = std::min<int64_t>((nrows_total + 3) / 4, TRI == 0 ? 64 : 256);
+  const int64_t gx = std::min<int64_t>((nrows_total + 3) / 4, TRI == 0 ? 64 : 1024);
   const int64_t gy = TRI == 0 ? std::min<int64_t>((cols + 8191) / 8192, 64) : 1;
   hipLaunchKernelGGL(absmax_kernel<TRI>, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, src, ld, stride, rows,
                      cols, nrows_total, (unsigned int*)out);

@@ -41,7 +41,7 @@ import torch
 from . import ops
 from .broadcasting_lik import BroadcastingLikelihood
 from .config import (conditional_mode, default_device, default_jitter, expert_cross, expert_planes,
-                     forward_image_format)
+                     forward_image_format, step_schedule)
 
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
@@ -265,18 +265,37 @@ class SVGPModified:
     def _marginals_kn(self, Xnew):
         """Xnew [..., N, D] -> (fmean, fvar, S, N, stride_s, lead): expert-major [K, cols]
         marginals where sample s of point n is column s * stride_s + n.  S tiled copies
-        of one input (SGP.integrate, models.py:35-36) are computed once (stride_s = 0)."""
-        X = self.kernel._x(Xnew)
+        of one input (SGP.integrate, models.py:35-36) are computed once (stride_s = 0).
+        Tiling is recognised without a device sync: a device tensor whose sample axis
+        has stride 0 (what integrate() returns, an expand() view), or a host array
+        whose copies compare equal on the host; a materialised device copy of tiled
+        rows is computed row by row (the same values, S times the work)."""
+        host_tiled = False
+        if not isinstance(Xnew, torch.Tensor):
+            Xh = np.asarray(Xnew)
+            if Xh.ndim >= 3:
+                Xh2 = Xh.reshape(-1, *Xh.shape[-2:])
+                host_tiled = Xh2.shape[0] > 1 and bool((Xh2 == Xh2[:1]).all())
+        elif Xnew.dim() >= 3:
+            lead_t = Xnew.shape[:-2]
+            if Xnew.device.type == "cpu":
+                X2 = Xnew.reshape(-1, *Xnew.shape[-2:])
+                host_tiled = X2.shape[0] > 1 and bool(torch.equal(X2, X2[:1].expand_as(X2)))
+            else:
+                host_tiled = all(st == 0 for st, n in zip(Xnew.stride()[:len(lead_t)], lead_t) if n > 1)
+        X = self.kernel._x(Xnew) if not host_tiled else None
+        if host_tiled:
+            Xsrc = Xnew if isinstance(Xnew, torch.Tensor) else torch.as_tensor(np.asarray(Xnew))
+            lead, N = Xsrc.shape[:-2], Xsrc.shape[-2]
+            S = int(np.prod(lead)) if len(lead) else 1
+            fm, fv = self.conditional_kn(Xsrc[(0,) * len(lead)])
+            return fm, fv, S, N, 0, lead
         if X.dim() == 2:
             fm, fv = self.conditional_kn(X)
             return fm, fv, 1, X.shape[0], 0, ()
         lead, N = X.shape[:-2], X.shape[-2]
-        Xs = X.reshape(-1, N, X.shape[-1])
-        S = Xs.shape[0]
-        if S > 1 and bool(torch.equal(Xs, Xs[:1].expand_as(Xs))):
-            fm, fv = self.conditional_kn(Xs[0])
-            return fm, fv, S, N, 0, lead
-        fm, fv = self.conditional_kn(Xs.reshape(-1, X.shape[-1]))
+        S = X.reshape(-1, N, X.shape[-1]).shape[0]
+        fm, fv = self.conditional_kn(X.reshape(-1, X.shape[-1]))
         return fm, fv, S, N, N, lead
 
     def posterior(self, precompute_cache=None):
@@ -351,17 +370,25 @@ class RelaxedOneHotCategorical:
     Gumbel-softmax kernel.  The first sample uses the key the logits were drawn with,
     so W_dist(Xt) -> sample(1) -> E_log_p_Y reproduces _build_likelihood with that key."""
 
-    def __init__(self, temperature, logits, rows, seed=None, n_offset=0):
+    def __init__(self, temperature, logits, rows, seed=None, n_offset=0, model=None):
         self.temperature = float(temperature)
         self.logits = logits
         self._S, self._N = rows
         self._seed = seed
+        self._model = model
         self._n_offset = int(n_offset)
         self._draws = 0
 
-    def sample(self, sample_shape=1, noise_u=None, seed=None):
-        """[n, S * N, K] relaxed one-hot samples; noise_u: explicit uniforms [n?, S, N, K]."""
-        n = int(sample_shape if not isinstance(sample_shape, (tuple, list)) else sample_shape[0])
+    def sample(self, sample_shape=(), noise_u=None, seed=None):
+        """TFP sample semantics: sample() -> [S * N, K], sample(n) / sample((n,)) ->
+        [n, S * N, K] relaxed one-hot samples (the reference draws sample(1)[0],
+        models.py:73).  noise_u: explicit uniforms [n?, S, N, K].  Without noise and
+        seed, the first draw uses the key the logits were drawn with (W_dist's, so
+        W_dist -> sample(1) -> E_log_p_Y reproduces _build_likelihood with that key)
+        and every later draw a fresh key from the model (TF's stateful RNG advances
+        per call); with W_dist(noise_z=...) and no seed every draw is fresh."""
+        shape = tuple(sample_shape) if isinstance(sample_shape, (tuple, list)) else (int(sample_shape),)
+        n = int(np.prod(shape)) if shape else 1
         outs = []
         for i in range(n):
             u = None
@@ -369,13 +396,18 @@ class RelaxedOneHotCategorical:
                 u = noise_u[i] if noise_u.dim() == 4 else noise_u
             if seed is not None:
                 key = _splitmix64(int(seed) + i) if i else int(seed)
+            elif self._draws == 0 and self._seed is not None:
+                key = self._seed
+            elif self._model is not None:
+                key = self._model.next_seed()
             else:
-                key = self._seed if self._draws == 0 and self._seed is not None else _splitmix64(
-                    (self._seed or 0) * 0x100000001B3 + 0x5EED + self._draws)
+                key = _splitmix64((self._seed or 0) * 0x100000001B3 + 0x5EED + self._draws)
             self._draws += 1
             outs.append(ops.relaxed_onehot_sample(self.logits, self._S, self._N, self.temperature, noise_u=u,
                                                   seed=key, n_offset=self._n_offset))
-        return torch.stack(outs)
+        if not shape:
+            return outs[0]
+        return torch.stack(outs).reshape(*shape, *outs[0].shape)
 
 
 class SGP:
@@ -587,17 +619,36 @@ class SMGP(SGP):
             with _Stage(timing, "split_tri"):
                 for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
                     Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt, bounded=bounded)
+        sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
+        late = {"overlap": (), "k1a_late": ("a",), "k1_main": ("f", "a"), "serial": ("f", "a")}[sched]
         if b["x6"]:
-            side.wait_event(prep)   # after Kuu's build (and so after everything before K3 on main)
-            with torch.cuda.stream(side):
+            def side_work():
                 for L, layer in layers:
-                    images[L] = layer.operand_images(X, {"Kfr": b["Kfr_" + L], "Lfr": b["Lfr_" + L]},
-                                                     timing, fmt)
+                    X_ = layer.kernel._x(X)
+                    if L not in late:
+                        with _Stage(timing, "rbf_kuf"):
+                            ops.rbf_kuf_x6(X_, layer.Z, layer.kernel.variance, layer.kernel.lengthscales,
+                                           out=b["Kfr_" + L], fmt=fmt)
+                    with _Stage(timing, "split_tri"):
+                        ops.split_lower_x6(layer.q_sqrt, out=b["Lfr_" + L], fmt=fmt)
+                    images[L] = (b["Kfr_" + L], b["Lfr_" + L])
                 if kl_out is not None:
                     with _Stage(timing, "gauss_kl"):
                         self.pred_layer.prior_kl(out=kl_out[0:1])
                         self.assign_layer.prior_kl(out=kl_out[1:2])
-            main.wait_stream(side)
+            if sched == "serial":
+                side_work()
+            else:
+                side.wait_event(prep)   # after Kuu's build (and so after everything before K3 on main)
+                with torch.cuda.stream(side):
+                    side_work()
+                main.wait_stream(side)
+
+            def kuf_late(L):   # a K1 kept off the chain's window (schedules k1a_late, k1_main, serial)
+                layer = self.pred_layer if L == "f" else self.assign_layer
+                with _Stage(timing, "rbf_kuf"):
+                    ops.rbf_kuf_x6(layer.kernel._x(X), layer.Z, layer.kernel.variance, layer.kernel.lengthscales,
+                                   out=b["Kfr_" + L], fmt=fmt)
         LinvT = {"f": LinvT_f, "a": LinvT_a}
         bufs = {L: {"Kuf": b["Kuf_" + L], "A": b["A_" + L], "stats": b["stats_" + L],
                     "fmean": b["mu_" + L], "fvar": b["var_" + L], "ws_expert": b["ws_expert"],
@@ -609,12 +660,26 @@ class SMGP(SGP):
             # matrix-core kernels fill the chip alone, and a cross-stream hand-off
             # costs 10-25 us of idle GPU per wait (measured)
             pf, pa = self.pred_layer, self.assign_layer
+            k1a_ev = None
+            if sched == "k1a_late":   # the assign layer's K1 beside the pred layer's K4
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    kuf_late("a")
+                k1a_ev = torch.cuda.Event()
+                k1a_ev.record(side)
+            elif sched in ("k1_main", "serial"):
+                kuf_late("f")
+                kuf_late("a")
             Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing, fmt, Tfr=Tfr["f"])
+            if k1a_ev is not None:
+                main.wait_event(k1a_ev)
             Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt, Tfr=Tfr["a"])
             pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
             pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)
         else:
             for L, layer in layers:
+                if L in late:
+                    kuf_late(L)
                 layer.conditional_kn(X, LinvT[L], bufs=bufs[L], timing=timing, images=images.get(L), fmt=fmt)
         if kl_out is not None and not b["x6"]:
             with _Stage(timing, "gauss_kl"):
@@ -640,7 +705,8 @@ class SMGP(SGP):
         if seed is None and noise_z is None:
             seed = self.next_seed()
         logits = ops.assign_logits(fm, fv, S, N, stride, noise_z=noise_z, seed=seed or 0, n_offset=n_offset)
-        return RelaxedOneHotCategorical(TAU, logits.reshape(S * N, self.K), (S, N), seed=seed, n_offset=n_offset)
+        return RelaxedOneHotCategorical(TAU, logits.reshape(S * N, self.K), (S, N), seed=seed, n_offset=n_offset,
+                                        model=self)
 
     def E_log_p_Y(self, Xt, Y, W_SND):
         """SMGP.E_log_p_Y (models.py:63-67): logsumexp_S(sum_K W ve) - log S -> [N]
@@ -661,8 +727,12 @@ class SMGP(SGP):
     @property
     def trainable_variables(self):
         """GPflow Module.trainable_variables (utils/training_utils.py:10): the device
-        tensors of trainable_parameters(), in its order (constrained values; the
-        optimiser keeps the unconstrained shadows, modulatedgps_amd.training.AdamTF)."""
+        tensors of trainable_parameters(), in its order.  These hold the CONSTRAINED
+        values (what every kernel reads); GPflow's tf.Variables hold the unconstrained
+        ones (softplus^-1 for positive parameters).  run_adam / AdamTF keep the
+        unconstrained shadows themselves; a custom loop gets GPflow's semantics from
+        unconstrained_variables(), elbo_and_grad(..., unconstrained=True) and
+        assign_unconstrained() (tests/test_gpu_api.py)."""
         return tuple(t for _, t, _ in self.trainable_parameters())
 
     # ------------------------------------------------------------------ ELBO
@@ -719,10 +789,36 @@ class SMGP(SGP):
             ps.append(("assign_lik_variance", self.assign_likelihood.likelihood.variance, "positive"))
         return ps
 
+    def unconstrained_variables(self):
+        """{name: device tensor} of the unconstrained values GPflow's trainable_variables
+        hold (utils/training_utils.py:10 differentiates w.r.t. these): free parameters as
+        they are, positive ones as u = softplus^-1(theta) (gpflow.utilities.positive(),
+        float64 inverse, then float32; the value theta = softplus(u) reproduces theta)."""
+        out = {}
+        for name, t, kind in self.trainable_parameters():
+            if kind == "positive":
+                th = t.detach().double()
+                out[name] = torch.where(th > 20, th, torch.log(torch.expm1(th))).float()
+            else:
+                out[name] = t.detach().clone()
+        return out
+
+    def assign_unconstrained(self, values):
+        """Set parameters from unconstrained values (dict name -> tensor, e.g. after a
+        custom optimiser step on unconstrained_variables()): theta = softplus(u) for
+        positive parameters, in place, so every kernel reads the new state."""
+        for name, t, kind in self.trainable_parameters():
+            if name not in values:
+                continue
+            v = values[name].to(device=t.device, dtype=torch.float32).reshape(t.shape)
+            t.copy_(torch.nn.functional.softplus(v.double()).float() if kind == "positive" else v)
+
     def elbo_and_grad(self, X, Y, noise=None, seed=None, n_offset=0, n_total=None, process_group=None,
-                      timing=None):
+                      timing=None, unconstrained=False):
         """ELBO (0-d float32) and its gradient w.r.t. every constrained parameter of
-        trainable_parameters() (dict name -> device tensor), i.e. the GradientTape pass
+        trainable_parameters() (dict name -> device tensor; unconstrained=True: w.r.t.
+        the unconstrained values of unconstrained_variables(), GPflow's
+        trainable_variables, by the softplus chain rule), i.e. the GradientTape pass
         of run_adam's optimisation step (training_utils.py:10) on the HIP kernels:
         K6 backward -> per layer conditional backward (x6) -> Cholesky backward -> RBF
         backward (Kuf and Kuu) -> + KL.  Data-parallel: one all-reduce of the
@@ -793,6 +889,10 @@ class SMGP(SGP):
         for name, layer in (("pred", self.pred_layer), ("assign", self.assign_layer)):
             ops.kl_grad(layer.q_mu, layer.q_sqrt, num_data, grads[name + ".q_mu"], grads[name + ".q_sqrt"])
         ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"], out64=b["elbo64"])
+        if unconstrained:   # d/du = d/dtheta * softplus'(u) = d/dtheta * (1 - exp(-theta)) for positive ones
+            for name, t, kind in self.trainable_parameters():
+                if kind == "positive":
+                    grads[name] = grads[name] * (-torch.expm1(-t.double())).float()
         return b["elbo"].clone(), grads
 
     def training_loss_closure(self, data_iter, compile=True):

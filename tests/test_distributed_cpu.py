@@ -72,8 +72,10 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_allreduce_reproduces_full_elbo():
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_two_rank_allreduce_reproduces_full_elbo(world):
+    """One float64 all-reduce of the per-shard data-term sums == the single-process
+    ELBO, at world 2 and at the north_star's 8 ranks (uneven 300 / 8 shards)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -158,11 +160,11 @@ def test_two_rank_gradient_allreduce_reproduces_full_gradient():
     assert max(errs) < 1e-10, errs
 
 
-def _a2a_worker(rank, world, port, q):
+def _a2a_worker(rank, world, port, q, K=5):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from modulatedgps_amd.distributed import redistribute_experts
-    K, C, N = 5, 4, 37
+    C, N = 4, 37
     counts = [b - a for a, b in (shard_rows(K, r, world) for r in range(world))]
     k0, k1 = shard_rows(K, rank, world)
     k = torch.arange(k0, k1, dtype=torch.float32)[:, None, None]
@@ -177,16 +179,17 @@ def _a2a_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_expert_layout_redistribution(world):
+@pytest.mark.parametrize("world,K", [(2, 5), (3, 5), (8, 8)])
+def test_expert_layout_redistribution(world, K):
     """Expert-parallel layout (north_star: experts sharded over GPUs): the exchange
     that moves every expert's conditionals to the rank owning each point slice
     (all_to_all on RCCL, point-to-point on gloo), including a rank with fewer
-    experts than another (K = 5)."""
+    experts than another (K = 5), and the north_star's exact c4 partition: K = 8
+    experts over 8 ranks, one expert each (counts [1] * 8), N = 37 in 8 slices."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_a2a_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_a2a_worker, args=(r, world, port, q, K)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=120) for _ in range(world)]

@@ -48,6 +48,14 @@ def test_posterior_conditional_fused(device, case):
     # predict_f goes through the same plugin (GPflow SVGP.predict_f -> posterior(NOCACHE))
     fm3, fv3 = model.pred_layer.predict_f(Xd)
     assert normwise(to_np(fm3), to_np(fm)) < 1e-7 and normwise(to_np(fv3), to_np(fv)) < 1e-7
+    # tiling is recognised without a device sync: an expand() view (integrate's output)
+    # and a host array are computed once (stride 0), a materialised device copy row by row
+    lay = model.pred_layer
+    Xe = torch.as_tensor(X, dtype=torch.float32, device=device)[None].expand(S, *X.shape)
+    assert lay._marginals_kn(Xe)[4] == 0 and lay._marginals_kn(Xt)[4] == 0
+    assert lay._marginals_kn(Xd)[4] == X.shape[0]
+    fm4, fv4 = post._conditional_fused(Xe)
+    assert normwise(to_np(fm4), to_np(fm)) < 1e-6 and normwise(to_np(fv4), to_np(fv)) < 1e-6
     # distinct inputs per sample (no tiling): one conditional over all S * N rows
     rng = np.random.default_rng(3)
     Xr = X[None] + 0.1 * rng.standard_normal((S,) + X.shape)
@@ -75,6 +83,14 @@ def test_w_dist_and_sample(device):
     W2 = model.W_dist(Xt, seed=7).sample(3)
     assert tuple(W2.shape) == (3, S * N, K) and not torch.equal(W2[0], W2[1])
     assert np.allclose(to_np(W2).sum(-1), 1.0, atol=1e-5)
+    # TFP sample shapes: sample() -> [S * N, K], sample((2, 2)) -> [2, 2, S * N, K]
+    wd3 = model.W_dist(Xt, seed=11)
+    W3 = wd3.sample()
+    assert tuple(W3.shape) == (S * N, K)
+    assert tuple(wd3.sample((2, 2)).shape) == (2, 2, S * N, K)
+    # explicit normals and no seed: every sample() call draws a fresh key
+    wd4 = model.W_dist(Xt, noise_z=z)
+    assert not torch.equal(wd4.sample(), wd4.sample())
 
 
 def test_e_log_p_y(device):
@@ -168,3 +184,32 @@ def test_trainable_variables(device):
     _, grads = model.elbo_and_grad(torch.as_tensor(d["X"], dtype=torch.float32, device=device), d["Y"], seed=3)
     for n, t, _ in tp:
         assert grads[n].numel() == t.numel(), n
+
+
+def test_unconstrained_variables_and_gradients(device):
+    """GPflow's trainable_variables are the unconstrained values (softplus^-1 for the
+    positive ones); unconstrained_variables / elbo_and_grad(unconstrained=True) /
+    assign_unconstrained give a custom loop those semantics: the gradient is the
+    constrained one times softplus'(u) = 1 - exp(-theta), the free blocks unchanged,
+    and a plain gradient-ascent step on u raises the ELBO."""
+    d, p, model = _golden(device)
+    X = torch.as_tensor(d["X"], dtype=torch.float32, device=device)
+    u = model.unconstrained_variables()
+    tp = model.trainable_parameters()
+    for n, t, kind in tp:
+        back = torch.nn.functional.softplus(u[n].double()).float() if kind == "positive" else u[n]
+        assert torch.allclose(back, t, rtol=1e-6, atol=1e-7), n
+    e0 = float(model._build_likelihood(X, d["Y"], seed=5).cpu())
+    _, g = model.elbo_and_grad(X, d["Y"], seed=5)
+    g = {k: v.clone() for k, v in g.items()}
+    _, gu = model.elbo_and_grad(X, d["Y"], seed=5, unconstrained=True)
+    for n, t, kind in tp:
+        ref = g[n] * (-torch.expm1(-t.double())).float() if kind == "positive" else g[n]
+        assert normwise(to_np(gu[n]), to_np(ref)) < 1e-6, n
+    gnorm = float(torch.sqrt(sum((gu[n].double() ** 2).sum() for n, _, _ in tp)).cpu())
+    lr = 1e-3 / gnorm   # a step of length 1e-3 along the gradient
+    model.assign_unconstrained({n: u[n] + lr * gu[n] for n, _, _ in tp})
+    e1 = float(model._build_likelihood(X, d["Y"], seed=5).cpu())
+    assert e1 > e0
+    model.assign_unconstrained(u)   # back to the start
+    assert float(model._build_likelihood(X, d["Y"], seed=5).cpu()) == pytest.approx(e0, rel=1e-6)

@@ -82,16 +82,20 @@ def _c4_expert_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(900)
-def test_c4_expert_layout_full_size(device):
+@pytest.mark.parametrize("world", [2, 8])
+def test_c4_expert_layout_full_size(device, world):
     """BASELINE c4 as north_star states it (the K = 8 experts sharded over the
-    ranks, here 4 + 4 on two ranks), at N = 65536, M = 1024, D = 8."""
+    ranks): 4 + 4 on two ranks, and the exact north_star partition -- one expert
+    per rank on 8 ranks (counts [1] * 8 in the all_to_all, 8 point slices) -- at
+    N = 65536, M = 1024, D = 8 (gloo ranks sharing cuda:0 on the one-GPU box)."""
     N, M, K, D, ls, S = C3
-    procs, q = _spawn(_c4_expert_worker, 2)
+    procs, q = _spawn(_c4_expert_worker, world)
     X, Y, p = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
     z, u = R.explicit_noise(S, N, K, seed=5)
     ref = R.smgp_elbo(X, Y, p, z, u)
-    res = sorted(q.get(timeout=800) for _ in range(2))
+    res = sorted(q.get(timeout=800) for _ in range(world))
     _join(procs)
+    assert len(res) == world
     model = build_model(p, device, seed=7)
     Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
     single_noise = float(model._build_likelihood(Xd, Y, noise=dev_noise(z, u, device)).cpu())

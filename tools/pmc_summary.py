@@ -5,9 +5,17 @@ HBM traffic follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced
 read, so bytes_read = 2 * FETCH_SIZE * 1024; bytes_written = WRITE_SIZE * 1024.
 Both count L2 misses served by the Infinity Cache as well as HBM.
-MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * GRBM_GUI_ACTIVE / 8); over the
-busy CUs only: SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs * SQ_BUSY_CU_CYCLES).
-Usage: python tools/pmc_summary.py gpurun_out profiles/pmc_traffic.json"""
+MFMA busy over the busy CUs: SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs * SQ_BUSY_CU_CYCLES) --
+a ratio of two counts of the same shader clock, so it needs no clock.  Chip-wide
+MFMA busy and the effective clock use GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs)
+over the dispatch duration, which MI355X_MICROARCH.md (DVFS give-back) trusts only
+for dispatches of 0.3 ms or more: on shorter ones the GUI-active window outlasts the
+kernel (round 3 reported 3.2-5.1 GHz for the 6-19 us K3 launches), so below 0.3 ms
+both are left out (null) and the clock-free figures stand alone.  When a pass adds
+SQ_INSTS_VALU_MFMA_MOPS_F64 (units of 512 flops), the f64 MFMA count per launch is
+reported too (a v_mfma_f64_16x16x4 is 2048 flops = 4 MOPS and keeps the pipe busy 64
+cycles), so mfma_busy_cycles / f64_mfma_count can be checked against 64.
+Usage: python tools/pmc_summary.py gpurun_out profiles/pmc_traffic.json [groups...]"""
 import collections
 import csv
 import json
@@ -55,9 +63,14 @@ def kernel_key(name):
     return base
 
 
-def main(root, out):
+MIN_CLOCK_DISPATCH_S = 0.3e-3
+
+
+def main(root, out, groups=("SQ_WAVE_CYCLES", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum")):
     res = collections.defaultdict(lambda: collections.defaultdict(list))
-    for group in ("SQ_WAVE_CYCLES", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum"):
+    for group in groups:
+        if not os.path.exists(os.path.join(root, f"pmc_{group}", "p_counter_collection.csv")):
+            continue
         per, dur, names = load(root, group)
         for d, cs in per.items():
             if "mgp::" not in names[d]:
@@ -78,15 +91,26 @@ def main(root, out):
             e.update(hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes_per_launch=rd + wr)
         if "TCC_HIT_sum" in avg:
             e["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"], 1.0)
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and avg.get("GRBM_GUI_ACTIVE"):
-            cyc = avg["GRBM_GUI_ACTIVE"] / 8.0
-            e["mfma_busy"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
-            e["effective_clock_ghz"] = cyc / (avg["duration_s"] * 1e9)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+            e["mfma_busy_cycles"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"]
             if avg.get("SQ_BUSY_CU_CYCLES"):
                 # MFMA busy over the CUs that had waves resident (latency-bound
-                # kernels such as the K3 chain occupy a few CUs of the 256)
+                # kernels such as the K3 chain occupy a few CUs of the 256); clock-free
                 e["mfma_busy_active_cus"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (4.0 * avg["SQ_BUSY_CU_CYCLES"])
-                e["active_cu_fraction"] = avg["SQ_BUSY_CU_CYCLES"] / (256.0 * cyc)
+            long_enough = avg.get("duration_s", 0.0) >= MIN_CLOCK_DISPATCH_S
+            if avg.get("GRBM_GUI_ACTIVE") and long_enough:
+                cyc = avg["GRBM_GUI_ACTIVE"] / 8.0
+                e["mfma_busy"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
+                e["effective_clock_ghz"] = cyc / (avg["duration_s"] * 1e9)
+                if avg.get("SQ_BUSY_CU_CYCLES"):
+                    e["active_cu_fraction"] = avg["SQ_BUSY_CU_CYCLES"] / (256.0 * cyc)
+            else:
+                e["effective_clock_ghz"] = None
+                e["clock_note"] = "dispatch < 0.3 ms: GRBM_GUI_ACTIVE outlasts the kernel, no clock derived"
+        if "SQ_INSTS_VALU_MFMA_MOPS_F64" in avg:
+            e["f64_mfma_count"] = avg["SQ_INSTS_VALU_MFMA_MOPS_F64"] / 4.0
+            if e.get("mfma_busy_cycles") and e["f64_mfma_count"] > 0:
+                e["mfma_busy_cycles_per_f64_mfma"] = e["mfma_busy_cycles"] / e["f64_mfma_count"]
         summary[k] = e
     json.dump({"source": "rocprofv3 --pmc passes of tools/pmc_pass.sh (tools/bench_kernels.py, c3)",
                "corrections": "bytes_read = 2 * FETCH_SIZE KiB (gfx950 wide-read undercount), "
@@ -96,4 +120,7 @@ def main(root, out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    if len(sys.argv) > 3:
+        main(sys.argv[1], sys.argv[2], tuple(sys.argv[3:]))
+    else:
+        main(sys.argv[1], sys.argv[2])
