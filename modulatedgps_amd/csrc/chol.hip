@@ -49,21 +49,12 @@ __device__ __forceinline__ int ctid() { return (int)(threadIdx.x & (kCholThreads
 
 #ifdef MGP_DBG_STAMPS
 __device__ unsigned long long g_stamps[64 * 16];
-// persistent path: chain stamps [batch 2][step 128][8]; worker phase totals [batch 2][wg 128][8]
-__device__ unsigned long long g_pchain[2 * 128 * 8];
-__device__ unsigned long long g_pwork[2 * 128 * 8];
-#define PSTAMP(b, j, k) do { if (ctid() == 0 && (b) < 2 && (j) < 128) g_pchain[((b) * 128 + (j)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-#define PWACC(b, w, k, v) do { if (ctid() == 0 && (b) < 2 && (w) < 128) g_pwork[((b) * 128 + (w)) * 8 + (k)] += (v); } while (0)
-#define PNOW() __builtin_amdgcn_s_memtime()
-#define STAMP(j, k) do { if (ctid() == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 // 100 MHz reference clock (one time base for every CU): slots 14 / 15
-#define RSTAMP(j, k) do { if (ctid() == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RSTAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(j, k) do {} while (0)
 #define RSTAMP(j, k) do {} while (0)
-#define PSTAMP(b, j, k) do {} while (0)
-#define PWACC(b, w, k, v) do {} while (0)
-#define PNOW() 0ull
 #endif
 
 struct CholArgs {
@@ -77,9 +68,6 @@ struct CholArgs {
   float* lt_absmax[kMaxBatch];                    // optional per batch: max |L^-T| (float bits, atomicMax)
   double* ws; int64_t strideWS;                   // per batch: W, B [Mp][Mp], D [nb][64][64]
   int64_t M, Mp; int nb;
-  // persistent path (chol_persist): per-batch sync words and the shared task table
-  int* sync; int64_t strideSync;                  // per batch: Wver[nb][nb], Bver[nb][nb], Dready[nb], head, err
-  int* tasks; int ntask;                          // task table (chol_task_order), built by chol_prep
 };
 
 __device__ __forceinline__ double* ws_W(const CholArgs& a, int b) { return a.ws + (int64_t)b * a.strideWS; }
@@ -593,13 +581,15 @@ __device__ __forceinline__ doublex4 neg_x_times(const double* __restrict__ Xii, 
 // of the lower blocks right of column block 0 (column block 0 already applied).
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0,
-                                                 const double* sPend = nullptr) {
-  const int w = ctid() >> 6, lane = ctid() & 63;
+                                                 const double* sPend = nullptr, bool active = true) {
+  // active = false: the caller's idle waves take part in every barrier and do no work
+  // (w = 4 matches no role), so the barrier sequence is the same for all waves
+  const int w = active ? (ctid() >> 6) : 4, lane = ctid() & 63;
   int bad = 0;
   const int js = (int)(gcol0 / CB) - 1;
   if (w == 0) {
     panel_factor<0>(sF, col, lane, bad);
-  } else if (sPend) {  // blocks (1,1), (2,1) | (3,1), (2,2) | (3,2), (3,3)
+  } else if (w < 4 && sPend) {  // blocks (1,1), (2,1) | (3,1), (2,2) | (3,2), (3,3)
     const int bi0 = (w == 1) ? 1 : 3, bj0 = (w == 3) ? 2 : 1;
     const int bi1 = (w == 3) ? 3 : 2, bj1 = (w == 1) ? 1 : (w == 2 ? 2 : 3);
     sub_outer_blk<4>(sF, 16 * bi0, 16 * bj0, sPend, sPend);
@@ -610,7 +600,7 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
   const double* P0 = sF;  // panel p's L columns: sF + 16 p
   if (w < 3) {
     sub_outer_blk<1>(sF, 16 * (w + 1), 16, P0, P0);  // update 0 of (1,1), (2,1), (3,1)
-  } else {
+  } else if (w == 3) {
     for (int q = 0; q < 6; ++q) {  // upper blocks (i < j) of X are zero
       const int i = q < 3 ? 0 : (q < 5 ? 1 : 2), j = q < 3 ? q + 1 : (q < 5 ? q - 1 : 3);
       blk_store(sX + 16 * i * LDT + 16 * j, doublex4{0.0, 0.0, 0.0, 0.0});
@@ -625,7 +615,7 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
   } else if (w == 2) {
     sub_outer_blk<1>(sF, 32, 32, P0, P0);  // update 0 of (2,2), (3,2)
     sub_outer_blk<1>(sF, 48, 32, P0, P0);
-  } else {
+  } else if (w == 3) {
     sub_outer_blk<1>(sF, 48, 48, P0, P0);  // update 0 of (3,3)
   }
   STAMP(js, 10);
@@ -664,7 +654,7 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     blk_mma<false>(t, L_(3, 0), X_(0, 0), 1.0);
     blk_mma<false>(t, L_(3, 1), X_(1, 0), 1.0);
     blk_store(S_(3, 0), t);
-  } else {
+  } else if (w == 3) {
     doublex4 t = {0.0, 0.0, 0.0, 0.0};
     blk_mma<false>(t, L_(3, 1), X_(1, 1), 1.0);
     blk_store(S_(3, 1), t);
@@ -681,7 +671,7 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     const doublex4 t = blk_load(S_(2, 0));
     blk_store(S_(2, 0), zero4);
     blk_store(X_(2, 0), neg_x_times(X_(2, 2), t, lane));
-  } else {
+  } else if (w == 3) {
     doublex4 y = blk_load(S_(3, 1));
     blk_mma<false>(y, L_(3, 2), X_(2, 1), 1.0);
     blk_store(S_(3, 1), y);
@@ -732,96 +722,6 @@ __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, cons
   }
 }
 
-// ------------------------------------------------------------------ persistent-path task order
-// The single-launch factorisation (chol_persist) runs the tile work of all steps
-// from one task table; every product is formed once and handed on through the
-// workspace (no per-tile recomputation).  Task kinds (nb = Mp / 64 tile rows):
-//   PAN(i, j)   L_ij = W_ij D_j^T, in place of W_ij (i >= j + 2; L_{j+1,j} is the chain's);
-//   U(i, l, j)  trailing update W_il -= L_ij L_lj^T of step j (j < l <= i), except the
-//               look-ahead tile (j+1, j+1), which the chain updates and factors;
-//   XR(j, c)    row block j of X = L^-1: X_jc = D_j B_jc, in place of B_jc (c < j);
-//   FU(i, c, j) forward substitution B_ic -= L_ij X_jc (i > j, c <= j; X_jj = D_j).
-// Order per step j: the tasks the chain's next step waits for (PAN(j+2, j),
-// U(j+2, j+1, j), U(j+2, j+2, j)), the other panels, the other updates by column;
-// the forward-substitution work of step j (F_j = XR(j, .), FU(., ., j)), needed only
-// at the end, one step later:  A_0 B_0 C_0, A_1 B_1 C_1, F_0, A_2 B_2 C_2, F_1, ...,
-// F_{nb-2}, XR(nb-1, .).  Every dependency of a task lies earlier in the table or is
-// a chain output whose own inputs do, so in-order dequeueing cannot deadlock.
-enum { kTaskPan = 0, kTaskU = 1, kTaskXR = 2, kTaskFU = 3 };
-
-// block q: q < 4 (nb - 1): step j = q / 4, slot s = q % 4 (A_j, B_j, C_j, F_{j-1});
-// then F_{nb-2}, then the last row.
-__host__ __device__ inline int task_block_count(int nb) { return 4 * (nb - 1) + 2; }
-__host__ __device__ inline int task_block_size(int q, int nb) {
-  if (q < 4 * (nb - 1)) {
-    const int j = q / 4, slot = q % 4, T = nb - 1 - j;
-    if (slot == 0) return T >= 2 ? 3 : 0;
-    if (slot == 1) return T >= 3 ? T - 2 : 0;
-    if (slot == 2) return T * (T + 1) / 2 - 1 - (T >= 2 ? 2 : 0);
-    return j >= 1 ? (j - 1) + (nb - j) * j : 0;      // F_{j-1}
-  }
-  if (q == 4 * (nb - 1)) return nb >= 2 ? (nb - 2) + (nb - 1 - (nb - 2)) * (nb - 1) : 0;   // F_{nb-2}
-  return nb - 1;                                                                          // XR(nb-1, .)
-}
-__host__ __device__ inline int task_count(int nb) {
-  int n = 0;
-  for (int q = 0; q < task_block_count(nb); ++q) n += task_block_size(q, nb);
-  return n;
-}
-__host__ __device__ inline int task_encode(int kind, int j, int i, int l) {
-  return (kind << 24) | (j << 16) | (i << 8) | l;
-}
-// entry e of the forward-substitution block F_j
-__device__ __forceinline__ int task_f(int j, int e) {
-  if (e < j) return task_encode(kTaskXR, j, j, e);
-  e -= j;
-  return task_encode(kTaskFU, j, j + 1 + e / (j + 1), e % (j + 1));
-}
-__device__ __forceinline__ int task_entry(int q, int e, int nb) {
-  if (q < 4 * (nb - 1)) {
-    const int j = q / 4, slot = q % 4, T = nb - 1 - j;
-    if (slot == 0) {
-      if (e == 0) return task_encode(kTaskPan, j, j + 2, j);
-      return task_encode(kTaskU, j, j + 2, e == 1 ? j + 1 : j + 2);
-    }
-    if (slot == 1) return task_encode(kTaskPan, j, j + 3 + e, j);
-    if (slot == 2) {
-      // the column-major triangle (l = j+1 .., i = l ..) without (j+1, j+1), (j+2, j+1), (j+2, j+2)
-      int f = e + 2;
-      if (T >= 2 && f >= T) ++f;                       // (j+2, j+2) sits at f = T
-      int l = j + 1;
-      while (f >= nb - l) { f -= nb - l; ++l; }
-      return task_encode(kTaskU, j, l + f, l);
-    }
-    return task_f(j - 1, e);
-  }
-  if (q == 4 * (nb - 1)) return task_f(nb - 2, e);
-  return task_encode(kTaskXR, nb - 1, nb - 1, e);
-}
-
-// Per-batch sync words of the persistent path: Wver[nb][nb] (tile (i, l) of W: the
-// number of updates applied, then l + 1 once it holds L_il), Bver[nb][nb] (tile
-// (i, c) of B: updates applied, then +1 once it holds X_ic), Dready[nb], head (next
-// task), err (a bounded wait gave up).
-__host__ __device__ inline int64_t chol_sync_words(int nb) { return ((int64_t)2 * nb * nb + nb + 2 + 63) / 64 * 64; }
-
-// chol_prep's share of the persistent state: zero this batch's sync words (Dready[0]
-// = 1: prep factors tile (0, 0)) and, for batch 0, fill the task table (block q of
-// the order by workgroup q).
-__device__ __forceinline__ void prep_persist_state(const CholArgs& a, int b) {
-  const int nb = a.nb;
-  int* s = a.sync + (int64_t)b * a.strideSync;
-  const int64_t nw = chol_sync_words(nb), d0 = (int64_t)2 * nb * nb;
-  for (int64_t w = (int64_t)blockIdx.x * kCholThreads + ctid(); w < nw; w += (int64_t)gridDim.x * kCholThreads)
-    s[w] = (w == d0) ? 1 : 0;
-  const int q = blockIdx.x;
-  if (b != 0 || q >= task_block_count(nb)) return;
-  int start = 0;
-  for (int r = 0; r < q; ++r) start += task_block_size(r, nb);
-  const int n = task_block_size(q, nb);
-  for (int e = ctid(); e < n; e += kCholThreads) a.tasks[start + e] = task_entry(q, e, nb);
-}
-
 // ------------------------------------------------------------------ prep launch
 __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   __shared__ double s1[CB * LDT], s2[CB * LDT], col[CB];
@@ -842,7 +742,6 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   auto elem = [&](int64_t gr, int64_t gc) {
     return a.A ? input_elem(a, b, gr, gc) : kuu_elem(a, Zb, sil, varb, gr, gc);
   };
-  if (a.sync) prep_persist_state(a, b);
   if (blockIdx.x == 0) {  // factor tile (0, 0) straight from the input (dispatched first)
     if (threadIdx.x == 0) {
       a.info[b] = 0;
@@ -886,145 +785,53 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
 // The look-ahead's factorisation of tile (j+1, j+1): s1 holds P = L_{j+1,j}, s2 the
 // tile with column block 0 of -P P^T still to apply.
 __device__ __forceinline__ void lookahead_factor(const CholArgs& a, int b, int j, double* s1, double* s2,
-                                                 double* col) {
+                                                 double* col, bool active) {
   // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
   // lower blocks are applied beside the first panel sweep
-  sub_outer_blk<4>(s2, 16 * (threadIdx.x >> 6), 0, s1, s1);
+  if (active) sub_outer_blk<4>(s2, 16 * (ctid() >> 6), 0, s1, s1);
   __syncthreads();
   STAMP(j, 3);
   STAMP(j, 4);
-  factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1);
+  factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1, active);
   STAMP(j, 6);
   __syncthreads();
-  write_diag(a, b, j + 1, s2, s1);
+  if (active) write_diag(a, b, j + 1, s2, s1);
   __syncthreads();
   STAMP(j, 7);
   RSTAMP(j, 15);
 }
 
-__global__ __launch_bounds__(kCholThreads) void chol_step(CholArgs a, int j) {
-  __shared__ double s1[CB * LDT], s2[CB * LDT], sD[CB * LDT], col[CB];
+// Last step (j = nb - 1, no trailing matrix): row block j of X = L^-1, X_jc = D_j B_jc
+// (c < j) and X_jj = D_j, written transposed into L^-T; one workgroup per tile c.
+__global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j) {
+  __shared__ double s1[CB * LDT], sD[CB * LDT];
   const int b = blockIdx.y;
-  const int T = a.nb - j - 1;
-  const int nU = T * (T + 1) / 2;
-  const int idx = blockIdx.x;
-  double* W = ws_W(a, b);
+  const int c = blockIdx.x;
   double* Bm = ws_B(a, b);
   float* LinvT = a.LinvT + (int64_t)b * a.strideL;
-  const int64_t Mp = a.Mp;
-  auto Wt = [&](int bi, int bl) { return W + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
-  auto Bt = [&](int bi, int bl) { return Bm + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
   float* lt_max = a.lt_absmax[0];  // this batch entry's max |L^-T| (no dynamic indexing of the arguments)
 #pragma unroll
   for (int q = 1; q < kMaxBatch; ++q)
     if (b == q) lt_max = a.lt_absmax[q];
-  auto store_linvT = [&](int c, const double* sx) {  // X_jc -> LinvT block (c, j)
+  auto store_linvT = [&](const double* sx) {  // X_jc -> LinvT block (c, j)
     const int64_t gr = (int64_t)c * CB, gc = (int64_t)j * CB;
     const float m = tile_store_f32_max(LinvT + gr * a.ldl + gc, a.ldl, sx, true, (int)min<int64_t>(CB, a.M - gr),
                                        (int)min<int64_t>(CB, a.M - gc));
     if (lt_max) wave_absmax_atomic(m, lt_max);
   };
-
-  if (T == 0) {  // last step: row block j of X only
-    const int c = idx;
-    tile_load(sD, ws_D(a, b, j), CB);
-    if (c < j) tile_load(s1, Bt(j, c), Mp);
-    __syncthreads();
-    if (c < j) {
-      Blk4 x = blk4_zero();
-      col_mma_lower(x, sD, s1);
-      __syncthreads();
-      blk4_to_lds<false>(s1, x);
-      __syncthreads();
-      store_linvT(c, s1);
-    } else {
-      store_linvT(c, sD);
-    }
-    return;
-  }
-
-  if (idx < nU) {  // ---------------- trailing update tile (i, l), j < l <= i
-    int ai = 0;
-    while ((ai + 1) * (ai + 2) / 2 <= idx) ++ai;
-    const int bl_ = idx - ai * (ai + 1) / 2;
-    const int i = j + 1 + ai, l = j + 1 + bl_;
-    const bool la = (ai == 0 && bl_ == 0);
-    if (la) { RSTAMP(j, 14); STAMP(j, 0); }
-    TileRegs r1, rD, r2;
-    Blk4 u;
-    tile_fetch(r1, Wt(i, j), Mp);
-    tile_fetch(rD, ws_D(a, b, j), CB);
-    tile_fetch(r2, (l != i) ? Wt(l, j) : Wt(i, l), Mp);  // P_l's operand, or the diagonal tile itself
-    if (l != i) row_from_global(u, Wt(i, l), Mp);      // the updated tile, in flight with the operands
-    tile_put(s1, r1);
-    tile_put(sD, rD);
-    tile_put(s2, r2);
-    __syncthreads();
-    if (la) STAMP(j, 1);
-    Blk4 pi = blk4_zero(), pl = blk4_zero();
-    row_mma<true, 1>(pi, s1, sD, 1.0);                 // P_i = W_ij D_j^T (D lower: 40 MFMAs/wave)
-    if (l != i) row_mma<true, 1>(pl, s2, sD, 1.0);     // P_l
-    __syncthreads();
-    blk4_to_lds<true>(s1, pi);
-    if (l != i) blk4_to_lds<true>(s2, pl);
-    __syncthreads();
-    if (la) STAMP(j, 2);
-    if (l == i && !la && a.L) {  // L_ij (the look-ahead's L_{j+1,j}: by forward-substitution tile (j+1, j))
-      const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
-      tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
-                     (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
-    }
-    if (l != i) {
-      row_mma<true, 0>(u, s1, s2, -1.0);               // W_il -= P_i P_l^T
-      row_to_global(Wt(i, l), Mp, u);
-      return;
-    }
-    if (la) {  // look-ahead: factor the next diagonal tile
-      lookahead_factor(a, b, j, s1, s2, col);
-    } else {
-      // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T in place in LDS (s2)
-      diag_lower_update(s2, s1);
-      __syncthreads();
-      tile_store_f64(Wt(i, l), Mp, s2);
-    }
-    return;
-  }
-
-  // ------------------ forward-substitution tile (i, c), i > j, c <= j
-  const int x = idx - nU;
-  const int i = j + 1 + x / (j + 1), c = x % (j + 1);
-  TileRegs r1, rD, r2;
-  Blk4 u = blk4_zero();
-  tile_fetch(r1, Wt(i, j), Mp);
-  tile_fetch(rD, ws_D(a, b, j), CB);
-  if (c < j) {
-    tile_fetch(r2, Bt(j, c), Mp);
-    row_from_global(u, Bt(i, c), Mp);
-  }
-  tile_put(s1, r1);
-  tile_put(sD, rD);
-  if (c < j) tile_put(s2, r2);
+  tile_load(sD, ws_D(a, b, j), CB);
+  if (c < j) tile_load(s1, Bm + (int64_t)j * CB * a.Mp + (int64_t)c * CB, a.Mp);
   __syncthreads();
-  Blk4 pi = blk4_zero(), xq = blk4_zero();
-  row_mma<true, 1>(pi, s1, sD, 1.0);                   // P_i
-  if (c < j) col_mma_lower(xq, sD, s2);                // X_jc = D_j B_jc
-  __syncthreads();
-  blk4_to_lds<true>(s1, pi);
-  if (c < j) blk4_to_lds<false>(s2, xq);
-  __syncthreads();
-  if (i == j + 1 && c == j && a.L) {                   // L_{j+1,j} (off the look-ahead's chain)
-    const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
-    tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
-                   (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
+  if (c < j) {   // (uniform per workgroup)
+    Blk4 x = blk4_zero();
+    col_mma_lower(x, sD, s1);
+    __syncthreads();
+    blk4_to_lds<false>(s1, x);
+    __syncthreads();
+    store_linvT(s1);
+  } else {
+    store_linvT(sD);
   }
-  if (c < j) {
-    if (i == j + 1) store_linvT(c, s2);
-    row_mma<false, 0>(u, s1, s2, -1.0);                // B_ic -= P_i X_jc
-  } else {                                             // X_jj = D_j (lower triangular)
-    if (i == j + 1) store_linvT(c, sD);
-    row_mma<false, 2>(u, s1, sD, -1.0);
-  }
-  row_to_global(Bt(i, c), Mp, u);
 }
 
 // ------------------------------------------------------------------ step launch j, tile pairs
@@ -1072,26 +879,28 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     if (lt_max) wave_absmax_atomic(m, lt_max);
   };
   int i = j + 1;
-  if (blockIdx.x == 0) {  // look-ahead: tile (j+1, j+1), group 0 (group 1's waves end here:
-    if (g != 0) return;   // a barrier waits only for the waves that have not terminated)
+  if (blockIdx.x == 0) {  // look-ahead: tile (j+1, j+1) on group 0; group 1's waves take part
+    const bool act = g == 0;  // in every barrier and do no work (uniform barrier sequence)
     RSTAMP(j, 14);
     STAMP(j, 0);
     TileRegs r1, rD, r2;
-    tile_fetch(r1, Wt(i, j), Mp);
-    tile_fetch(rD, ws_D(a, b, j), CB);
-    tile_fetch(r2, Wt(i, i), Mp);
-    tile_put(s1, r1);
-    tile_put(sD, rD);
-    tile_put(s2[0], r2);
+    if (act) {
+      tile_fetch(r1, Wt(i, j), Mp);
+      tile_fetch(rD, ws_D(a, b, j), CB);
+      tile_fetch(r2, Wt(i, i), Mp);
+      tile_put(s1, r1);
+      tile_put(sD, rD);
+      tile_put(s2[0], r2);
+    }
     __syncthreads();
     STAMP(j, 1);
     Blk4 pi = blk4_zero();
-    row_mma<true, 1>(pi, s1, sD, 1.0);
+    if (act) row_mma<true, 1>(pi, s1, sD, 1.0);
     __syncthreads();
-    blk4_to_lds<true>(s1, pi);
+    if (act) blk4_to_lds<true>(s1, pi);
     __syncthreads();
     STAMP(j, 2);
-    lookahead_factor(a, b, j, s1, s2[0], col);
+    lookahead_factor(a, b, j, s1, s2[0], col, act);
     return;
   }
   // pair -> (row i, tile e of the row)
@@ -1154,403 +963,25 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
                    (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
   }
-  if (!has) return;
+  // the final products; the diagonal tile's LDS hand-off barrier is taken by every wave
+  // of both groups (uniform barrier sequence; the other paths have no barrier here)
+  const bool diag = upd && l == i;
   if (upd && l != i) {
     row_mma<true, 0>(u, s1, sT, -1.0);    // W_il -= P_i P_l^T
     row_to_global(Wt(i, l), Mp, u);
-  } else if (upd) {                        // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T
+  } else if (diag) {                       // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T
     diag_lower_update(sT, s1);
-    __syncthreads();
-    tile_store_f64(Wt(i, i), Mp, sT);
   } else if (fwd) {
     if (i == j + 1) store_linvT(c, sT);
     row_mma<false, 0>(u, s1, sT, -1.0);    // B_ic -= P_i X_jc
     row_to_global(Bt(i, c), Mp, u);
-  } else {                                 // X_jj = D_j (lower triangular)
+  } else if (has) {                        // X_jj = D_j (lower triangular)
     if (i == j + 1) store_linvT(c, sD);
     row_mma<false, 2>(u, s1, sD, -1.0);
     row_to_global(Bt(i, c), Mp, u);
   }
-}
-
-// ------------------------------------------------------------------ persistent launch
-// chol_persist: the nb - 1 steps after chol_prep in ONE launch.  Per batch entry,
-// workgroup 0 is the CHAIN: it keeps D_j in LDS and, step after step, forms the
-// look-ahead panel P = W_{j+1,j} D_j^T, applies P P^T to W_{j+1,j+1}, factors it
-// (factor_diag_tile) and publishes D_{j+1}; it never waits for a launch boundary.
-// Workgroups 1.. are WORKERS: they take tasks from the table in order (one
-// returning atomic add per task) and wait only for the tiles and D a task reads.
-// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, the flag form with
-// sc1 payload): every byte another workgroup reads is stored write-through (sc1) by
-// 8/16-B buffer stores, every storing wave drains vmcnt(0), the workgroup barrier,
-// then ONE lane's relaxed agent-scope store of the version / ready word; consumers
-// poll with relaxed agent loads (sc1) and read every handed-off byte with sc1
-// buffer loads (no acquire fence needed).  Every wait is bounded: on a give-up the
-// workgroup records err and info and leaves.
-typedef __attribute__((address_space(1))) int gint;
-constexpr int kSc1 = 16;                 // buffer instruction aux bits: sc1
-constexpr uint32_t kSpinLimit = 1u << 22;  // polls (~s_sleep 2 each) before a wait gives up
-
-// sc1 buffer accesses: voff = this lane's part of the offset (a VGPR), soff = the
-// wave-uniform part (an SGPR: tile origin + compile-time element offsets)
-__device__ __forceinline__ double2 ld16c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kSc1));
-}
-__device__ __forceinline__ double ld8c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kSc1));
-}
-__device__ __forceinline__ void st16c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x, double y) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, make_double2(x, y)), r, voff, soff, kSc1);
-}
-__device__ __forceinline__ void st8c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
-  typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, x), r, voff, soff, kSc1);
-}
-// Lane offsets (bytes) of the two access patterns within a tile of leading dimension ld:
-//   pair pattern (tile_fetch / tile_store): element (tid / 32 + 8 it, 2 (tid % 32)), soff += 64 it ld
-//   row-stripe accumulator pattern (Blk4, blk4_foreach<true>): (16 w + lane / 16 + 4 q, 16 t + lane % 16)
-__device__ __forceinline__ uint32_t lane_off_pair(int64_t ld) {
-  return (uint32_t)((((int)threadIdx.x >> 5) * ld + (threadIdx.x & 31) * 2) * 8);
-}
-__device__ __forceinline__ uint32_t lane_off_row(int64_t ld) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  return (uint32_t)(((16 * w + (lane >> 4)) * ld + (lane & 15)) * 8);
-}
-// 64x64 f64 tile at byte offset `off` (leading dimension ld doubles), sc1 loads
-__device__ __forceinline__ void tile_fetch_c(TileRegs& t, __amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld) {
-  const uint32_t v = lane_off_pair(ld);
-#pragma unroll
-  for (int it = 0; it < 8; ++it) t.v[it] = ld16c(r, v, off + (uint32_t)(it * 64 * ld));
-}
-__device__ __forceinline__ void row_from_global_c(Blk4& u, __amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld) {
-  const uint32_t v = lane_off_row(ld);
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) u.c[t][q] = ld8c(r, v, off + (uint32_t)((4 * q * ld + 16 * t) * 8));
-}
-__device__ __forceinline__ void row_to_global_c(__amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld, const Blk4& u) {
-  const uint32_t v = lane_off_row(ld);
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) st8c(r, v, off + (uint32_t)((4 * q * ld + 16 * t) * 8), u.c[t][q]);
-}
-__device__ __forceinline__ void tile_store_c(__amdgpu_buffer_rsrc_t r, uint32_t off, int64_t ld, const double* s) {
-  const uint32_t v = lane_off_pair(ld);
-  const int rr = threadIdx.x >> 5, c = (threadIdx.x & 31) * 2;
-#pragma unroll
-  for (int it = 0; it < 8; ++it)
-    st16c(r, v, off + (uint32_t)(it * 64 * ld), s[(rr + 8 * it) * LDT + c], s[(rr + 8 * it) * LDT + c + 1]);
-}
-__device__ __forceinline__ int flag_load(const int* p) {
-  return __hip_atomic_load((gint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void flag_store(int* p, int v) {
-  __hip_atomic_store((gint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// All threads: wait until every word p[k] >= v[k] (k < n <= 4; one lane polls each),
-// then the workgroup barrier.  Returns false (uniformly) when a wait gave up.
-__device__ __forceinline__ bool wait_all(const int* const (&p)[4], const int (&v)[4], int n, int* err,
-                                         int* s_flag) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const int* mp = p[0];
-    int mv = v[0];
-#pragma unroll
-    for (int k = 1; k < 4; ++k)
-      if (lane == k) { mp = p[k]; mv = v[k]; }
-    bool ok = true;
-    for (uint32_t it = 0;; ++it) {
-      const bool mine = lane >= n || flag_load(mp) >= mv;
-      if (__all(mine)) break;
-      if (it >= kSpinLimit || flag_load(err) != 0) {
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (lane == 0) {
-      *s_flag = ok ? 1 : 0;
-      if (!ok) __hip_atomic_store((gint*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
   __syncthreads();
-  const bool ok = *s_flag != 0;
-  __syncthreads();
-  return ok;
-}
-
-// All threads: one poll of the words (no wait); true (uniformly) when every p[k] >= v[k].
-__device__ __forceinline__ bool poll_all(const int* const (&p)[4], const int (&v)[4], int n, int* s_flag) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const int* mp = p[0];
-    int mv = v[0];
-#pragma unroll
-    for (int k = 1; k < 4; ++k)
-      if (lane == k) { mp = p[k]; mv = v[k]; }
-    const bool mine = lane >= n || flag_load(mp) >= mv;
-    const bool all = __all(mine);
-    if (lane == 0) *s_flag = all ? 1 : 0;
-  }
-  __syncthreads();
-  const bool ok = *s_flag != 0;
-  __syncthreads();
-  return ok;
-}
-
-// every storing wave drains its sc1 stores, then one lane publishes `v` at p
-__device__ __forceinline__ void publish(int* p, int v) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) flag_store(p, v);
-}
-
-__global__ __launch_bounds__(kCholThreads) void chol_persist(CholArgs a) {
-  __shared__ double bufA[CB * LDT], bufB[CB * LDT], bufC[CB * LDT], col[CB];
-  __shared__ int s_task, s_flag;
-  const int b = blockIdx.y, nb = a.nb;
-  const int64_t Mp = a.Mp;
-  int* sync = a.sync + (int64_t)b * a.strideSync;
-  int* Wver = sync;
-  int* Bver = sync + nb * nb;
-  int* Dready = sync + 2 * nb * nb;
-  int* head = Dready + nb;
-  int* err = head + 1;
-  const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)ws_W(a, b), (short)0, (int)(uint32_t)(a.strideWS * 8), 0x00020000);
-  auto offW = [&](int i, int l) { return (uint32_t)(((int64_t)i * CB * Mp + (int64_t)l * CB) * 8); };
-  auto offB = [&](int i, int c) { return (uint32_t)((Mp * Mp + (int64_t)i * CB * Mp + (int64_t)c * CB) * 8); };
-  auto offD = [&](int j) { return (uint32_t)((2 * Mp * Mp + (int64_t)j * CB * CB) * 8); };
-  float* LinvT = a.LinvT + (int64_t)b * a.strideL;
-  float* lt_max = a.lt_absmax[0];
-#pragma unroll
-  for (int q = 1; q < kMaxBatch; ++q)
-    if (b == q) lt_max = a.lt_absmax[q];
-  auto store_linvT = [&](int c, int j, const double* sx) {  // X_jc -> LinvT block (c, j)
-    const int64_t gr = (int64_t)c * CB, gc = (int64_t)j * CB;
-    const float m = tile_store_f32_v4(LinvT + gr * a.ldl + gc, a.ldl, sx, true, (int)min<int64_t>(CB, a.M - gr),
-                                      (int)min<int64_t>(CB, a.M - gc));
-    if (lt_max) wave_absmax_atomic(m, lt_max);
-  };
-  auto store_L = [&](int i, int j, const double* s) {     // L block (i, j), float32
-    if (!a.L) return;
-    const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
-    tile_store_f32_v4(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s, false,
-                      (int)min<int64_t>(CB, a.M - gr), (int)min<int64_t>(CB, a.M - gc));
-  };
-  auto give_up = [&]() {
-    if (threadIdx.x == 0) atomicCAS(a.info + b, 0, -1);
-  };
-
-  if (blockIdx.x == 0) {
-    // ---------------------------------------------------------------- chain
-    double *sD = bufA, *s1 = bufB, *s2 = bufC;
-    {
-      TileRegs rD;
-      tile_fetch_c(rD, R, offD(0), CB);
-      tile_put(sD, rD);
-      __syncthreads();
-      store_linvT(0, 0, sD);                             // X_00 = D_0
-    }
-    for (int j = 0; j + 1 < nb; ++j) {
-      PSTAMP(b, j, 0);
-      const int* p[4] = {Wver + (j + 1) * nb + j, Wver + (j + 1) * nb + j + 1, Wver, Wver};
-      const int v[4] = {j, j, 0, 0};
-      if (!wait_all(p, v, 2, err, &s_flag)) { give_up(); return; }
-      PSTAMP(b, j, 1);
-      TileRegs r1, r2;
-      tile_fetch_c(r1, R, offW(j + 1, j), Mp);
-      tile_fetch_c(r2, R, offW(j + 1, j + 1), Mp);
-      tile_put(s1, r1);
-      tile_put(s2, r2);
-      __syncthreads();
-      PSTAMP(b, j, 2);
-      Blk4 pi = blk4_zero();
-      row_mma<true, 1>(pi, s1, sD, 1.0);                 // L_{j+1,j} = W_{j+1,j} D_j^T
-      row_to_global_c(R, offW(j + 1, j), Mp, pi);        // handed to the U tasks of column j + 1
-      __syncthreads();
-      blk4_to_lds<true>(s1, pi);
-      __syncthreads();
-      // column block 0 of W_{j+1,j+1} -= P P^T (one 16x16 block per wave); the rest
-      // beside the first panel sweep (factor_diag_tile's pending update).  The
-      // L_{j+1,j} stores drain meanwhile.
-      sub_outer_blk<4>(s2, 16 * (threadIdx.x >> 6), 0, s1, s1);
-      publish(Wver + (j + 1) * nb + j, j + 1);
-      __syncthreads();
-      PSTAMP(b, j, 3);
-      store_L(j + 1, j, s1);
-      factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1);
-      __syncthreads();
-      PSTAMP(b, j, 4);
-      tile_store_c(R, offD(j + 1), CB, s1);              // D_{j+1}, handed to the workers
-      publish(Dready + j + 1, 1);
-      PSTAMP(b, j, 5);
-      store_L(j + 1, j + 1, s2);
-      store_linvT(j + 1, j + 1, s1);                     // X_{j+1,j+1} = D_{j+1}
-      __syncthreads();
-      PSTAMP(b, j, 6);
-      double* t = sD; sD = s1; s1 = t;                   // D_{j+1} stays in LDS
-    }
-    return;
-  }
-
-  // ------------------------------------------------------------------ workers
-  // Software-pipelined: the next task is dequeued while the current one's tiles load,
-  // and its tiles are loaded (when its inputs are already published) while the
-  // current one computes.  A task's operands: tile 1 -> s1, tile 2 -> s2 (optional),
-  // the read-modify-write tile in registers (optional), D_j -> sD (cached per step).
-  double *s1 = bufA, *s2 = bufB, *sD = bufC;
-  int dcur = -1;                                         // the step whose D is in sD
-  struct Plan { int kind, j, i, l; uint32_t o1, o2, ou; bool t2, u, d; };
-  auto decode = [&](int t, Plan& P) {
-    const int code = a.tasks[t];
-    P.kind = code >> 24; P.j = (code >> 16) & 255; P.i = (code >> 8) & 255; P.l = code & 255;
-    const int j = P.j, i = P.i, l = P.l;
-    P.t2 = P.u = P.d = false;
-    P.o2 = P.ou = 0;
-    if (P.kind == kTaskPan) { P.o1 = offW(i, j); P.d = true; }
-    else if (P.kind == kTaskU) {
-      P.o1 = offW(i, j); P.t2 = true;
-      if (l != i) { P.o2 = offW(l, j); P.u = true; P.ou = offW(i, l); }
-      else P.o2 = offW(i, i);
-    } else if (P.kind == kTaskXR) { P.o1 = offB(j, l); P.d = true; }
-    else {
-      P.o1 = offW(i, j);
-      if (l < j) { P.t2 = true; P.o2 = offB(j, l); P.u = true; P.ou = offB(i, l); }
-      else P.d = true;
-    }
-  };
-  auto deps = [&](const Plan& P, const int* (&p)[4], int (&v)[4]) {
-    const int j = P.j, i = P.i, l = P.l;
-    for (int k = 0; k < 4; ++k) { p[k] = Wver; v[k] = 0; }
-    if (P.kind == kTaskPan) {
-      p[0] = Dready + j; v[0] = 1; p[1] = Wver + i * nb + j; v[1] = j;
-      return 2;
-    }
-    if (P.kind == kTaskU) {
-      p[0] = Wver + i * nb + j; v[0] = j + 1; p[1] = Wver + i * nb + l; v[1] = j;
-      p[2] = Wver + l * nb + j; v[2] = j + 1;
-      return (l != i) ? 3 : 2;
-    }
-    if (P.kind == kTaskXR) {
-      p[0] = Dready + j; v[0] = 1; p[1] = Bver + j * nb + l; v[1] = j - l;
-      return 2;
-    }
-    p[0] = Wver + i * nb + j; v[0] = j + 1;
-    if (l < j) {
-      p[1] = Bver + j * nb + l; v[1] = j - l + 1; p[2] = Bver + i * nb + l; v[2] = j - l;
-      return 3;
-    }
-    p[1] = Dready + j; v[1] = 1;
-    return 2;
-  };
-  struct Regs { TileRegs r1, r2; Blk4 u; };
-  auto issue = [&](const Plan& P, Regs& G) {
-    tile_fetch_c(G.r1, R, P.o1, Mp);
-    if (P.t2) tile_fetch_c(G.r2, R, P.o2, Mp);
-    if (P.u) row_from_global_c(G.u, R, P.ou, Mp);
-  };
-  auto dequeue = [&]() {
-    if (threadIdx.x == 0) s_task = atomicAdd(head, 1);
-    __syncthreads();
-    const int t = s_task;
-    __syncthreads();
-    return t;
-  };
-
-  int tc = dequeue();
-  if (tc >= a.ntask) return;
-  Plan P;
-  decode(tc, P);
-  Regs G;
-  {
-    const int* p[4];
-    int v[4];
-    const int n = deps(P, p, v);
-    if (!wait_all(p, v, n, err, &s_flag)) { give_up(); return; }
-    issue(P, G);
-  }
-  const int wid = blockIdx.x;
-  for (;;) {
-    unsigned long long c0 = PNOW();
-    const int tn = dequeue();                            // overlaps the loads in flight
-    unsigned long long c1 = PNOW();
-    PWACC(b, wid, 0, c1 - c0);
-    if (P.d && dcur != P.j) {
-      TileRegs rD;
-      tile_fetch_c(rD, R, offD(P.j), CB);
-      tile_put(sD, rD);
-      dcur = P.j;
-      PWACC(b, wid, 7, 1);
-    }
-    tile_put(s1, G.r1);
-    if (P.t2) tile_put(s2, G.r2);
-    Blk4 u = P.u ? G.u : blk4_zero();
-    __syncthreads();
-    unsigned long long c2 = PNOW();
-    PWACC(b, wid, 2, c2 - c1);
-    // the next task's operands, in flight during this task's MFMAs (when published)
-    Plan Q;
-    bool have = tn < a.ntask, issued = false;
-    const int* pq[4];
-    int vq[4], nq = 0;
-    if (have) {
-      decode(tn, Q);
-      nq = deps(Q, pq, vq);
-      if (poll_all(pq, vq, nq, &s_flag)) { issue(Q, G); issued = true; }
-    }
-    unsigned long long c3 = PNOW();
-    PWACC(b, wid, 3, c3 - c2);
-    PWACC(b, wid, 6, issued ? 1 : 0);
-    PWACC(b, wid, 5, 1);
-    const int j = P.j, i = P.i, l = P.l;
-    if (P.kind == kTaskPan) {                            // L_ij = W_ij D_j^T in place
-      Blk4 pi = blk4_zero();
-      row_mma<true, 1>(pi, s1, sD, 1.0);
-      row_to_global_c(R, offW(i, j), Mp, pi);
-      __syncthreads();
-      blk4_to_lds<true>(s1, pi);
-      publish(Wver + i * nb + j, j + 1);
-      __syncthreads();
-      store_L(i, j, s1);
-    } else if (P.kind == kTaskU && l != i) {             // W_il -= L_ij L_lj^T
-      row_mma<true, 0>(u, s1, s2, -1.0);
-      row_to_global_c(R, offW(i, l), Mp, u);
-      publish(Wver + i * nb + l, j + 1);
-    } else if (P.kind == kTaskU) {                       // lower blocks of W_ii -= L_ij L_ij^T
-      diag_lower_update(s2, s1);
-      __syncthreads();
-      tile_store_c(R, offW(i, i), Mp, s2);
-      publish(Wver + i * nb + i, j + 1);
-    } else if (P.kind == kTaskXR) {                      // X_jc = D_j B_jc in place, LinvT block (c, j)
-      Blk4 x = blk4_zero();
-      col_mma_lower(x, sD, s1);
-      __syncthreads();
-      blk4_to_lds<false>(s1, x);
-      __syncthreads();
-      tile_store_c(R, offB(j, l), Mp, s1);
-      publish(Bver + j * nb + l, j - l + 1);
-      store_linvT(l, j, s1);
-    } else {                                             // FU: B_ic -= L_ij X_jc (X_jj = D_j)
-      if (l < j) row_mma<false, 0>(u, s1, s2, -1.0);
-      else row_mma<false, 2>(u, s1, sD, -1.0);
-      row_to_global_c(R, offB(i, l), Mp, u);
-      publish(Bver + i * nb + l, j - l + 1);
-    }
-    __syncthreads();
-    unsigned long long c4 = PNOW();
-    PWACC(b, wid, 4, c4 - c3);
-    if (!have) break;
-    if (!issued) {
-      if (!wait_all(pq, vq, nq, err, &s_flag)) { give_up(); return; }
-      issue(Q, G);
-    }
-    PWACC(b, wid, 1, PNOW() - c4);
-    P = Q;
-  }
+  if (diag) tile_store_f64(Wt(i, i), Mp, sT);
 }
 
 // ------------------------------------------------------------------ Cholesky backward
@@ -1676,51 +1107,12 @@ static int64_t chol_ws_doubles_per_batch(int64_t M) {
 extern "C" int mgp_dbg_chol_stamps(unsigned long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
 }
-extern "C" int mgp_dbg_persist_stamps(unsigned long long* chain, unsigned long long* work, int reset) {
-  if (reset) {
-    static unsigned long long zeros[2 * 128 * 8] = {};
-    hipMemcpyToSymbol(HIP_SYMBOL(g_pchain), zeros, sizeof(zeros));
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_pwork), zeros, sizeof(zeros));
-  }
-  hipMemcpyFromSymbol(chain, HIP_SYMBOL(g_pchain), sizeof(g_pchain));
-  return (int)hipMemcpyFromSymbol(work, HIP_SYMBOL(g_pwork), sizeof(g_pwork));
-}
 #endif
 
-static int64_t chol_task_ints(int nb) { return ((int64_t)task_count(nb) + 63) / 64 * 64; }
-
-// doubles of every batch entry, then the persistent path's sync words (per batch)
-// and its task table (shared)
+// the doubles of every batch entry (W, B, D; chol_ws_doubles_per_batch)
 extern "C" size_t mgp_chol_workspace_bytes(int64_t M, int32_t batch) {
   if (M <= 0 || batch <= 0) return 0;
-  const int nb = (int)(chol_mp(M) / CB);
-  return (size_t)chol_ws_doubles_per_batch(M) * (size_t)batch * sizeof(double) +
-         (size_t)(chol_sync_words(nb) * batch + chol_task_ints(nb)) * sizeof(int);
-}
-
-// Persistent launch (chol_persist) with MGP_CHOL_PERSIST=1 (measured at c3: 0.27-0.28 ms
-// standalone at 48-64 workers per layer against 0.28 ms for the per-step launches, 445 vs
-// 434 us in the ELBO step -- the chain -> worker -> chain hand-offs of every step cost what
-// the launch boundaries did); sizes it supports: task codes hold 8-bit tile
-// indices, the per-batch buffer resource 31-bit offsets.
-static bool chol_persist_ok(int nb, int64_t strideWS) {
-  const char* e = getenv("MGP_CHOL_PERSIST");   // read per call (tuning runs switch it in-process)
-  const int env = e ? atoi(e) : 0;
-  return env != 0 && nb >= 3 && nb <= 128 && strideWS * 8 < ((int64_t)1 << 31);
-}
-// Worker workgroups per batch entry (MGP_CHOL_WORKERS overrides)
-static int chol_persist_workers(int nb) {
-  const char* e = getenv("MGP_CHOL_WORKERS");
-  const int env = e ? atoi(e) : 0;
-  if (env > 0) return env;
-  return std::min(48, std::max(2, 2 * nb));
-}
-
-// Per-step launches on tile pairs (chol_step_pair, default) or one tile per workgroup
-// (chol_step, MGP_CHOL_PAIR=0; read per call).
-static bool chol_pair_enabled() {
-  const char* e = getenv("MGP_CHOL_PAIR");
-  return e ? atoi(e) != 0 : true;
+  return (size_t)chol_ws_doubles_per_batch(M) * (size_t)batch * sizeof(double);
 }
 
 static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s,
@@ -1734,13 +1126,6 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
   a.nb = (int)(a.Mp / CB);
   a.strideWS = chol_ws_doubles_per_batch(a.M);
   a.ws = (double*)workspace;
-  const bool persist = chol_persist_ok(a.nb, a.strideWS);
-  if (persist) {
-    a.strideSync = chol_sync_words(a.nb);
-    a.sync = (int*)((char*)workspace + (size_t)a.strideWS * batch * sizeof(double));
-    a.tasks = a.sync + a.strideSync * batch;
-    a.ntask = task_count(a.nb);
-  }
   const dim3 block(kCholThreads);
   hipLaunchKernelGGL(chol_prep, dim3(a.nb * a.nb + 1, batch), block, 0, s, a);
   int st = launch_status();
@@ -1749,21 +1134,12 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
     st = hip_status(hipEventRecord(prep_done, s));
     if (st) return st;
   }
-  if (persist) {
-    hipLaunchKernelGGL(chol_persist, dim3(1 + chol_persist_workers(a.nb), batch), block, 0, s, a);
-    return launch_status();
-  }
-  const bool pair = chol_pair_enabled();
   for (int j = 0; j < a.nb; ++j) {
     const int T = a.nb - j - 1;
-    if (pair && T > 0) {
+    if (T > 0)
       hipLaunchKernelGGL(chol_step_pair, dim3(1 + step_pair_count(a.nb, j), batch), dim3(kPairThreads), 0, s, a, j);
-      st = launch_status();
-      if (st) return st;
-      continue;
-    }
-    const int n = (T == 0) ? a.nb : T * (T + 1) / 2 + T * (j + 1);
-    hipLaunchKernelGGL(chol_step, dim3(n, batch), block, 0, s, a, j);
+    else
+      hipLaunchKernelGGL(chol_last_step, dim3(a.nb, batch), block, 0, s, a, j);
     st = launch_status();
     if (st) return st;
   }

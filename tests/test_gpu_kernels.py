@@ -38,19 +38,8 @@ def test_rbf_kuf_kuu(device, N, M, D, ard):
     assert np.array_equal(Kuu, Kuu.T)
 
 
-@pytest.fixture(params=["steps", "tiles", "persist"])
-def chol_path(request, monkeypatch):
-    """K3's launch structures: one launch per panel step with two tiles per workgroup
-    (default, chol_step_pair), the same with one tile per workgroup (chol_step,
-    MGP_CHOL_PAIR=0), and the single persistent launch (chol_persist, MGP_CHOL_PERSIST=1);
-    the library reads both switches per call."""
-    monkeypatch.setenv("MGP_CHOL_PERSIST", "1" if request.param == "persist" else "0")
-    monkeypatch.setenv("MGP_CHOL_PAIR", "0" if request.param == "tiles" else "1")
-    return request.param
-
-
 @pytest.mark.parametrize("M,batch", [(1, 1), (25, 2), (64, 1), (100, 2), (256, 2), (1024, 2)])
-def test_potrf_trtri(device, M, batch, chol_path):
+def test_potrf_trtri(device, M, batch):
     from modulatedgps_amd import ops
     rng = np.random.default_rng(M)
     As = []
@@ -74,7 +63,7 @@ def test_potrf_trtri(device, M, batch, chol_path):
         assert normwise(Lt.T, Li) < tol
 
 
-def test_potrf_reports_non_spd(device, chol_path):
+def test_potrf_reports_non_spd(device):
     from modulatedgps_amd import ops
     M = 130
     A = np.eye(M)
@@ -128,7 +117,7 @@ def test_kuu_factorisation_matches_float64(device):
 
 
 @pytest.mark.parametrize("M", [300, 1024])
-def test_kuu_linvt_bound_and_bounded_split(device, M, chol_path):
+def test_kuu_linvt_bound_and_bounded_split(device, M):
     """mgp_kuu_potrf_trtri_ex: K3 writes max |LinvT| into the L^-T images' trailers
     (bit-exact vs the reduction of the written LinvT), and the bounded split then
     gives the same split-f16 image as mgp_split_upper_f16's own reduction."""
@@ -154,7 +143,7 @@ def test_kuu_linvt_bound_and_bounded_split(device, M, chol_path):
 
 
 @pytest.mark.parametrize("M,dup", [(1024, 0.0), (1024, 1e-3), (700, 1e-2)])
-def test_kuu_factorisation_ill_conditioned(device, M, dup, chol_path):
+def test_kuu_factorisation_ill_conditioned(device, M, dup):
     """K3 on badly conditioned Kuu (inducing points with near-duplicates, cond up
     to ~1e9): L and L^-1 against float64 LAPACK, to float32 output rounding
     amplified by at most cond(L) eps64."""

@@ -64,3 +64,11 @@ def test_jitter_argument_is_validated():
     c = ctypes.c_void_p(8)
     rc = lib.mgp_elbo_terms(c, c, c, c, 4, c, c, 4, 2, 3, 0.01, -1.0, None, None, 0, 0, c, c, 64, None)
     assert rc == -14
+
+
+def test_library_reads_no_environment():
+    """the only process-global state is the lazily loaded code object --
+    kernel choices follow from the entry point and its arguments, so the library
+    imports no getenv (round 4 removed its per-call variant switches)."""
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"getenv\x00" not in data
