@@ -100,10 +100,12 @@ def set_expert_cross(cross):
 #              stream beside K3 (round 1-3 default);
 #   "k1a_late" the assign layer's K1 on the side stream after K3, beside the pred
 #              layer's K4 (one K1 beside the chain instead of two);
+#   "k1a_k5"   as k1a_late, but the layers run K4, K5 of the pred layer before the
+#              assign layer's K4, so that K1 runs beside the MFMA-bound K5;
 #   "k1_main"  both K1 on the main stream after K3 (only the small images and
 #              the KL beside the chain);
 #   "serial"   everything on the main stream, K3 alone on the chip.
-STEP_SCHEDULES = ("overlap", "k1a_late", "k1_main", "serial")
+STEP_SCHEDULES = ("overlap", "k1a_late", "k1a_k5", "k1_main", "serial")
 
 
 def step_schedule():

@@ -52,9 +52,13 @@ __device__ unsigned long long g_stamps[64 * 16];
 #define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 // 100 MHz reference clock (one time base for every CU): slots 14 / 15
 #define RSTAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// one pair workgroup per step (the first pair of the last tile row, batch 0): phase stamps
+__device__ unsigned long long g_pair_stamps[64 * 8];
+#define PAIRSTAMP(on, j, k) do { if ((on) && threadIdx.x == 0) g_pair_stamps[(j) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define STAMP(j, k) do {} while (0)
 #define RSTAMP(j, k) do {} while (0)
+#define PAIRSTAMP(on, j, k) do {} while (0)
 #endif
 
 struct CholArgs {
@@ -743,6 +747,8 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     return a.A ? input_elem(a, b, gr, gc) : kuu_elem(a, Zb, sil, varb, gr, gc);
   };
   if (blockIdx.x == 0) {  // factor tile (0, 0) straight from the input (dispatched first)
+    STAMP(63, 0);
+    RSTAMP(63, 14);
     if (threadIdx.x == 0) {
       a.info[b] = 0;
       float* lt = a.lt_absmax[0];
@@ -756,9 +762,13 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
       s1[r * LDT + c] = elem(r, c);
     }
     __syncthreads();
+    STAMP(63, 1);
     factor_diag_tile(s1, s2, col, a.info + b, 0);
     __syncthreads();
+    STAMP(63, 2);
     write_diag(a, b, 0, s1, s2);
+    STAMP(63, 3);
+    RSTAMP(63, 15);
     return;
   }
   const int bi = (blockIdx.x - 1) / a.nb, bl = (blockIdx.x - 1) % a.nb;
@@ -879,25 +889,35 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     if (lt_max) wave_absmax_atomic(m, lt_max);
   };
   int i = j + 1;
-  if (blockIdx.x == 0) {  // look-ahead: tile (j+1, j+1) on group 0; group 1's waves take part
-    const bool act = g == 0;  // in every barrier and do no work (uniform barrier sequence)
+  if (blockIdx.x == 0) {
+    // look-ahead: tile (j+1, j+1).  Both groups load and form P = W_{j+1,j} D_j^T (group 0
+    // column blocks 0 and 3, group 1 blocks 1 and 2: equal MFMA counts, as the pairs'
+    // P_i); the factorisation then runs on group 0 while group 1's waves take part in
+    // every barrier and do no work (uniform barrier sequence)
+    const bool act = g == 0;
     RSTAMP(j, 14);
     STAMP(j, 0);
     TileRegs r1, rD, r2;
     if (act) {
       tile_fetch(r1, Wt(i, j), Mp);
       tile_fetch(rD, ws_D(a, b, j), CB);
+    } else {
       tile_fetch(r2, Wt(i, i), Mp);
+    }
+    if (act) {
       tile_put(s1, r1);
       tile_put(sD, rD);
+    } else {
       tile_put(s2[0], r2);
     }
     __syncthreads();
     STAMP(j, 1);
     Blk4 pi = blk4_zero();
-    if (act) row_mma<true, 1>(pi, s1, sD, 1.0);
+    if (act) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);
+    else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
     __syncthreads();
-    if (act) blk4_to_lds<true>(s1, pi);
+    if (act) blk4_to_lds<true, 0x9>(s1, pi);
+    else blk4_to_lds<true, 0x6>(s1, pi);
     __syncthreads();
     STAMP(j, 2);
     lookahead_factor(a, b, j, s1, s2[0], col, act);
@@ -913,6 +933,8 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   }
   const int e = 2 * q + g;
   const bool has = e < nt;  // an odd row's last pair: group 1 has no tile (it forms its half of P_i)
+  const bool pst = i == a.nb - 1 && q == 0 && blockIdx.y == 0;   // debug stamps only
+  PAIRSTAMP(pst, j, 0);
   const int nupd = (i == j + 1) ? 0 : i - j;
   const bool upd = has && e < nupd;
   const int l = j + 1 + e, c = e - nupd;
@@ -943,6 +965,7 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   }
   if (upd || fwd) tile_put(sT, r2);
   __syncthreads();
+  PAIRSTAMP(pst, j, 1);
   // P_i's column blocks split over the groups with equal MFMA counts (D_j^T upper:
   // block tj takes 4 (tj + 1) k-steps): group 0 blocks 0 and 3, group 1 blocks 1 and 2;
   // each group then forms its tile's own first product
@@ -954,10 +977,12 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     else col_mma_lower(t, sD, sT);               // X_jc = D_j B_jc
   }
   __syncthreads();
+  PAIRSTAMP(pst, j, 2);
   if (g == 0) blk4_to_lds<true, 0x9>(s1, pi);
   else blk4_to_lds<true, 0x6>(s1, pi);
   if (first) upd ? blk4_to_lds<true>(sT, t) : blk4_to_lds<false>(sT, t);
   __syncthreads();
+  PAIRSTAMP(pst, j, 3);
   if (g == 0 && q == 0 && a.L) {  // L_ij, once per row
     const int64_t gr = (int64_t)i * CB, gc = (int64_t)j * CB;
     tile_store_f32(a.L + (int64_t)b * a.strideL + gr * a.ldl + gc, a.ldl, s1, false,
@@ -980,8 +1005,10 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     row_mma<false, 2>(u, s1, sD, -1.0);
     row_to_global(Bt(i, c), Mp, u);
   }
+  PAIRSTAMP(pst, j, 4);
   __syncthreads();
   if (diag) tile_store_f64(Wt(i, i), Mp, sT);
+  PAIRSTAMP(pst, j, 5);
 }
 
 // ------------------------------------------------------------------ Cholesky backward
@@ -1106,6 +1133,9 @@ static int64_t chol_ws_doubles_per_batch(int64_t M) {
 #ifdef MGP_DBG_STAMPS
 extern "C" int mgp_dbg_chol_stamps(unsigned long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
+}
+extern "C" int mgp_dbg_pair_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_stamps), sizeof(g_pair_stamps));
 }
 #endif
 

@@ -620,7 +620,8 @@ class SMGP(SGP):
                 for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
                     Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt, bounded=bounded)
         sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
-        late = {"overlap": (), "k1a_late": ("a",), "k1_main": ("f", "a"), "serial": ("f", "a")}[sched]
+        late = {"overlap": (), "k1a_late": ("a",), "k1a_k5": ("a",), "k1_main": ("f", "a"),
+                "serial": ("f", "a")}[sched]
         if b["x6"]:
             def side_work():
                 for L, layer in layers:
@@ -661,20 +662,28 @@ class SMGP(SGP):
             # costs 10-25 us of idle GPU per wait (measured)
             pf, pa = self.pred_layer, self.assign_layer
             k1a_ev = None
-            if sched == "k1a_late":   # the assign layer's K1 beside the pred layer's K4
+
+            def side_kuf_a():   # the assign layer's K1 on the side stream from here on
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     kuf_late("a")
-                k1a_ev = torch.cuda.Event()
-                k1a_ev.record(side)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                return ev
+            if sched == "k1a_late":          # beside the pred layer's K4
+                k1a_ev = side_kuf_a()
             elif sched in ("k1_main", "serial"):
                 kuf_late("f")
                 kuf_late("a")
             Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing, fmt, Tfr=Tfr["f"])
+            if sched == "k1a_k5":            # beside the pred layer's K5
+                k1a_ev = side_kuf_a()
+                pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
             if k1a_ev is not None:
                 main.wait_event(k1a_ev)
             Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt, Tfr=Tfr["a"])
-            pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
+            if sched != "k1a_k5":
+                pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
             pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)
         else:
             for L, layer in layers:

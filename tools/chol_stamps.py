@@ -60,3 +60,17 @@ for j in range(steps):
     clk = (s[7] - s[0]) / max(1, s[15] - s[14]) / 10.0
     gap = (n[14] - s[15]) * 1e-2 if n and n[14] else float("nan")
     print(f"{j:2d} wall {wall:6.2f} us  clock {clk:5.2f} GHz  gap {gap:6.2f} us")
+# one pair workgroup per step (first pair of the last tile row, batch 0): shader cycles per phase
+pb = (ctypes.c_ulonglong * (64 * 8))()
+lib.mgp_dbg_pair_stamps(pb)
+print("pair workgroup (row nb-1, pair 0): loads+stage  P_i+first  stage2  final  store  | total (shader cycles)")
+for j in range(steps - 1):
+    s = [pb[j * 8 + k] for k in range(8)]
+    if not s[0] or not s[5]:
+        continue
+    d = [s[k + 1] - s[k] for k in range(5)]
+    print(j, *d, "|", s[5] - s[0])
+p = st[63]
+if p[0]:
+    print(f"prep tile (0, 0): build {p[1] - p[0]}  factor {p[2] - p[1]}  write {p[3] - p[2]} shader cycles; "
+          f"wall {(p[15] - p[14]) * 1e-2:.2f} us; first step's look-ahead starts {(st[0][14] - p[15]) * 1e-2:.2f} us later")
