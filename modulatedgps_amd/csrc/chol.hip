@@ -746,6 +746,46 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   auto elem = [&](int64_t gr, int64_t gc) {
     return a.A ? input_elem(a, b, gr, gc) : kuu_elem(a, Zb, sil, varb, gr, gc);
   };
+  // The 64 x 64 Kuu tile (r0, c0) into dst (leading dimension ld): with Z in LDS
+  // (rows r0.. as zr[64][D], columns c0.. transposed as zc[D][64], staged in the
+  // scratch space `stage`, >= 2 * 64 * D floats) -- the same float64 arithmetic as
+  // kuu_elem, without its 2 D dependent global loads per element.
+  auto build_tile = [&](double* dst, int64_t ld, int64_t r0, int64_t c0, float* stage) {
+    if (a.A || a.D > 32) {
+      for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+        const int r = idx >> 6, c = idx & 63;
+        dst[(int64_t)r * ld + c] = elem(r0 + r, c0 + c);
+      }
+      return;
+    }
+    const int D = a.D;
+    float* zr = stage;
+    float* zc = stage + CB * D;
+    for (int idx = threadIdx.x; idx < CB * D; idx += kCholThreads) {
+      const int r = idx / D, d = idx % D;
+      zr[idx] = (r0 + r < a.M) ? Zb[(r0 + r) * a.ldz + d] : 0.f;
+      zc[d * CB + r] = (c0 + r < a.M) ? Zb[(c0 + r) * a.ldz + d] : 0.f;
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
+      const int r = idx >> 6, c = idx & 63;
+      const int64_t gr = r0 + r, gc = c0 + c;
+      double v;
+      if (gr >= a.M || gc >= a.M) {
+        v = gr == gc ? 1.0 : 0.0;
+      } else {
+        double sacc = 0.0;
+        for (int d = 0; d < D; ++d) {
+          const double diff = ((double)zr[r * D + d] - (double)zc[d * CB + c]) * sil[d];
+          sacc = fma(diff, diff, sacc);
+        }
+        v = varb * exp(-0.5 * sacc);
+        if (gr == gc) v += a.jitter;
+      }
+      dst[(int64_t)r * ld + c] = v;
+    }
+    __syncthreads();
+  };
   if (blockIdx.x == 0) {  // factor tile (0, 0) straight from the input (dispatched first)
     STAMP(63, 0);
     RSTAMP(63, 14);
@@ -757,10 +797,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
         if (b == i) lt = a.lt_absmax[i];
       if (lt) *lt = 0.f;
     }
-    for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
-      const int r = idx >> 6, c = idx & 63;
-      s1[r * LDT + c] = elem(r, c);
-    }
+    build_tile(s1, LDT, 0, 0, reinterpret_cast<float*>(s2));
     __syncthreads();
     STAMP(63, 1);
     factor_diag_tile(s1, s2, col, a.info + b, 0);
@@ -773,13 +810,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   }
   const int bi = (blockIdx.x - 1) / a.nb, bl = (blockIdx.x - 1) % a.nb;
   const int64_t r0 = (int64_t)bi * CB, c0 = (int64_t)bl * CB;
-  if (bl <= bi) {
-    double* W = ws_W(a, b) + r0 * a.Mp + c0;
-    for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
-      const int r = idx >> 6, c = idx & 63;
-      W[(int64_t)r * a.Mp + c] = elem(r0 + r, c0 + c);
-    }
-  }
+  if (bl <= bi) build_tile(ws_W(a, b) + r0 * a.Mp + c0, a.Mp, r0, c0, reinterpret_cast<float*>(s2));
   // zero L above / LinvT below the block diagonal (within M x M)
   if (bl != bi && (bl < bi || a.L)) {
     float* dst = (bl > bi ? a.L : a.LinvT) + (int64_t)b * a.strideL;
