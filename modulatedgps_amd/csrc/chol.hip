@@ -286,39 +286,63 @@ __device__ __forceinline__ Blk4 blk4_zero() {
 // B(k, j) = TB ? sb[16tj + j][k] : sb[k][16tj + j].  TRI = 0: every k; TRI = 1:
 // k < 16 (tj + 1) (B = D^T, D lower triangular: 40 of 64 MFMAs); TRI = 2:
 // k >= 16 tj (B = D, lower triangular).  BLK: the column blocks tj formed (bit tj).
+// The LDS operands of k-step s + 1 are read before the MFMAs of k-step s (two register
+// sets; round 4): the compiler had issued each k-step's reads right in front of its own
+// MFMAs and waited for them (lgkmcnt(0) after one MFMA of cover).  The sign is applied
+// at the MFMA, so the reads need no VALU op behind them; per accumulator the MFMAs run
+// in the same k order (same bits).
 template <bool TB, int TRI, int BLK = 0xF>
 __device__ __forceinline__ void row_mma(Blk4& r, const double* __restrict__ sa, const double* __restrict__ sb,
                                         double sign) {
   const int lane = ctid() & 63, w = ctid() >> 6, l16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-  for (int k0 = 0; k0 < CB; k0 += 4) {
+  auto on = [](int tj, int k0) {
+    return ((BLK >> tj) & 1) && !(TRI == 1 && k0 >= 16 * (tj + 1)) && !(TRI == 2 && k0 < 16 * tj);
+  };
+  double av[2], bv[2][4];
+  auto load = [&](int buf, int k0) {
     const int k = k0 + kq;
-    const double av = sign * sa[(16 * w + l16) * LDT + k];
+    av[buf] = sa[(16 * w + l16) * LDT + k];
 #pragma unroll
-    for (int tj = 0; tj < 4; ++tj) {
-      if (!((BLK >> tj) & 1)) continue;
-      if (TRI == 1 && k0 >= 16 * (tj + 1)) continue;
-      if (TRI == 2 && k0 < 16 * tj) continue;
-      const double bv = TB ? sb[(16 * tj + l16) * LDT + k] : sb[k * LDT + 16 * tj + l16];
-      r.c[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, r.c[tj], 0, 0, 0);
-    }
+    for (int tj = 0; tj < 4; ++tj)
+      if (on(tj, k0)) bv[buf][tj] = TB ? sb[(16 * tj + l16) * LDT + k] : sb[k * LDT + 16 * tj + l16];
+  };
+  load(0, 0);
+#pragma unroll
+  for (int st = 0; st < CB / 4; ++st) {
+    const int k0 = 4 * st, cur = st & 1;
+    if (st + 1 < CB / 4) load(cur ^ 1, k0 + 4);
+    __builtin_amdgcn_sched_barrier(0);
+    const double a = sign * av[cur];
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj)
+      if (on(tj, k0)) r.c[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv[cur][tj], r.c[tj], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // Column stripe: C[16ti + i][16w + j] += sum_k D[16ti + i][k] sb[k][16w + j] with
-// D lower triangular (k < 16 (ti + 1)): X_jc = D_j B_jc.
+// D lower triangular (k < 16 (ti + 1)): X_jc = D_j B_jc.  Operands one k-step ahead
+// as row_mma.
 __device__ __forceinline__ void col_mma_lower(Blk4& r, const double* __restrict__ sD, const double* __restrict__ sb) {
   const int lane = ctid() & 63, w = ctid() >> 6, l16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-  for (int k0 = 0; k0 < CB; k0 += 4) {
+  double bv[2], av[2][4];
+  auto load = [&](int buf, int k0) {
     const int k = k0 + kq;
-    const double bv = sb[k * LDT + 16 * w + l16];
+    bv[buf] = sb[k * LDT + 16 * w + l16];
 #pragma unroll
-    for (int ti = 0; ti < 4; ++ti) {
-      if (k0 >= 16 * (ti + 1)) continue;
-      const double av = sD[(16 * ti + l16) * LDT + k];
-      r.c[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, r.c[ti], 0, 0, 0);
-    }
+    for (int ti = 0; ti < 4; ++ti)
+      if (k0 < 16 * (ti + 1)) av[buf][ti] = sD[(16 * ti + l16) * LDT + k];
+  };
+  load(0, 0);
+#pragma unroll
+  for (int st = 0; st < CB / 4; ++st) {
+    const int k0 = 4 * st, cur = st & 1;
+    if (st + 1 < CB / 4) load(cur ^ 1, k0 + 4);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+      if (k0 < 16 * (ti + 1)) r.c[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[cur][ti], bv[cur], r.c[ti], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
