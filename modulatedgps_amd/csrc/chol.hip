@@ -412,12 +412,14 @@ template <bool TB>
 __device__ __forceinline__ void blk_mma(doublex4& acc, const double* __restrict__ sa,
                                         const double* __restrict__ sb, double sign) {
   const int lane = ctid() & 63, i = lane & 15, kq = lane >> 4;
+  double av[4], bv[4];   // all operands read before the first MFMA (one LDS wait, not four)
 #pragma unroll
-  for (int k0 = 0; k0 < 16; k0 += 4) {
-    const double av = sign * sa[i * LDT + k0 + kq];
-    const double bv = TB ? sb[i * LDT + k0 + kq] : sb[(k0 + kq) * LDT + i];
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  for (int q = 0; q < 4; ++q) {
+    av[q] = sa[i * LDT + 4 * q + kq];
+    bv[q] = TB ? sb[i * LDT + 4 * q + kq] : sb[(4 * q + kq) * LDT + i];
   }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sign * av[q], bv[q], acc, 0, 0, 0);
 }
 
 __device__ __forceinline__ doublex4 blk_load(const double* __restrict__ s) {
@@ -444,11 +446,23 @@ __device__ __forceinline__ void diag_lower_update(double* __restrict__ s, const 
     const int bj = q - bi * (bi + 1) / 2;
     doublex4 acc = blk_load(s + 16 * bi * LDT + 16 * bj);
     const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
+    // operands of the next four k-steps read before the current four MFMAs
+    double av[2][4], bv[2][4];
+    auto load = [&](int buf, int c) {
 #pragma unroll
-    for (int k0 = 0; k0 < CB; k0 += 4) {
-      const double av = -sP[(16 * bi + l16) * LDT + k0 + kq];
-      const double bv = sP[(16 * bj + l16) * LDT + k0 + kq];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      for (int q = 0; q < 4; ++q) {
+        av[buf][q] = sP[(16 * bi + l16) * LDT + 16 * c + 4 * q + kq];
+        bv[buf][q] = sP[(16 * bj + l16) * LDT + 16 * c + 4 * q + kq];
+      }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c + 1 < 4) load((c + 1) & 1, c + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[c & 1][q], bv[c & 1][q], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     blk_store(s + 16 * bi * LDT + 16 * bj, acc);
   }
@@ -459,9 +473,27 @@ __device__ __forceinline__ void diag_lower_update(double* __restrict__ s, const 
 template <int NK>
 __device__ __forceinline__ void sub_outer_blk(double* __restrict__ s, int R0, int C1, const double* __restrict__ sa,
                                               const double* __restrict__ sb) {
+  const int lane = ctid() & 63, i = lane & 15, kq = lane >> 4;
   doublex4 acc = blk_load(s + R0 * LDT + C1);
+  // the 16-deep chunks' operands one chunk ahead (two register sets), same MFMA order
+  double av[2][4], bv[2][4];
+  auto load = [&](int buf, int kk) {
 #pragma unroll
-  for (int kk = 0; kk < NK; ++kk) blk_mma<true>(acc, sa + R0 * LDT + 16 * kk, sb + C1 * LDT + 16 * kk, -1.0);
+    for (int q = 0; q < 4; ++q) {
+      av[buf][q] = sa[(R0 + i) * LDT + 16 * kk + 4 * q + kq];
+      bv[buf][q] = sb[(C1 + i) * LDT + 16 * kk + 4 * q + kq];
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    if (kk + 1 < NK) load((kk + 1) & 1, kk + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[kk & 1][q], bv[kk & 1][q], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   blk_store(s + R0 * LDT + C1, acc);
 }
 
