@@ -72,6 +72,23 @@ def test_config_expert_cross_knob():
         config.set_expert_cross(old)
 
 
+def test_config_step_schedule_knob():
+    """Launch placement of the Cholesky-independent work relative to K3
+    (config.step_schedule, host-side only): every documented schedule is accepted,
+    anything else is refused."""
+    import pytest
+    from modulatedgps_amd import config
+    old = config.step_schedule()
+    try:
+        for v in config.STEP_SCHEDULES:
+            config.set_step_schedule(v)
+            assert config.step_schedule() == v
+        with pytest.raises(ValueError):
+            config.set_step_schedule("k1_first")
+    finally:
+        config.set_step_schedule(old)
+
+
 def test_host_arrays_feed_the_demo_post_processing():
     """predict_* return HostArray (float64 numpy); the demo's numpy lines
     (demos/demo_tf2.py, reference demo_tf2.py:63-72,98-99) and `.numpy()` work."""
@@ -96,7 +113,7 @@ def test_env_config_is_validated():
                         env={**os.environ, "MGP_K5_FORMAT": "x6", "MGP_K5_PLANES": "2"})
     assert ok.returncode == 0 and ok.stdout.split() == ["x6", "2"]
     for k, v in (("MGP_K5_FORMAT", "bf8"), ("MGP_K5_PLANES", "4"), ("MGP_K5_CROSS", "x"),
-                 ("MGP_CONDITIONAL", "f64")):
+                 ("MGP_CONDITIONAL", "f64"), ("MGP_STEP_SCHEDULE", "late")):
         bad = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
                              env={**os.environ, k: v})
         assert bad.returncode != 0 and "ValueError" in bad.stderr, (k, v)
