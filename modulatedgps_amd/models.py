@@ -856,18 +856,20 @@ class SMGP(SGP):
         grads = {"lik_variance": glv} if mc is None else {}
         if alv is not None:
             grads["assign_lik_variance"] = glva
-        pending = []
-        for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
+
+        def cond_backward(L, layer, gi, ws):
             M = layer.num_inducing
             with _Stage(timing, "conditional_bwd"):
                 cimg = None
                 if "Cfr_" + L in b:  # the forward's C_k images (mgp_conditional_backward_f16c)
                     cimg = (b["Cfr_" + L], b["colmax_" + L],
                             ops.image_bound(b["Lfr_" + L], M, K=layer.num_latent_gps))
-                g = ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], layer.q_sqrt,
-                                                layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
-                                                workspace=b["ws_cbwd"], fmt=forward_image_format(True),
-                                                c_images=cimg)
+                return ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], layer.q_sqrt,
+                                                   layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
+                                                   workspace=ws, fmt=forward_image_format(True),
+                                                   c_images=cimg)
+
+        def tail_backward(L, name, layer, g):
             with _Stage(timing, "chol_bwd"):
                 gKuu = ops.chol_backward(b["L_" + L], b["LinvT_" + L], g["g_Lm"])
             with _Stage(timing, "rbf_bwd"):
@@ -879,16 +881,28 @@ class SMGP(SGP):
                                                                   device=self.device))
                 ops.rbf_backward(layer.Z, layer.Z, k.variance, k.lengthscales, gKuu, symmetric=True,
                                  accumulate=True, gZ=gZ, g_var=gvar, g_ls=gls)
-            layer_grads = {name + ".Z": gZ, name + ".variance": gvar, name + ".lengthscales": gls,
-                           name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]}
+            return {name + ".Z": gZ, name + ".variance": gvar, name + ".lengthscales": gls,
+                    name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]}
+
+        pending = []
+
+        def reduce_bucket(layer_grads):
             if process_group is not None:
-                # one bucket per layer, all-reduced while the next layer's backward runs
-                # (the first also carries the data-term sum and the likelihood gradients)
+                # one bucket per layer (the first also carries the data-term sum and the
+                # likelihood gradients); the pred layer's is in flight while the assign
+                # layer's backward still runs
                 from .distributed import allreduce_gradients_async
                 bucket = list(layer_grads.values())
                 if not pending:
                     bucket = [b["data_sum"]] + list(grads.values()) + bucket
                 pending.append(allreduce_gradients_async(bucket, group=process_group))
+
+        # the two layers in order on this stream (a side stream for one layer's Cholesky /
+        # RBF backward beside the other's conditional backward measured slower: the
+        # matrix-core kernel starves the small ones, DESIGN.md round-4 results)
+        for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
+            layer_grads = tail_backward(L, name, layer, cond_backward(L, layer, gi, b["ws_cbwd"]))
+            reduce_bucket(layer_grads)
             grads.update(layer_grads)
         if process_group is not None:
             with _Stage(timing, "allreduce"):
