@@ -405,48 +405,47 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
   // chunk), so neither role's registers are live in the other's loop.
   if (producer) {
     Regs r2, r3;
-    if (nch > 0) load(ra, 0);
-    if (nch > 1) load(rb, 1);
-    if (nch > 2) load(r2, 2);
-    if (nch > 3) load(r3, 3);
-    if (nch > 0) {
-      stash(ra, 0, 0);
-      if (nch > 4) load(ra, 4);
-    }
+    // phase of chunk c: stash it (set c % 4, buffer c % 2), load chunk c + 4 (past the
+    // data the buffer resources read zeros; never stashed), one barrier.  Full rounds
+    // of four phases in the loop, the rest after it (no exit inside the loop body, so
+    // the register sets need no copies at the back edge)
+    auto phase = [&](Regs& r, int64_t c, int buf) {
+      if (c < nch) stash(r, c, buf);
+      load(r, c + 4);
+      __syncthreads();
+    };
+    load(ra, 0);
+    load(rb, 1);
+    load(r2, 2);
+    load(r3, 3);
+    if (nch > 0) stash(ra, 0, 0);
+    load(ra, 4);
     __syncthreads();
-    for (int64_t i = 0; i < nch; i += 4) {
-      if (i + 1 < nch) {
-        stash(rb, i + 1, 1);
-        if (i + 5 < nch) load(rb, i + 5);
-      }
-      __syncthreads();
-      if (i + 1 >= nch) break;
-      if (i + 2 < nch) {
-        stash(r2, i + 2, 0);
-        if (i + 6 < nch) load(r2, i + 6);
-      }
-      __syncthreads();
-      if (i + 2 >= nch) break;
-      if (i + 3 < nch) {
-        stash(r3, i + 3, 1);
-        if (i + 7 < nch) load(r3, i + 7);
-      }
-      __syncthreads();
-      if (i + 3 >= nch) break;
-      if (i + 4 < nch) {
-        stash(ra, i + 4, 0);
-        if (i + 8 < nch) load(ra, i + 8);
-      }
-      __syncthreads();
+    int64_t c = 1;
+    for (; c + 3 <= nch; c += 4) {
+      phase(rb, c, 1);
+      phase(r2, c + 1, 0);
+      phase(r3, c + 2, 1);
+      phase(ra, c + 3, 0);
     }
+    if (c <= nch) phase(rb, c, 1);
+    if (c + 1 <= nch) phase(r2, c + 1, 0);
+    if (c + 2 <= nch) phase(r3, c + 2, 1);
     return;
   }
   __syncthreads();
-  for (int64_t i = 0; i < nch; i += 2) {
+  // chunk pairs, then the odd chunk after the loop: a break between the two halves
+  // made the compiler copy all accumulators at every back edge (64 moves behind a
+  // drained MFMA pipe per chunk pair)
+  int64_t i = 0;
+  for (; i + 1 < nch; i += 2) {
     compute(0);
     __syncthreads();
-    if (i + 1 >= nch) break;
     compute(1);
+    __syncthreads();
+  }
+  if (i < nch) {
+    compute(0);
     __syncthreads();
   }
   float* out = ws + (int64_t)z * zstride + (int64_t)b * bstride;
@@ -627,27 +626,36 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
     if (nch > 0) stash(ra, 0, 0);
     load(ra, 3);
     __syncthreads();
-    for (int64_t i = 0; i < nch; i += 6) {
-      phase(rb, i + 1, 1);
-      if (i + 1 >= nch) break;
-      phase(rc, i + 2, 0);
-      if (i + 2 >= nch) break;
-      phase(ra, i + 3, 1);
-      if (i + 3 >= nch) break;
-      phase(rb, i + 4, 0);
-      if (i + 4 >= nch) break;
-      phase(rc, i + 5, 1);
-      if (i + 5 >= nch) break;
-      phase(ra, i + 6, 0);
+    // phases of chunks 1 .. nch: full rounds of six in the loop, the rest after it
+    int64_t c = 1;
+    for (; c + 5 <= nch; c += 6) {
+      phase(rb, c, 1);
+      phase(rc, c + 1, 0);
+      phase(ra, c + 2, 1);
+      phase(rb, c + 3, 0);
+      phase(rc, c + 4, 1);
+      phase(ra, c + 5, 0);
     }
+    if (c <= nch) phase(rb, c, 1);
+    if (c + 1 <= nch) phase(rc, c + 1, 0);
+    if (c + 2 <= nch) phase(ra, c + 2, 1);
+    if (c + 3 <= nch) phase(rb, c + 3, 0);
+    if (c + 4 <= nch) phase(rc, c + 4, 1);
     return;
   }
   __syncthreads();
-  for (int64_t i = 0; i < nch; i += 2) {
+  // chunk pairs, then the odd chunk after the loop: a break between the two halves
+  // made the compiler copy all accumulators at every back edge (64 moves behind a
+  // drained MFMA pipe per chunk pair)
+  int64_t i = 0;
+  for (; i + 1 < nch; i += 2) {
     compute(0);
     __syncthreads();
-    if (i + 1 >= nch) break;
     compute(1);
+    __syncthreads();
+  }
+  if (i < nch) {
+    compute(0);
     __syncthreads();
   }
   if (e == 1 && !two) return;
