@@ -485,16 +485,19 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
   __shared__ __attribute__((aligned(16))) char sX[2][8 * kXG2], sY[2][2][8 * kXG2];
   int q, pr, z;
   {
+    // the entry pairs of a tile are adjacent (one XCD, in flight together): A's chunks
+    // are fetched into L2 once for all of them (tile-outer order fetched them once per
+    // pair, 2.85 GB per launch at c3)
     const int id = blockIdx.x, items = tiles * pairs;
     if (nsplit % 8 == 0) {
       const int x = id & 7, j = id >> 3;
       z = x + 8 * (j / items);
       const int rem = j % items;
-      q = rem % tiles;
-      pr = rem / tiles;
+      pr = rem % pairs;
+      q = rem / pairs;
     } else {
-      q = id % tiles;
-      pr = (id / tiles) % pairs;
+      pr = id % pairs;
+      q = (id / pairs) % tiles;
       z = id / items;
     }
   }
