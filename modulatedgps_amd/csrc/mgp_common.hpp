@@ -3,6 +3,8 @@
 // f32-input MFMA v_mfma_f32_32x32x2_f32.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #include "mgp_hip.h"
@@ -29,6 +31,46 @@ int mgp_launch_cond_finalize(const float* stats, int64_t lds, int nTs, const flo
 // D(32x32) += A(32x2) * B(2x32), exact f32 (fmaf chain).  Lane l supplies
 // A[i = l & 31][k = l >> 5] and B[k = l >> 5][j = l & 31].  Result register r of
 // lane l holds D[row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)][col = l & 31].
+// Cross-lane moves on gfx950's permlane swaps (VALU ops; __shfl_xor compiles to an
+// LDS-crossbar ds_bpermute whose latency every use then waits for).
+// lane_half_swap: lanes 0-31 get (a, a of lane + 32), lanes 32-63 get (b of lane - 32, b)
+// -- the two halves of an output fragment from the 16x16 accumulator layout.
+__device__ __forceinline__ void lane_half_swap(uint32_t& a, uint32_t& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void lane_half_swap(float& a, float& b) {
+  uint32_t x = __float_as_uint(a), y = __float_as_uint(b);
+  lane_half_swap(x, y);
+  a = __uint_as_float(x);
+  b = __uint_as_float(y);
+}
+// the value of lane l ^ 32 / l ^ 16
+__device__ __forceinline__ float lane_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float lane_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+}
+
+// max over the 64 lanes of a wave, every lane gets it: DPP within rows of 16 (quad
+// swaps, half-row and row mirrors pair the groups already reduced), then the
+// permlane swaps across rows (no LDS round trips)
+__device__ __forceinline__ float wave_max_f32(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));
+  };
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0xB1>{}));   // quad_perm [1, 0, 3, 2]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x4E>{}));   // quad_perm [2, 3, 0, 1]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x141>{}));  // row_half_mirror
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x140>{}));  // row_mirror
+  v = fmaxf(v, lane_xor16(v));
+  return fmaxf(v, lane_xor32(v));
+}
+
 __device__ __forceinline__ floatx16 mfma32x32x2(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -47,6 +47,15 @@
 
 namespace mgp {
 
+// Debug builds only (-DMGP_DBG_STAMPS, tools/k4_stamps.py): K4 phase times per
+// workgroup on the 100 MHz reference clock (one time base for every CU).
+#ifdef MGP_DBG_STAMPS
+__device__ unsigned long long g_k4_stamps[4096 * 8];
+#define K4STAMP(i, k) do { if (threadIdx.x == 0 && (i) >= 0 && (i) < 4096) g_k4_stamps[(i) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define K4STAMP(i, k) do {} while (0)
+#endif
+
 constexpr int kX6BM = 128;   // rows m' per item
 constexpr int kX6BN = 256;   // columns n per item
 constexpr int kFragBytes = 1024;
@@ -618,14 +627,13 @@ __global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __r
     for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const floatx4v send = lo_half ? acc[ib][2 * c + 1] : acc[ib][2 * c];
-        float y[4], v[8];
+        float v[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(send[r], 32, 64);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = (lo_half ? acc[ib][2 * c][r] : y[r]) * cmul;
-          v[4 + r] = (lo_half ? y[r] : acc[ib][2 * c + 1][r]) * cmul;
+        for (int r = 0; r < 4; ++r) {  // lanes 0-31: (own 2c, lane + 32's 2c); 32-63: (lane - 32's 2c + 1, own)
+          float x0 = acc[ib][2 * c][r], x1 = acc[ib][2 * c + 1][r];
+          lane_half_swap(x0, x1);
+          v[r] = x0 * cmul;
+          v[4 + r] = x1 * cmul;
         }
         store_split_f16(Ck + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, 1.f);
       }
@@ -640,8 +648,8 @@ __global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __r
     for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
       for (int r = 0; r < 4; ++r) s = fmaf(acc[ib][cb][r], acc[ib][cb][r], s);
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s += lane_xor16(s);
+    s += lane_xor32(s);
     const int64_t n = (int64_t)tn * kX6BN + 64 * w + 16 * cb + li;
     if (lane < 16 && n < N) dst[n] = s * unscale;
   }
@@ -1738,7 +1746,7 @@ __device__ __forceinline__ void trsm_stats16_item(
     uint32_t tfr_bytes, const bf16x8* __restrict__ Kfr, uint32_t kfr_bytes, int nmk, int64_t M, int64_t N,
     const float* __restrict__ q_mu, int64_t ldq, int K, bf16x8* __restrict__ Afr, float* __restrict__ stats,
     int64_t lds_, float* __restrict__ Af32, int64_t lda, const float* __restrict__ a_var,
-    const float* __restrict__ t_bound, const float* __restrict__ k_bound) {
+    const float* __restrict__ t_bound, const float* __restrict__ k_bound, int sidx = -1, int sbase = 0) {
   static_assert(KMAX <= 16, "the stats block has 16 rows");
   const int lane = threadIdx.x & 63, li = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1753,14 +1761,14 @@ __device__ __forceinline__ void trsm_stats16_item(
       sQ[idx] = qv;
       qmax = fmaxf(qmax, fabsf(qv));
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+    qmax = wave_max_f32(qmax);
     if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(sQ + 128 * KMAX), __float_as_uint(qmax));
   }
   floatx4v acc[8][4];
   x6_mainloop16<2, 2, true>(acc, sL, img_rsrc(Tfr, tfr_bytes), (uint32_t)(4 * t * nmk) * 3u * kFragBytes,
                             img_rsrc(Kfr, kfr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 0,
                             4 * t + 4, nmk);
+  K4STAMP(sidx, sbase);
   {
     const float unscale = ldexpf(1.f, -(img_exp(*t_bound) + img_exp(*k_bound)));
 #pragma unroll
@@ -1779,14 +1787,12 @@ __device__ __forceinline__ void trsm_stats16_item(
     for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const floatx4v send = lo_half ? acc[ib][2 * c + 1] : acc[ib][2 * c];
-        float y[4], v[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(send[r], 32, 64);
+        float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          v[r] = lo_half ? acc[ib][2 * c][r] : y[r];
-          v[4 + r] = lo_half ? y[r] : acc[ib][2 * c + 1][r];
+          v[r] = acc[ib][2 * c][r];
+          v[4 + r] = acc[ib][2 * c + 1][r];
+          lane_half_swap(v[r], v[4 + r]);
         }
         store_split_f16(Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, a_scale);
       }
@@ -1830,17 +1836,19 @@ __device__ __forceinline__ void trsm_stats16_item(
     for (int d = 0; d < 2; ++d)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int cs = lo_half ? 2 * c + 1 : 2 * c, co = lo_half ? 2 * c : 2 * c + 1;
-        uint32_t yh[2], yl[2];
+        // lanes 0-31: (own block 2c, lane + 32's 2c); 32-63: (lane - 32's 2c + 1, own 2c + 1)
+        uint32_t h0[2], h1[2], l0[2], l1[2];
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
-          yh[h2] = (uint32_t)__shfl_xor((int)hp[d][cs][h2], 32, 64);
-          yl[h2] = (uint32_t)__shfl_xor((int)lp[d][cs][h2], 32, 64);
+          h0[h2] = hp[d][2 * c][h2];
+          h1[h2] = hp[d][2 * c + 1][h2];
+          l0[h2] = lp[d][2 * c][h2];
+          l1[h2] = lp[d][2 * c + 1][h2];
+          lane_half_swap(h0[h2], h1[h2]);
+          lane_half_swap(l0[h2], l1[h2]);
         }
-        const u32x4v fh = lo_half ? u32x4v{hp[d][co][0], hp[d][co][1], yh[0], yh[1]}
-                                  : u32x4v{yh[0], yh[1], hp[d][co][0], hp[d][co][1]};
-        const u32x4v fl = lo_half ? u32x4v{lp[d][co][0], lp[d][co][1], yl[0], yl[1]}
-                                  : u32x4v{yl[0], yl[1], lp[d][co][0], lp[d][co][1]};
+        const u32x4v fh = u32x4v{h0[0], h0[1], h1[0], h1[1]};
+        const u32x4v fl = u32x4v{l0[0], l0[1], l1[0], l1[1]};
         bf16x8* dst = Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib0 + d) * 3) * 64 + pos;
         dst[0] = __builtin_bit_cast(bf16x8, fh);
         dst[64] = __builtin_bit_cast(bf16x8, fl);
@@ -1874,8 +1882,8 @@ __device__ __forceinline__ void trsm_stats16_item(
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           const int64_t n = (int64_t)tn * kX6BN + 64 * w + 16 * cb + li;
-          float s_a2 = a2[cb] + __shfl_xor(a2[cb], 16, 64);
-          s_a2 += __shfl_xor(s_a2, 32, 64);
+          float s_a2 = a2[cb] + lane_xor16(a2[cb]);
+          s_a2 += lane_xor32(s_a2);
           if (n < N) {
             float* dst = stats + st * (K + 1) * lds_ + n;
             if (lane < 16) dst[0] = s_a2;
@@ -1905,16 +1913,20 @@ __global__ __launch_bounds__(256, 2) void trsm_stats16_kernel(
   int p, tn;
   if (blockIdx.x == 0 && threadIdx.x == 0) *a_bound = sqrtf(*a_var);
   col_major_item(blockIdx.x, nP, nTn, p, tn);
+  const int it = blockIdx.x;  // debug stamps only
+  K4STAMP(it, 0);
   if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
   __syncthreads();
   trsm_stats16_item<KMAX>(sL, sQ, nT - 1 - p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats,
-                          lds_, Af32, lda, a_var, t_bound, k_bound);
+                          lds_, Af32, lda, a_var, t_bound, k_bound, it, 1);
+  K4STAMP(it, 2);
   if (nT - 1 - p == p) return;
   __syncthreads();
   if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
   __syncthreads();
   trsm_stats16_item<KMAX>(sL, sQ, p, tn, Tfr, tfr_bytes, Kfr, kfr_bytes, nmk, M, N, q_mu, ldq, K, Afr, stats, lds_,
-                          Af32, lda, a_var, t_bound, k_bound);
+                          Af32, lda, a_var, t_bound, k_bound, it, 3);
+  K4STAMP(it, 4);
 }
 
 }  // namespace mgp
@@ -2731,3 +2743,9 @@ extern "C" int mgp_conditional_backward_f16x8(
                               N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
                               workspace_bytes, stream, true, true);
 }
+
+#ifdef MGP_DBG_STAMPS
+extern "C" int mgp_dbg_k4_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mgp::g_k4_stamps), sizeof(mgp::g_k4_stamps));
+}
+#endif
