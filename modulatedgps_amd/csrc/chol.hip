@@ -25,7 +25,8 @@
 //            update (look-ahead), producing L_{j+1,j+1} and D_{j+1}.
 // One launch per step; every tile of a step is independent (each workgroup
 // recomputes the 64^3 panels it needs); every launch carries all `batch`
-// matrices (blockIdx.y).  nb + 1 launches per factorisation.
+// matrices (chol_prep: blockIdx.y; the step launches: step_pair_count).  nb + 1
+// launches per factorisation.
 #include <math.h>
 #include <stdlib.h>
 
@@ -49,13 +50,18 @@ __device__ __forceinline__ int ctid() { return (int)(threadIdx.x & (kCholThreads
 
 #ifdef MGP_DBG_STAMPS
 __device__ unsigned long long g_stamps[64 * 16];
-#define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 // 100 MHz reference clock (one time base for every CU): slots 14 / 15
-#define RSTAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RSTAMP(j, k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_stamps[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 // one pair workgroup per step (the first pair of the last tile row, batch 0): phase stamps
 __device__ unsigned long long g_pair_stamps[64 * 8];
 #define PAIRSTAMP(on, j, k) do { if ((on) && threadIdx.x == 0) g_pair_stamps[(j) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+// the time at kernel entry (held in a register until the workgroup knows whether it stamps)
+#define ENTRYTIME(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
+#define PAIRSTAMP_AT(on, j, k, t) do { if ((on) && threadIdx.x == 0) g_pair_stamps[(j) * 8 + (k)] = (t); } while (0)
 #else
+#define ENTRYTIME(t) do {} while (0)
+#define PAIRSTAMP_AT(on, j, k, t) do {} while (0)
 #define STAMP(j, k) do {} while (0)
 #define RSTAMP(j, k) do {} while (0)
 #define PAIRSTAMP(on, j, k) do {} while (0)
@@ -70,12 +76,18 @@ struct CholArgs {
   float* L; float* LinvT; int64_t ldl, strideL;   // L may be NULL
   int32_t* info;
   float* lt_absmax[kMaxBatch];                    // optional per batch: max |L^-T| (float bits, atomicMax)
-  double* ws; int64_t strideWS;                   // per batch: W, B [Mp][Mp], D [nb][64][64]
+  double* ws; int64_t strideWS;                   // per batch: W, B tile-major [nb][nb][64][64], D [nb][64][64]
   int64_t M, Mp; int nb;
 };
 
 __device__ __forceinline__ double* ws_W(const CholArgs& a, int b) { return a.ws + (int64_t)b * a.strideWS; }
 __device__ __forceinline__ double* ws_B(const CholArgs& a, int b) { return ws_W(a, b) + a.Mp * a.Mp; }
+// W and B are tile-major: tile (bi, bl) is 64 x 64 contiguous doubles (leading dimension
+// CB) at ((bi nb + bl) 64 64).  A row-major tile's 64 rows sit Mp doubles apart (8 KiB at
+// M = 1024), so every step launch's concurrent tile loads hit the same few HBM channels.
+__device__ __forceinline__ double* ws_tile(const CholArgs& a, double* base, int bi, int bl) {
+  return base + ((int64_t)bi * a.nb + bl) * (CB * CB);
+}
 __device__ __forceinline__ double* ws_D(const CholArgs& a, int b, int j) {
   return ws_W(a, b) + 2 * a.Mp * a.Mp + (int64_t)j * CB * CB;
 }
@@ -128,6 +140,15 @@ __device__ __forceinline__ void tile_fetch(TileRegs& t, const double* __restrict
   for (int it = 0; it < 8; ++it) {
     const int idx = ctid() + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
     t.v[it] = *reinterpret_cast<const double2*>(g + (int64_t)r * ld + c);
+  }
+}
+// tile_fetch of a block-lower-triangular tile (D_j = L_jj^-1): the 16 x 16 blocks above the
+// block diagonal are not loaded (their lanes are masked off) and come back as zeros
+__device__ __forceinline__ void tile_fetch_lower(TileRegs& t, const double* __restrict__ g, int64_t ld) {
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = ctid() + kCholThreads * it, r = idx >> 5, c = (idx & 31) * 2;
+    t.v[it] = (c >> 4) <= (r >> 4) ? *reinterpret_cast<const double2*>(g + (int64_t)r * ld + c) : double2{0.0, 0.0};
   }
 }
 __device__ __forceinline__ void tile_put(double* __restrict__ s, const TileRegs& t) {
@@ -866,7 +887,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   }
   const int bi = (blockIdx.x - 1) / a.nb, bl = (blockIdx.x - 1) % a.nb;
   const int64_t r0 = (int64_t)bi * CB, c0 = (int64_t)bl * CB;
-  if (bl <= bi) build_tile(ws_W(a, b) + r0 * a.Mp + c0, a.Mp, r0, c0, reinterpret_cast<float*>(s2));
+  if (bl <= bi) build_tile(ws_tile(a, ws_W(a, b), bi, bl), CB, r0, c0, reinterpret_cast<float*>(s2));
   // zero L above / LinvT below the block diagonal (within M x M)
   if (bl != bi && (bl < bi || a.L)) {
     float* dst = (bl > bi ? a.L : a.LinvT) + (int64_t)b * a.strideL;
@@ -917,7 +938,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j
     if (lt_max) wave_absmax_atomic(m, lt_max);
   };
   tile_load(sD, ws_D(a, b, j), CB);
-  if (c < j) tile_load(s1, Bm + (int64_t)j * CB * a.Mp + (int64_t)c * CB, a.Mp);
+  if (c < j) tile_load(s1, ws_tile(a, Bm, j, c), CB);
   __syncthreads();
   if (c < j) {   // (uniform per workgroup)
     Blk4 x = blk4_zero();
@@ -949,22 +970,52 @@ __global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j
 // l = i is the diagonal tile), then the forward-substitution tiles (i, c), c = 0 .. j.
 constexpr int kPairThreads = 2 * kCholThreads;
 __host__ __device__ inline int step_row_tiles(int i, int j) { return i == j + 1 ? j + 1 : i + 1; }
-__host__ __device__ inline int step_pair_count(int nb, int j) {
+__host__ __device__ inline int step_row_pairs(int i, int j) { return (step_row_tiles(i, j) + 1) / 2; }
+__host__ __device__ inline int step_pair_count(int nb, int j) {  // per batch entry
   int n = 0;
-  for (int i = j + 1; i < nb; ++i) n += (step_row_tiles(i, j) + 1) / 2;
+  for (int i = j + 1; i < nb; ++i) n += step_row_pairs(i, j);
   return n;
 }
-
-__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j) {
+// Workgroups of a step launch (one dimension, batch (1 + step_pair_count) of them): the
+// batch's look-ahead workgroups first (workgroup b: batch entry b), then one per pair.
+// The pairs, in the order (batch entry, tile row, pair), are cut into 8 consecutive runs,
+// and run x goes to the workgroups w with (w - batch) % 8 == x, which share an XCD under
+// the round-robin placement (speed only, nothing depends on it): a row's pairs then load
+// its panel tile W_ij into one L2 and a run's rows (of one batch entry where the run
+// does not straddle two) share the panel tiles W_lj, B_jc there.  No idle workgroups.
+__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb) {
   __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB];
-  const int b = blockIdx.y;
+  ENTRYTIME(t_entry);
+  // the kernel arguments every workgroup reads, loaded at entry as one batch of scalar
+  // loads behind one wait (the compiler had placed each at its first use: three dependent
+  // scalar-cache round trips before the first tile load)
+  asm volatile("" ::"s"(a.ws), "s"(a.strideWS), "s"(a.Mp), "s"(a.M), "s"(a.nb), "s"(a.L), "s"(a.LinvT),
+               "s"(a.ldl), "s"(a.strideL), "s"(a.info), "s"(j), "s"(batch), "s"(Pb));
+  asm volatile("" ::"s"(a.lt_absmax[0]), "s"(a.lt_absmax[1]), "s"(a.lt_absmax[2]), "s"(a.lt_absmax[3]),
+               "s"(a.lt_absmax[4]), "s"(a.lt_absmax[5]), "s"(a.lt_absmax[6]), "s"(a.lt_absmax[7]));
   const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));  // tile group
+  const int wg = blockIdx.x;
+  // workgroup -> (batch entry, tile row, pair of the row): step_pair_count
+  int b = wg, i = j + 1, q = 0;
+  if (wg >= batch) {
+    // Pb = step_pair_count(nb, j) from the host; position k in the pair order: run x
+    // starts after the runs y < x, (P - y + 7) / 8 pairs each (m + 1 for y < P % 8, else m)
+    const int P = batch * Pb, m = P >> 3, x = (wg - batch) & 7;
+    int k = ((wg - batch) >> 3) + x * m + min(x, P & 7);
+    b = k / Pb;
+    k -= b * Pb;
+    for (;; ++i) {
+      const int np = step_row_pairs(i, j);
+      if (k < np) break;
+      k -= np;
+    }
+    q = k;
+  }
   double* W = ws_W(a, b);
   double* Bm = ws_B(a, b);
   float* LinvT = a.LinvT + (int64_t)b * a.strideL;
-  const int64_t Mp = a.Mp;
-  auto Wt = [&](int bi, int bl) { return W + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
-  auto Bt = [&](int bi, int bl) { return Bm + (int64_t)bi * CB * Mp + (int64_t)bl * CB; };
+  auto Wt = [&](int bi, int bl) { return ws_tile(a, W, bi, bl); };
+  auto Bt = [&](int bi, int bl) { return ws_tile(a, Bm, bi, bl); };
   float* lt_max = a.lt_absmax[0];
 #pragma unroll
   for (int q = 1; q < kMaxBatch; ++q)
@@ -975,8 +1026,7 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
                                        (int)min<int64_t>(CB, a.M - gc));
     if (lt_max) wave_absmax_atomic(m, lt_max);
   };
-  int i = j + 1;
-  if (blockIdx.x == 0) {
+  if (wg < batch) {
     // look-ahead: tile (j+1, j+1).  Both groups load and form P = W_{j+1,j} D_j^T (group 0
     // column blocks 0 and 3, group 1 blocks 1 and 2: equal MFMA counts, as the pairs'
     // P_i); the factorisation then runs on group 0 while group 1's waves take part in
@@ -986,10 +1036,10 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     STAMP(j, 0);
     TileRegs r1, rD, r2;
     if (act) {
-      tile_fetch(r1, Wt(i, j), Mp);
-      tile_fetch(rD, ws_D(a, b, j), CB);
+      tile_fetch(r1, Wt(i, j), CB);
+      tile_fetch_lower(rD, ws_D(a, b, j), CB);
     } else {
-      tile_fetch(r2, Wt(i, i), Mp);
+      tile_fetch(r2, Wt(i, i), CB);
     }
     if (act) {
       tile_put(s1, r1);
@@ -1010,17 +1060,12 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     lookahead_factor(a, b, j, s1, s2[0], col, act);
     return;
   }
-  // pair -> (row i, tile e of the row)
-  int q = blockIdx.x - 1, nt = 0;
-  for (; i < a.nb; ++i) {
-    nt = step_row_tiles(i, j);
-    const int np = (nt + 1) / 2;
-    if (q < np) break;
-    q -= np;
-  }
+  // pair q of row i: tiles e = 2 q, 2 q + 1 of the row
+  const int nt = step_row_tiles(i, j);
   const int e = 2 * q + g;
   const bool has = e < nt;  // an odd row's last pair: group 1 has no tile (it forms its half of P_i)
-  const bool pst = i == a.nb - 1 && q == 0 && blockIdx.y == 0;   // debug stamps only
+  const bool pst = i == a.nb - 1 && q == 0 && b == 0;   // debug stamps only
+  PAIRSTAMP_AT(pst, j, 7, t_entry);
   PAIRSTAMP(pst, j, 0);
   const int nupd = (i == j + 1) ? 0 : i - j;
   const bool upd = has && e < nupd;
@@ -1032,20 +1077,21 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   TileRegs r1, rD, r2;
   Blk4 u = blk4_zero();  // B_ij is zero before step j
   if (g == 0) {
-    tile_fetch(r1, Wt(i, j), Mp);
-    tile_fetch(rD, ws_D(a, b, j), CB);
+    tile_fetch(r1, Wt(i, j), CB);
+    tile_fetch_lower(rD, ws_D(a, b, j), CB);
   }
-  if (upd) {
-    if (l != i) {
-      tile_fetch(r2, Wt(l, j), Mp);
-      row_from_global(u, Wt(i, l), Mp);
-    } else {
-      tile_fetch(r2, Wt(i, i), Mp);
-    }
-  } else if (fwd) {
-    tile_fetch(r2, Bt(j, c), Mp);
-    row_from_global(u, Bt(i, c), Mp);
-  }
+  // one fetch site per operand, its source chosen by tile kind (one site per kind had the
+  // compiler merge the kinds' pending loads and wait for most of group 0's loads before a
+  // forward-substitution tile issued its own)
+  const double* src2 = upd ? Wt(l != i ? l : i, l != i ? j : i) : fwd ? Bt(j, c) : nullptr;
+  const double* srcu = (upd && l != i) ? Wt(i, l) : fwd ? Bt(i, c) : nullptr;
+  if (src2) tile_fetch(r2, src2, CB);
+  if (srcu) row_from_global(u, srcu, CB);
+#ifdef MGP_DBG_STAMPS
+  __builtin_amdgcn_sched_barrier(0);
+  PAIRSTAMP(pst, j, 6);  // every load issued
+  __builtin_amdgcn_sched_barrier(0);
+#endif
   if (g == 0) {
     tile_put(s1, r1);
     tile_put(sD, rD);
@@ -1080,21 +1126,21 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   const bool diag = upd && l == i;
   if (upd && l != i) {
     row_mma<true, 0>(u, s1, sT, -1.0);    // W_il -= P_i P_l^T
-    row_to_global(Wt(i, l), Mp, u);
+    row_to_global(Wt(i, l), CB, u);
   } else if (diag) {                       // diagonal tile (i, i): lower blocks of W_ii -= P_i P_i^T
     diag_lower_update(sT, s1);
   } else if (fwd) {
     if (i == j + 1) store_linvT(c, sT);
     row_mma<false, 0>(u, s1, sT, -1.0);    // B_ic -= P_i X_jc
-    row_to_global(Bt(i, c), Mp, u);
+    row_to_global(Bt(i, c), CB, u);
   } else if (has) {                        // X_jj = D_j (lower triangular)
     if (i == j + 1) store_linvT(c, sD);
     row_mma<false, 2>(u, s1, sD, -1.0);
-    row_to_global(Bt(i, c), Mp, u);
+    row_to_global(Bt(i, c), CB, u);
   }
   PAIRSTAMP(pst, j, 4);
   __syncthreads();
-  if (diag) tile_store_f64(Wt(i, i), Mp, sT);
+  if (diag) tile_store_f64(Wt(i, i), CB, sT);
   PAIRSTAMP(pst, j, 5);
 }
 
@@ -1253,10 +1299,12 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
   }
   for (int j = 0; j < a.nb; ++j) {
     const int T = a.nb - j - 1;
-    if (T > 0)
-      hipLaunchKernelGGL(chol_step_pair, dim3(1 + step_pair_count(a.nb, j), batch), dim3(kPairThreads), 0, s, a, j);
-    else
+    if (T > 0) {
+      const int Pb = step_pair_count(a.nb, j);
+      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb)), dim3(kPairThreads), 0, s, a, j, batch, Pb);
+    } else {
       hipLaunchKernelGGL(chol_last_step, dim3(a.nb, batch), block, 0, s, a, j);
+    }
     st = launch_status();
     if (st) return st;
   }

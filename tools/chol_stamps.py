@@ -69,7 +69,7 @@ for j in range(steps - 1):
     if not s[0] or not s[5]:
         continue
     d = [s[k + 1] - s[k] for k in range(5)]
-    print(j, *d, "|", s[5] - s[0])
+    print(j, *d, "|", s[5] - s[0], "| entry->start", s[0] - s[7], " start->loads issued", s[6] - s[0])
 p = st[63]
 if p[0]:
     print(f"prep tile (0, 0): build {p[1] - p[0]}  factor {p[2] - p[1]}  write {p[3] - p[2]} shader cycles; "

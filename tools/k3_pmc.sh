@@ -2,8 +2,8 @@
 # durations, then one PMC pass per counter group (kernel-trace only), summarised by
 # tools/pmc_summary.py (clock-free MFMA busy + the f64 MFMA count) and the analytic count.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/k3pmc
-OUT=gpurun_out/k3pmc
+OUT=${K3PMC_OUT:-gpurun_out/k3pmc}
+mkdir -p $OUT
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o k3 -- python3 tools/bench_kernels.py --reps 3 --only kuu_chol_x2 > $OUT/trace.log 2>&1 || { echo "trace fail"; exit 1; }
 for c in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
   n=$(echo $c | cut -d' ' -f1)
