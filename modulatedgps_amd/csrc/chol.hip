@@ -966,8 +966,13 @@ __global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j
 // for the live waves of both groups wherever they are, so it still orders that group's
 // own LDS hand-off (and a group that has ended is not waited for: a barrier counts only
 // the waves that have not terminated).
-// Row i's tiles in order: the update tiles (i, l), l = j + 1 .. i (rows i > j + 1;
-// l = i is the diagonal tile), then the forward-substitution tiles (i, c), c = 0 .. j.
+// Row i's tiles in order: the heavy tiles first -- the off-diagonal update tiles (i, l),
+// l = j + 1 .. i - 1 (rows i > j + 1), then the forward-substitution tiles (i, c), c < j --,
+// then the two light ones, the diagonal tile (i, i) (rows i > j + 1) and (i, j) (X_jj = D_j,
+// one triangular product).  A heavy tile runs three products (two of them full), a light
+// one a triangular product only: with the light tiles adjacent they share a pair (a short
+// workgroup) on every row whose tile count is even, instead of each holding a heavy tile's
+// workgroup to the heavy tile's length with one group idle.
 constexpr int kPairThreads = 2 * kCholThreads;
 __host__ __device__ inline int step_row_tiles(int i, int j) { return i == j + 1 ? j + 1 : i + 1; }
 __host__ __device__ inline int step_row_pairs(int i, int j) { return (step_row_tiles(i, j) + 1) / 2; }
@@ -1067,10 +1072,14 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   const bool pst = i == a.nb - 1 && q == 0 && b == 0;   // debug stamps only
   PAIRSTAMP_AT(pst, j, 7, t_entry);
   PAIRSTAMP(pst, j, 0);
-  const int nupd = (i == j + 1) ? 0 : i - j;
-  const bool upd = has && e < nupd;
-  const int l = j + 1 + e, c = e - nupd;
-  const bool fwd = has && !upd && c < j;  // forward-substitution tile reading B_jc
+  const int nh = (i == j + 1) ? 0 : i - j - 1;  // off-diagonal update tiles of the row
+  int l = -1, c = -1;                              // update tile (i, l) or B tile (i, c)
+  if (e < nh) l = j + 1 + e;
+  else if (e < nh + j) c = e - nh;
+  else if (i > j + 1 && e == nh + j) l = i;
+  else c = j;
+  const bool upd = has && l >= 0;
+  const bool fwd = has && c >= 0 && c < j;  // forward-substitution tile reading B_jc
   const bool first = (upd && l != i) || fwd;  // P_l / X_jc before the update
   double* sT = s2[g];
   // this tile's operands: sT's tile (when it reads one) and the updated tile (u)

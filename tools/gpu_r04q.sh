@@ -1,4 +1,4 @@
-# K3 step launches: pairs of a tile row on one XCD, kernel arguments in one batch, D_j lower blocks only:
+# K3 step launches: + the two light tiles of a row in one pair:
 # K3 tests, K3 PMC (MFMA busy on the active CUs), ELBO-step A/B against the previous
 # K3 (abvar/lib_old.so), then the stamps of the debug build.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
