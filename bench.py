@@ -428,11 +428,16 @@ def main():
                               "peak": PEAK_HBM / 1e9, "frac": kuf_bytes / (ms * 1e-3) / PEAK_HBM,
                               "timing": "20 back-to-back launches after the timed steps",
                               "in_step_avg_us": st["rbf_kuf"][0] * 1e3}
+    # both layers' K4 (and K5) run as one launch each in the default schedule: a launch's
+    # algorithmic work is then twice one layer's
+    lpl = int(getattr(model, "layers_per_launch", 1))
+    trsm_flops *= lpl
+    expert_flops *= lpl
     for name, fl, peak in (("trsm_stats", trsm_flops, (PEAK_BF16_MFMA / 3 if f16 else PEAK_X6) if x6 else PEAK_F32_MFMA),
                            ("expert_cond", expert_flops, peak_k5)):
         if name in st:
             ms = st[name][0]
-            kernels[name] = {"bound": "mfma", "avg_us": ms * 1e3, "flops": fl,
+            kernels[name] = {"bound": "mfma", "avg_us": ms * 1e3, "flops": fl, "layers_per_launch": lpl,
                              "achieved": fl / (ms * 1e-3) / 1e12, "unit": "TFLOP/s",
                              "peak": peak / 1e12, "frac": fl / (ms * 1e-3) / peak}
     if "kuu_chol" in st:
@@ -445,17 +450,21 @@ def main():
             kernels[name] = {"avg_us": st[name][0] * 1e3}
 
     ek = kernels.get("expert_cond", {})
-    kname = (("expert_cond_f16x8_kernel" if f16x8 else "expert_cond16_kernel") if f16 else
+    kname = (("expert_cond_f16x8_kernel" if f16x8 else
+              ("expert_cond16_pair_kernel" if lpl == 2 else "expert_cond16_kernel")) if f16 else
              "expert_cond_x6_kernel") if x6 else "expert_cond_kernel"
     traffic, traffic_src = load_traffic(kname)
     klabel = {"expert_cond16_kernel": "expert_cond16_kernel<false> (split-f16, 16x16x32 MFMA)",
+              "expert_cond16_pair_kernel": "expert_cond16_pair_kernel<false> (split-f16, 16x16x32 MFMA, "
+                                           "both layers in one launch)",
               "expert_cond_f16x8_kernel": "expert_cond_x6_kernel<2, true, true> (split-f16 + e4m3 cross terms)"
               }.get(kname, kname)
     roofline = {"kernel": f"{klabel} (K5, L_k^T A + sum of squares, + cond_finalize)", "bound": "mfma",
                 "achieved": ek.get("achieved"), "peak": peak_k5 / 1e12,
                 "unit": "TFLOP/s", "frac": ek.get("frac"), "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_per_launch": f"K*M^2*N = {expert_flops:.4g} f32 flop",
+                "algorithmic_per_launch": f"{lpl}*K*M^2*N = {expert_flops:.4g} f32 flop" if lpl > 1 else
+                                          f"K*M^2*N = {expert_flops:.4g} f32 flop",
                 "peak_note": ("split-f16 + e4m3 cross terms: each f32 product is 1 f16 MFMA product + both "
                               "cross products at e4m3 (2x rate), peak = 2.5 PF f16 dense / 2" if f16x8 else
                               "split-f16: each f32 product is 3 f16 MFMA products, peak = 2.5 PF f16 dense / 3"

@@ -238,6 +238,30 @@ int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_
                        int64_t N, const float* q_mu, int64_t ldq, int32_t K, const float* variance,
                        void* Afr, size_t afr_bytes, float* stats, int64_t lds, float* A, int64_t lda,
                        mgp_stream_t stream);
+/* mgp_trsm_stats_f16 for batch (1 or 2) layers of equal M, N, K in one launch: the
+ * two SMGP layers' triangular solves (models.py:141-143 for pred_layer and
+ * assign_layer, one call instead of two).  Tfr, Kfr, q_mu, variance, Afr, stats
+ * (and A, if not NULL; A[b] may be NULL) are host arrays of `batch` device
+ * pointers; sizes and leading dimensions are shared.  Bit-identical to one
+ * mgp_trsm_stats_f16 call per layer.  -17: batch outside [1, 2]. */
+int mgp_trsm_stats_f16_batch(int32_t batch, const void* const* Tfr, size_t tfr_bytes, const void* const* Kfr,
+                             size_t kfr_bytes, int64_t M, int64_t N, const float* const* q_mu, int64_t ldq,
+                             int32_t K, const float* const* variance, void* const* Afr, size_t afr_bytes,
+                             float* const* stats, int64_t lds, float* const* A, int64_t lda,
+                             mgp_stream_t stream);
+/* mgp_expert_conditional_f16 (Cfr == NULL) or mgp_expert_conditional_f16c (Cfr and
+ * colmax given) for batch (1 or 2) layers of equal M, N, K: one K5 launch over both
+ * layers' items (models.py:141-143's LTA and fvar for pred_layer and assign_layer),
+ * then each layer's finalize.  Afr, Lfr, stats, variance, fmean, fvar, workspace (one
+ * per layer, mgp_expert_x6_workspace_bytes each), Cfr, colmax are host arrays of
+ * `batch` device pointers.  Bit-identical to one call per layer.  -20: batch outside
+ * [1, 2]. */
+int mgp_expert_conditional_f16_batch(int32_t batch, const void* const* Afr, size_t afr_bytes,
+                                     const void* const* Lfr, size_t lfr_bytes, const float* const* stats,
+                                     int64_t lds, const float* const* variance, int64_t M, int64_t N, int32_t K,
+                                     float* const* fmean, float* const* fvar, int64_t ldf, void* const* workspace,
+                                     size_t workspace_bytes, void* const* Cfr, size_t cfr_bytes,
+                                     const float* const* colmax, mgp_stream_t stream);
 /* mgp_trsm_stats_f16 that also writes plane 2 of A's image (e4m3 cross terms,
  * the operand of mgp_expert_conditional_f16x8).  With A == NULL plane 1 (f16 lo)
  * is not written: the image then feeds mgp_expert_conditional_f16x8 only. */

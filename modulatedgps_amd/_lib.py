@@ -140,6 +140,11 @@ SIGNATURES = {
     "mgp_x6_bound_ptr": (ctypes.c_void_p, [c_ptr, c_i64, c_i64, c_i32]),
     "mgp_trsm_stats_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                           c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "mgp_trsm_stats_f16_batch": (ctypes.c_int, [c_i32, c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64,
+                                                c_i32, c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "mgp_expert_conditional_f16_batch": (ctypes.c_int, [c_i32, c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr,
+                                                        c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
+                                                        c_ptr, c_size, c_ptr, c_ptr]),
     "mgp_trsm_stats_f16x8": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                             c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "mgp_expert_conditional_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,

@@ -184,9 +184,9 @@ __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t vof
 // fetched about once instead of once per row tile (C-writing K5 1.60 -> 1.51 ms;
 // without the C writes the row-tile-outer order is faster, 1.33 vs 1.36 ms).
 template <bool TN_OUTER = false>
-__device__ __forceinline__ void x6_item(int b, int nTn, int K, int& t, int& tn, int& k) {
+__device__ __forceinline__ void x6_item(int b, int nTn, int K, int& t, int& tn, int& k, int grid = -1) {
   if (TN_OUTER && nTn % 8 == 0) {
-    const int nT = gridDim.x / (nTn * K);
+    const int nT = (grid < 0 ? (int)gridDim.x : grid) / (nTn * K);
     const int x = b & 7, j = b >> 3;
     const int per_g = nT * K;
     t = (j % per_g) / K;
@@ -598,18 +598,17 @@ __device__ __forceinline__ void x6_mainloop16(floatx4v (&acc)[8][4], bf16x8 (*sL
 // COUT (training): C_k = L_k^T A is also written as a split-f16 B-layout image per expert,
 // (the B-layout of the images K4 writes); a fragment's lane position takes
 // 8 rows from two lanes of the 16x16 accumulator layout (one exchange across the lane halves).
-template <bool COUT = false>
-__global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __restrict__ Afr,
-                                                               const bf16x8* __restrict__ Lfr, uint32_t afr_bytes,
-                                                               uint32_t lfr_bytes, int nmk, int nmb, int nTn, int K,
-                                                               int64_t N, float* __restrict__ part, int64_t ldp,
-                                                               const float* __restrict__ a_bound,
-                                                               const float* __restrict__ l_bound,
-                                                               bf16x8* __restrict__ Cfr = nullptr, int64_t cexp = 0,
-                                                               const float* __restrict__ colmax = nullptr) {
-  __shared__ bf16x8 sL[2][4 * 2 * 3 * 64];  // [row sub-tile][k-step of pair][plane][lane position] (2 planes used)
+// One item (workgroup index b of a launch of `grid` items) of the split-f16 K5.
+template <bool COUT>
+__device__ __forceinline__ void expert_cond16_item(bf16x8 (*sL)[4 * 2 * 3 * 64], int b, int grid,
+                                                   const bf16x8* __restrict__ Afr, const bf16x8* __restrict__ Lfr,
+                                                   uint32_t afr_bytes, uint32_t lfr_bytes, int nmk, int nmb, int nTn,
+                                                   int K, int64_t N, float* __restrict__ part, int64_t ldp,
+                                                   const float* __restrict__ a_bound,
+                                                   const float* __restrict__ l_bound, bf16x8* __restrict__ Cfr,
+                                                   int64_t cexp, const float* __restrict__ colmax) {
   int t, tn, k;
-  x6_item<COUT>(blockIdx.x, nTn, K, t, tn, k);
+  x6_item<COUT>(b, nTn, K, t, tn, k, grid);
   const int nTp = nmb / 4;
   const int lane = threadIdx.x & 63, li = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -653,6 +652,46 @@ __global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __r
     const int64_t n = (int64_t)tn * kX6BN + 64 * w + 16 * cb + li;
     if (lane < 16 && n < N) dst[n] = s * unscale;
   }
+}
+
+template <bool COUT = false>
+__global__ __launch_bounds__(256, 2) void expert_cond16_kernel(const bf16x8* __restrict__ Afr,
+                                                               const bf16x8* __restrict__ Lfr, uint32_t afr_bytes,
+                                                               uint32_t lfr_bytes, int nmk, int nmb, int nTn, int K,
+                                                               int64_t N, float* __restrict__ part, int64_t ldp,
+                                                               const float* __restrict__ a_bound,
+                                                               const float* __restrict__ l_bound,
+                                                               bf16x8* __restrict__ Cfr = nullptr, int64_t cexp = 0,
+                                                               const float* __restrict__ colmax = nullptr) {
+  __shared__ bf16x8 sL[2][4 * 2 * 3 * 64];  // [row sub-tile][k-step of pair][plane][lane position] (2 planes used)
+  expert_cond16_item<COUT>(sL, blockIdx.x, gridDim.x, Afr, Lfr, afr_bytes, lfr_bytes, nmk, nmb, nTn, K, N, part, ldp,
+                           a_bound, l_bound, Cfr, cexp, colmax);
+}
+
+// One layer's operands of the batched K5.
+struct K5Layer {
+  const bf16x8* Afr;
+  const bf16x8* Lfr;
+  float* part;
+  const float* a_bound;
+  const float* l_bound;
+  bf16x8* Cfr;
+  const float* colmax;
+};
+
+// expert_cond16_kernel over two layers in one launch: workgroups [0, per) run layer 0's
+// items, [per, 2 per) layer 1's (same items, same arithmetic: bit-identical partials
+// and C_k images); one kernel tail fewer between the layers.
+template <bool COUT>
+__global__ __launch_bounds__(256, 2) void expert_cond16_pair_kernel(K5Layer l0, K5Layer l1, int per,
+                                                                    uint32_t afr_bytes, uint32_t lfr_bytes, int nmk,
+                                                                    int nmb, int nTn, int K, int64_t N, int64_t ldp,
+                                                                    int64_t cexp) {
+  __shared__ bf16x8 sL[2][4 * 2 * 3 * 64];
+  const bool second = (int)blockIdx.x >= per;
+  const K5Layer& l = second ? l1 : l0;
+  expert_cond16_item<COUT>(sL, (int)blockIdx.x - (second ? per : 0), per, l.Afr, l.Lfr, afr_bytes, lfr_bytes, nmk,
+                           nmb, nTn, K, N, l.part, ldp, l.a_bound, l.l_bound, l.Cfr, cexp, l.colmax);
 }
 
 // ------------------------------------------------------------------ backward (x6)
@@ -1929,6 +1968,50 @@ __global__ __launch_bounds__(256, 2) void trsm_stats16_kernel(
   K4STAMP(it, 4);
 }
 
+// One layer's operands of the batched K4 (both SMGP layers share M, N and K).
+struct K4Layer {
+  const bf16x8* Tfr;
+  const bf16x8* Kfr;
+  const float* q_mu;
+  bf16x8* Afr;
+  float* stats;
+  float* Af32;
+  const float* a_var;
+  float* a_bound;
+  const float* t_bound;
+  const float* k_bound;
+  int64_t ldq, lds, lda;
+};
+
+// trsm_stats16_kernel over two layers in one launch: workgroups [0, per) run layer 0's
+// items, [per, 2 per) layer 1's, each exactly as the one-layer kernel does (same items,
+// same arithmetic: bit-identical images and statistics).  One launch instead of two
+// drops a dispatch round boundary and a kernel tail between the layers.
+template <int KMAX>
+__global__ __launch_bounds__(256, 2) void trsm_stats16_pair_kernel(K4Layer l0, K4Layer l1, int per,
+                                                                  uint32_t tfr_bytes, uint32_t kfr_bytes, int nmk,
+                                                                  int nTn, int64_t M, int64_t N, int K) {
+  __shared__ bf16x8 sL[2][4 * 2 * 3 * 64];
+  __shared__ float sQ[128 * KMAX + 1];
+  const bool second = (int)blockIdx.x >= per;
+  const K4Layer& l = second ? l1 : l0;
+  const int bid = (int)blockIdx.x - (second ? per : 0);
+  const int nT = nmk / 8, nP = (nT + 1) / 2;
+  int p, tn;
+  if (bid == 0 && threadIdx.x == 0) *l.a_bound = sqrtf(*l.a_var);
+  col_major_item(bid, nP, nTn, p, tn);
+  if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
+  __syncthreads();
+  trsm_stats16_item<KMAX>(sL, sQ, nT - 1 - p, tn, l.Tfr, tfr_bytes, l.Kfr, kfr_bytes, nmk, M, N, l.q_mu, l.ldq, K,
+                          l.Afr, l.stats, l.lds, l.Af32, l.lda, l.a_var, l.t_bound, l.k_bound);
+  if (nT - 1 - p == p) return;
+  __syncthreads();
+  if (threadIdx.x == 0) sQ[128 * KMAX] = 0.f;
+  __syncthreads();
+  trsm_stats16_item<KMAX>(sL, sQ, p, tn, l.Tfr, tfr_bytes, l.Kfr, kfr_bytes, nmk, M, N, l.q_mu, l.ldq, K, l.Afr,
+                          l.stats, l.lds, l.Af32, l.lda, l.a_var, l.t_bound, l.k_bound);
+}
+
 }  // namespace mgp
 
 using namespace mgp;
@@ -2213,6 +2296,67 @@ extern "C" int mgp_trsm_stats_f16(const void* Tfr, size_t tfr_bytes, const void*
                             stream, true, A, lda);
 }
 
+// mgp_trsm_stats_f16 for `batch` (1 or 2) layers of equal M, N, K in one launch (the two
+// SMGP layers' K4); the per-layer operands are host arrays of device pointers (A[b] may be
+// NULL; A itself may be NULL: no f32 A for any layer).  Results are bit-identical to one
+// mgp_trsm_stats_f16 call per layer.  Errors: the single call's codes for the first bad
+// layer; -17 for a batch outside [1, 2].
+extern "C" int mgp_trsm_stats_f16_batch(int32_t batch, const void* const* Tfr, size_t tfr_bytes,
+                                        const void* const* Kfr, size_t kfr_bytes, int64_t M, int64_t N,
+                                        const float* const* q_mu, int64_t ldq, int32_t K,
+                                        const float* const* variance, void* const* Afr, size_t afr_bytes,
+                                        float* const* stats, int64_t lds, float* const* A, int64_t lda,
+                                        mgp_stream_t stream) {
+  if (batch < 1 || batch > 2) return -17;
+  if (!Tfr || !Kfr || !q_mu || !variance || !Afr || !stats) return -1;
+  if (A && lda < N) return -16;
+  for (int b = 0; b < batch; ++b) {
+    if (!Tfr[b]) return -1;
+    if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return -2;
+    if (!Kfr[b]) return -3;
+    if (kfr_bytes < mgp_x6_cols_bytes(M, N)) return -4;
+    if (M < 0) return -5;
+    if (N < 0) return -6;
+    if (!q_mu[b]) return -7;
+    if (ldq < K) return -8;
+    if (K < 1) return -9;
+    if (K > 16) return MGP_ERR_UNSUPPORTED;
+    if (!variance[b]) return -10;
+    if (!Afr[b]) return -11;
+    if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -12;
+    if (!stats[b]) return -13;
+    if (lds < N) return -14;
+    if (!aligned16(Tfr[b]) || !aligned16(Kfr[b]) || !aligned16(Afr[b])) return MGP_ERR_ALIGN;
+  }
+  if (mgp_x6_cols_bytes(M, N) >= ((size_t)1 << 32) || mgp_x6_lower_bytes(M, 1) >= ((size_t)1 << 32))
+    return MGP_ERR_UNSUPPORTED;
+  if (M == 0 || N == 0) return MGP_OK;
+  const size_t tb = mgp_x6_lower_bytes(M, 1), kb = mgp_x6_cols_bytes(M, N);
+  const int64_t Mp = x6_mp(M);
+  const int nmk = (int)(Mp / 16), nT = (int)(Mp / kX6BM), nTn = (int)(x6_np(N) / kX6BN);
+  const int per = (nT + 1) / 2 * nTn;
+  K4Layer l[2];
+  for (int b = 0; b < 2; ++b) {
+    const int s = b < batch ? b : 0;
+    l[b] = K4Layer{(const bf16x8*)Tfr[s], (const bf16x8*)Kfr[s], q_mu[s], (bf16x8*)Afr[s], stats[s],
+                   A ? A[s] : nullptr, variance[s], trailer(Afr[s], cols_planes(M, N)),
+                   trailer(const_cast<void*>(Tfr[s]), lower_planes(M, 1)),
+                   trailer(const_cast<void*>(Kfr[s]), cols_planes(M, N)), ldq, lds, lda};
+  }
+  const dim3 grid((unsigned)(per * batch));
+  hipStream_t s = (hipStream_t)stream;
+  if (K <= 4)
+    hipLaunchKernelGGL(trsm_stats16_pair_kernel<4>, grid, dim3(256), 0, s, l[0], l[1], per, (uint32_t)tb,
+                       (uint32_t)kb, nmk, nTn, M, N, (int)K);
+  else if (K <= 8)
+    hipLaunchKernelGGL(trsm_stats16_pair_kernel<8>, grid, dim3(256), 0, s, l[0], l[1], per, (uint32_t)tb,
+                       (uint32_t)kb, nmk, nTn, M, N, (int)K);
+  else
+    hipLaunchKernelGGL(trsm_stats16_pair_kernel<16>, grid, dim3(256), 0, s, l[0], l[1], per, (uint32_t)tb,
+                       (uint32_t)kb, nmk, nTn, M, N, (int)K);
+  return launch_status();
+}
+
 // mgp_trsm_stats_f16 that also writes the A image's e4m3 cross-term plane (the
 // operand of mgp_expert_conditional_f16x8).  With A == NULL the f16 lo plane is
 // not written (only the f16x8 K5 reads that image).
@@ -2369,6 +2513,76 @@ extern "C" int mgp_expert_conditional_f16c(const void* Afr, size_t afr_bytes, co
   if (!Cfr) return -16;
   return expert_cond_planes(Afr, afr_bytes, Lfr, lfr_bytes, stats, lds, variance, M, N, K, 2, fmean, fvar, ldf,
                             workspace, workspace_bytes, stream, true, false, Cfr, cfr_bytes, colmax);
+}
+
+// mgp_expert_conditional_f16 (Cfr == NULL) or mgp_expert_conditional_f16c (Cfr, colmax:
+// host arrays of device pointers) for `batch` (1 or 2) layers of equal M, N, K: one K5
+// launch over both layers, then each layer's finalize.  Per-layer operands are host arrays
+// of device pointers, one workspace per layer.  Bit-identical to one call per layer.
+// Errors: the single call's codes for the first bad layer; -20 for a batch outside [1, 2].
+extern "C" int mgp_expert_conditional_f16_batch(int32_t batch, const void* const* Afr, size_t afr_bytes,
+                                                const void* const* Lfr, size_t lfr_bytes, const float* const* stats,
+                                                int64_t lds, const float* const* variance, int64_t M, int64_t N,
+                                                int32_t K, float* const* fmean, float* const* fvar, int64_t ldf,
+                                                void* const* workspace, size_t workspace_bytes,
+                                                void* const* Cfr, size_t cfr_bytes, const float* const* colmax,
+                                                mgp_stream_t stream) {
+  if (batch < 1 || batch > 2) return -20;
+  if (!Afr || !Lfr || !stats || !variance || !fmean || !fvar || !workspace) return -1;
+  const size_t cexp = cols_planes(M, N);
+  for (int b = 0; b < batch; ++b) {
+    if (!Afr[b]) return -1;
+    if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
+    if (!Lfr[b]) return -3;
+    if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return -4;
+    if (!stats[b]) return -5;
+    if (lds < N) return -6;
+    if (!variance[b]) return -7;
+    if (M < 0) return -8;
+    if (N < 0) return -9;
+    if (K < 1) return -10;
+    if (!fmean[b]) return -11;
+    if (!fvar[b]) return -12;
+    if (ldf < N) return -13;
+    if (!aligned16(Afr[b]) || !aligned16(Lfr[b])) return MGP_ERR_ALIGN;
+    if (M > 0 && N > 0 && (!workspace[b] || workspace_bytes < mgp_expert_x6_workspace_bytes(M, N, K)))
+      return MGP_ERR_WORKSPACE;
+    if (Cfr) {
+      if (!Cfr[b]) return -16;
+      if (cfr_bytes < (size_t)K * cexp) return -17;
+      if (!colmax || !colmax[b]) return -18;
+      if (!aligned16(Cfr[b])) return MGP_ERR_ALIGN;
+    }
+  }
+  if (afr_bytes >= ((size_t)1 << 32) || lfr_bytes >= ((size_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  if (M == 0 || N == 0) return MGP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t Mp = x6_mp(M);
+  const int nmk = (int)(Mp / 16), nmb = (int)(Mp / 32), nTp = (int)(Mp / kX6BM);
+  const int nTn = (int)(x6_np(N) / kX6BN);
+  const int64_t ldp = (N + 3) / 4 * 4;
+  const int per = K * nTp * nTn;
+  K5Layer l[2];
+  for (int b = 0; b < 2; ++b) {
+    const int q = b < batch ? b : 0;
+    l[b] = K5Layer{(const bf16x8*)Afr[q], (const bf16x8*)Lfr[q], (float*)workspace[q],
+                   trailer(const_cast<void*>(Afr[q]), cols_planes(M, N)),
+                   trailer(const_cast<void*>(Lfr[q]), lower_planes(M, K)), Cfr ? (bf16x8*)Cfr[q] : nullptr,
+                   Cfr ? colmax[q] : nullptr};
+  }
+  const dim3 grid((unsigned)(per * batch));
+  const uint32_t ab = (uint32_t)mgp_x6_cols_bytes(M, N), lb = (uint32_t)mgp_x6_lower_bytes(M, K);
+  if (Cfr)
+    hipLaunchKernelGGL(expert_cond16_pair_kernel<true>, grid, dim3(256), 0, s, l[0], l[1], per, ab, lb, nmk, nmb, nTn,
+                       (int)K, N, ldp, (int64_t)(cexp / 16));
+  else
+    hipLaunchKernelGGL(expert_cond16_pair_kernel<false>, grid, dim3(256), 0, s, l[0], l[1], per, ab, lb, nmk, nmb,
+                       nTn, (int)K, N, ldp, (int64_t)0);
+  int st = launch_status();
+  for (int b = 0; b < batch && !st; ++b)
+    st = mgp_launch_cond_finalize(stats[b], lds, mgp_stats_tiles(M), (const float*)workspace[b], ldp, nTp,
+                                  variance[b], N, K, fmean[b], fvar[b], ldf, s);
+  return st;
 }
 
 // Split-f16 images with the X8 plane (mgp_split_lower_f16, mgp_split_cols_f16,

@@ -43,6 +43,10 @@ from .broadcasting_lik import BroadcastingLikelihood
 from .config import (conditional_mode, default_device, default_jitter, expert_cross, expert_planes,
                      forward_image_format, step_schedule)
 
+# both layers' K4, and both layers' K5, in one launch each in the step (False: one launch
+# per layer and kernel; A/B probes only)
+_K4_BATCHED = True
+
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
 # device's HBM (config 5: 2 x 51.5 GB of 288 GB); beyond it the backward rebuilds
@@ -509,6 +513,8 @@ class SMGP(SGP):
                                          ops.expert_x6_workspace_bytes(Mx, N, K)), dtype=torch.uint8,
                                      device=dev),
         }
+        if x6:  # the second layer's K5 workspace (both layers' K5 in one launch)
+            b["ws_expert2"] = torch.empty_like(b["ws_expert"])
         if x6:  # split-bf16 images: Kuf / tril(q_sqrt) per layer (built on the side
             # stream while K3 runs), A and L^-T shared by the layers (processed in turn)
             for L in ("f", "a"):
@@ -675,16 +681,48 @@ class SMGP(SGP):
             elif sched in ("k1_main", "serial"):
                 kuf_late("f")
                 kuf_late("a")
-            Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bufs["f"], timing, fmt, Tfr=Tfr["f"])
+            bf, ba = bufs["f"], bufs["a"]
+            # both layers' K4 in one launch (mgp_trsm_stats_f16_batch, bit-identical to
+            # two): one kernel tail and dispatch-round boundary fewer (~25 us, measured)
+            batched = (_K4_BATCHED and sched in ("overlap", "k1_main", "serial") and fmt == "f16" and expert_cross() == "f16"
+                       and pf.num_inducing == pa.num_inducing and pf.num_latent_gps == pa.num_latent_gps
+                       and all(x.get("Afr") is not None and x.get("stats") is not None for x in (bf, ba))
+                       and bf["Afr"].data_ptr() != ba["Afr"].data_ptr()
+                       and (bf.get("A32") is None) == (ba.get("A32") is None))
+            self.layers_per_launch = 2 if batched else 1   # K4 / K5 launches cover this many layers
+            if batched:
+                with _Stage(timing, "trsm_stats"):
+                    (Afr_f, st_f), (Afr_a, st_a) = ops.trsm_stats_f16_batch(
+                        [Tfr["f"], Tfr["a"]], [images["f"][0], images["a"][0]], [pf.q_mu, pa.q_mu],
+                        pf.num_inducing, N, [bf["Afr"], ba["Afr"]], [bf["stats"], ba["stats"]],
+                        [pf.kernel.variance, pa.kernel.variance],
+                        As=[bf["A32"], ba["A32"]] if bf.get("A32") is not None else None)
+            else:
+                Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bf, timing, fmt, Tfr=Tfr["f"])
             if sched == "k1a_k5":            # beside the pred layer's K5
                 k1a_ev = side_kuf_a()
                 pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
             if k1a_ev is not None:
                 main.wait_event(k1a_ev)
-            Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], bufs["a"], timing, fmt, Tfr=Tfr["a"])
-            if sched != "k1a_k5":
-                pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
-            pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)
+            if not batched:
+                Afr_a, st_a = pa.x6_trsm(N, LinvT["a"], images["a"][0], ba, timing, fmt, Tfr=Tfr["a"])
+            if batched and "ws_expert2" in b and (bf.get("c_out") is None) == (ba.get("c_out") is None):
+                # both layers' K5 in one launch too (mgp_expert_conditional_f16_batch, bit-identical)
+                with _Stage(timing, "expert_cond"):
+                    c_outs = None
+                    if bf.get("c_out") is not None and ba.get("c_out") is not None:
+                        c_outs = [bf["c_out"], ba["c_out"]]
+                        ops.colnorm_max(pf.q_sqrt, out=bf["c_out"][1])
+                        ops.colnorm_max(pa.q_sqrt, out=ba["c_out"][1])
+                    ops.expert_conditional_f16_batch(
+                        [Afr_f, Afr_a], [images["f"][1], images["a"][1]], [st_f, st_a],
+                        [pf.kernel.variance, pa.kernel.variance], pf.num_inducing, N, pf.num_latent_gps,
+                        [bf["fmean"], ba["fmean"]], [bf["fvar"], ba["fvar"]], [b["ws_expert"], b["ws_expert2"]],
+                        c_outs=c_outs)
+            else:
+                if sched != "k1a_k5":
+                    pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
+                pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)
         else:
             for L, layer in layers:
                 if L in late:

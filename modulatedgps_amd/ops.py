@@ -9,6 +9,7 @@ dimensions padded to a multiple of 4 elements so rows can be read as float4.
 ``padded(rows, cols)`` returns such a view; the expert-major conditional
 outputs are [K][N] views.
 """
+import ctypes
 import torch
 
 from . import _lib
@@ -277,6 +278,35 @@ def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_varian
     return Afr, stats
 
 
+def trsm_stats_f16_batch(Tfrs, Kfrs, q_mus, M, N, Afrs, statss, variances, As=None):
+    """K4 of several layers (1 or 2, equal M, N, K) in one launch (mgp_trsm_stats_f16_batch):
+    trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=Afr, stats=stats, A=A, f16_variance=variance,
+    in_fmt="f16", cross="f16") for each layer, bit-identical.  Afrs / statss: the output
+    buffers (required); As: f32 A buffers or None."""
+    n = len(Tfrs)
+    for seq in (Kfrs, q_mus, Afrs, statss, variances) + ((As,) if As is not None else ()):
+        if len(seq) != n:
+            raise ValueError("one entry per layer in every operand list")
+    K = q_mus[0].shape[1]
+    ldq, lds = _ld(q_mus[0]), _ld(statss[0])
+    for q, st in zip(q_mus, statss):
+        _check(q, "q_mu", 2)
+        if q.shape[1] != K or _ld(q) != ldq or _ld(st) != lds:
+            raise ValueError("the layers' q_mu / stats must share K and leading dimensions")
+    lda = N
+    if As is not None:
+        lda = _ld(As[0])
+        if any(_ld(a) != lda for a in As):
+            raise ValueError("the f32 A buffers must share a leading dimension")
+
+    def arr(ts):
+        return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+    _lib.call("mgp_trsm_stats_f16_batch", n, arr(Tfrs), min(t.numel() for t in Tfrs), arr(Kfrs),
+              min(t.numel() for t in Kfrs), M, N, arr(q_mus), ldq, K, arr(variances), arr(Afrs),
+              min(t.numel() for t in Afrs), arr(statss), lds, arr(As) if As is not None else None, lda, _stream())
+    return list(zip(Afrs, statss))
+
+
 def expert_workspace_bytes(M, N, K):
     return max(int(_lib.load().mgp_expert_workspace_bytes(M, N, K)), 16)
 
@@ -389,6 +419,31 @@ def expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K, fmean=None, fvar=N
                   stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K, int(planes), fmean.data_ptr(),
                   fvar.data_ptr(), _ld(fmean), workspace.data_ptr(), workspace.numel(), _stream())
     return fmean, fvar
+
+
+def expert_conditional_f16_batch(Afrs, Lfrs, statss, variances, M, N, K, fmeans, fvars, workspaces, c_outs=None):
+    """K5 of several layers (1 or 2, equal M, N, K) in one launch
+    (mgp_expert_conditional_f16_batch): expert_conditional_x6(Afr, Lfr, stats, variance, M, N, K,
+    fmean=..., fvar=..., workspace=..., fmt="f16", cross="f16", c_out=...) for each layer,
+    bit-identical.  Outputs and one workspace per layer are required; c_outs: a
+    (Cfr, colmax) per layer (training) or None."""
+    n = len(Afrs)
+    lists = (Lfrs, statss, variances, fmeans, fvars, workspaces) + ((c_outs,) if c_outs is not None else ())
+    if any(len(x) != n for x in lists):
+        raise ValueError("one entry per layer in every operand list")
+    lds, ldf = _ld(statss[0]), _ld(fmeans[0])
+    if any(_ld(t) != lds for t in statss) or any(_ld(t) != ldf for t in list(fmeans) + list(fvars)):
+        raise ValueError("the layers' stats / fmean / fvar must share leading dimensions")
+
+    def arr(ts):
+        return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+    cf = arr([c[0] for c in c_outs]) if c_outs is not None else None
+    cm = arr([c[1] for c in c_outs]) if c_outs is not None else None
+    cb = min(c[0].numel() for c in c_outs) if c_outs is not None else 0
+    _lib.call("mgp_expert_conditional_f16_batch", n, arr(Afrs), min(t.numel() for t in Afrs), arr(Lfrs),
+              min(t.numel() for t in Lfrs), arr(statss), lds, arr(variances), M, N, K, arr(fmeans), arr(fvars), ldf,
+              arr(workspaces), min(t.numel() for t in workspaces), cf, cb, cm, _stream())
+    return list(zip(fmeans, fvars))
 
 
 def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise=None, seed=0,

@@ -176,3 +176,93 @@ def test_mfma_shape_switches(device):
                                          c_out=(Cfr, ops.colnorm_max(qs)))
     assert normwise(to_np(fvc).T, var_ref) < 1e-4
     assert normwise(to_np(fvc), to_np(fv)) < 1e-6
+
+
+@pytest.mark.parametrize("N,M,K,with_a", [(65536, 1024, 8, False), (8192, 256, 4, True), (3000, 200, 3, True)])
+def test_trsm_stats_f16_batch_bit_identical(device, N, M, K, with_a):
+    """mgp_trsm_stats_f16_batch (both layers' K4 in one launch) writes the same A
+    images, statistics and f32 A bits as one mgp_trsm_stats_f16 call per layer,
+    including ragged M and N (models.py:141-143 for pred_layer and assign_layer)."""
+    from modulatedgps_amd import ops
+    g = torch.Generator(device=device).manual_seed(11)
+    D = 4
+    X = torch.randn(N, D, device=device, generator=g)
+    per = []
+    for b in range(2):
+        Z = torch.randn(M, D, device=device, generator=g)
+        var = torch.tensor([0.7 + 0.2 * b], device=device)
+        ls = torch.tensor([1.0 + 0.5 * b], device=device)
+        _, LinvT, _ = ops.kuu_potrf_trtri([Z], [var], [ls], 1e-6)
+        q_mu = torch.randn(M, K, device=device, generator=g)
+        Thr = ops.split_upper_x6(LinvT[0], fmt="f16")
+        Khr = ops.rbf_kuf_x6(X, Z, var, ls, fmt="f16")
+        per.append((Thr, Khr, q_mu, var))
+    ref = []
+    for Thr, Khr, q_mu, var in per:
+        A = ops.padded(M, N, device) if with_a else None
+        Afr, st = ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, A=A, f16_variance=var, in_fmt="f16", cross="f16")
+        ref.append((Afr.clone(), st.clone(), None if A is None else A.clone()))
+    Afrs = [torch.full_like(r[0], 0x7F) for r in ref]
+    sts = [torch.full_like(r[1], float("nan")) for r in ref]
+    As = [torch.full_like(r[2], float("nan")) for r in ref] if with_a else None
+    out = ops.trsm_stats_f16_batch([p[0] for p in per], [p[1] for p in per], [p[2] for p in per], M, N, Afrs, sts,
+                                   [p[3] for p in per], As=As)
+    torch.cuda.synchronize()
+    # fragment planes 0-1 (f16 hi, lo; plane 2 is the f16x8 K4's) and the trailer's scale bound
+    planes = ops.x6_cols_bytes(M, N) - 256
+    for b in range(2):
+        got, exp = out[b][0], ref[b][0]
+        assert torch.equal(got[:planes].view(-1, 3, 64 * 16)[:, :2], exp[:planes].view(-1, 3, 64 * 16)[:, :2])
+        assert torch.equal(got[planes:planes + 4], exp[planes:planes + 4])
+        assert torch.equal(out[b][1][..., :N], ref[b][1][..., :N])
+        if with_a:
+            assert torch.equal(As[b][:, :N], ref[b][2][:, :N])
+
+
+@pytest.mark.parametrize("N,M,K,train", [(65536, 1024, 8, False), (8192, 256, 4, True), (3000, 200, 3, True)])
+def test_expert_conditional_f16_batch_bit_identical(device, N, M, K, train):
+    """mgp_expert_conditional_f16_batch (both layers' K5 in one launch, forward or with
+    the training C_k images) gives the same fmean / fvar / C_k bits as one
+    mgp_expert_conditional_f16(c) call per layer (models.py:141-143, both layers)."""
+    from modulatedgps_amd import ops
+    g = torch.Generator(device=device).manual_seed(5)
+    D = 4
+    X = torch.randn(N, D, device=device, generator=g)
+    per = []
+    for b in range(2):
+        Z = torch.randn(M, D, device=device, generator=g)
+        var = torch.tensor([0.6 + 0.3 * b], device=device)
+        ls = torch.tensor([0.9 + 0.4 * b], device=device)
+        _, LinvT, _ = ops.kuu_potrf_trtri([Z], [var], [ls], 1e-6)
+        q_mu = torch.randn(M, K, device=device, generator=g)
+        qs = ops.padded(M, M, device, batch=K)
+        qs.copy_(0.4 * torch.eye(M, device=device) + torch.tril(0.05 * torch.randn(K, M, M, device=device,
+                                                                                     generator=g)))
+        Thr = ops.split_upper_x6(LinvT[0], fmt="f16")
+        Khr = ops.rbf_kuf_x6(X, Z, var, ls, fmt="f16")
+        Afr, st = ops.trsm_stats_x6(Thr, Khr, q_mu, M, N, f16_variance=var, in_fmt="f16", cross="f16")
+        Lhr = ops.split_lower_x6(qs, fmt="f16")
+        c_out = None
+        if train:
+            c_out = (torch.zeros(ops.c_images_bytes(M, N, K), dtype=torch.uint8, device=device), ops.colnorm_max(qs))
+        per.append((Afr, Lhr, st, var, c_out))
+    ref = []
+    for Afr, Lhr, st, var, c_out in per:
+        fm, fv = ops.expert_conditional_x6(Afr, Lhr, st, var, M, N, K, fmt="f16", cross="f16", c_out=c_out)
+        ref.append((fm.clone(), fv.clone(), None if c_out is None else c_out[0].clone()))
+    fms = [ops.padded(K, N, device) for _ in range(2)]
+    fvs = [ops.padded(K, N, device) for _ in range(2)]
+    for t in fms + fvs:
+        t.fill_(float("nan"))
+    wss = [torch.empty(ops.expert_x6_workspace_bytes(M, N, K), dtype=torch.uint8, device=device) for _ in range(2)]
+    c_outs = None
+    if train:
+        c_outs = [(torch.zeros_like(p[4][0]), p[4][1]) for p in per]
+    ops.expert_conditional_f16_batch([p[0] for p in per], [p[1] for p in per], [p[2] for p in per],
+                                     [p[3] for p in per], M, N, K, fms, fvs, wss, c_outs=c_outs)
+    torch.cuda.synchronize()
+    for b in range(2):
+        assert torch.equal(fms[b], ref[b][0])
+        assert torch.equal(fvs[b], ref[b][1])
+        if train:
+            assert torch.equal(c_outs[b][0], ref[b][2])
