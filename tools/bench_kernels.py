@@ -92,8 +92,18 @@ def main():
     ops.expert_conditional_x6(Ahr, Lhr, sth, var, M, N, K, fmean=fm6, fvar=fv6, fmt="f16", cross="f16",
                               c_out=(Cfr, colmax))
     cimg = (Cfr, colmax, ops.image_bound(Lhr, M, K=K))
+    # both layers in one launch (distinct operand copies for the second layer)
+    Thr2, Khr2, Ahr2, Lhr2 = Thr.clone(), Khr.clone(), Ahr.clone(), Lhr.clone()
+    sth2 = sth.clone()
+    fmB, fvB = fm6.clone(), fv6.clone()
+    wsx = [torch.empty(ops.expert_x6_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev) for _ in range(2)]
     torch.cuda.synchronize()
     runs = {
+        "trsm_f16_pair": lambda: ops.trsm_stats_f16_batch([Thr, Thr2], [Khr, Khr2], [q_mu, q_mu], M, N, [Ahr, Ahr2],
+                                                          [sth, sth2], [var, var]),
+        "expert_cond_f16_pair": lambda: ops.expert_conditional_f16_batch([Ahr, Ahr2], [Lhr, Lhr2], [sth, sth2],
+                                                                         [var, var], M, N, K, [fm6, fmB], [fv6, fvB],
+                                                                         wsx),
         "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
         "kuu_chol_x1": lambda: ops.kuu_potrf_trtri([Z], [var], [lsc], 1e-6, LinvT=LinvT[0:1], info=info[0:1]),
         "rbf_kuf": lambda: ops.rbf_kuf(X, Z, var, lsc, out=Kuf),
@@ -152,6 +162,10 @@ def main():
         out["expert_cond"]["tflops"] = K * M * M * N / (out["expert_cond"]["median_ms"] * 1e-3) / 1e12
     if "expert_cond_x6" in out:
         out["expert_cond_x6"]["tflops"] = K * M * M * N / (out["expert_cond_x6"]["median_ms"] * 1e-3) / 1e12
+    if "expert_cond_f16_pair" in out:
+        out["expert_cond_f16_pair"]["tflops"] = 2 * K * M * M * N / (out["expert_cond_f16_pair"]["median_ms"] * 1e-3) / 1e12
+    if "trsm_f16_pair" in out:
+        out["trsm_f16_pair"]["tflops"] = 2 * M * M * N / (out["trsm_f16_pair"]["median_ms"] * 1e-3) / 1e12
     for name in ("expert_cond_f16", "expert_cond_f16x8"):
         if name in out:
             out[name]["tflops"] = K * M * M * N / (out[name]["median_ms"] * 1e-3) / 1e12

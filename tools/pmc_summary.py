@@ -58,6 +58,8 @@ def kernel_key(name):
         return "expert_cond_f16c_kernel"        # split-f16, also writing the C_k images (training)
     if base == "expert_cond16_kernel" and flags[:1] == ["true"]:
         return "expert_cond16c_kernel"          # 16x16x32, also writing the C_k images (training)
+    if base == "expert_cond16_pair_kernel" and flags[:1] == ["true"]:
+        return "expert_cond16c_pair_kernel"     # both layers in one launch, with the C_k images
     if base in ("expert_cond_x6_kernel", "rbf_kuf_x6_kernel") and "true" in flags:
         return base.replace("_x6_", "_f16_")
     return base
