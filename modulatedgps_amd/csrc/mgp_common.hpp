@@ -26,6 +26,16 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 int mgp_launch_cond_finalize(const float* stats, int64_t lds, int nTs, const float* part, int64_t ldp, int nTp,
                              const float* variance, int64_t N, int K, float* fmean, float* fvar, int64_t ldf,
                              hipStream_t s);
+// One layer's operands of the two-layer finalize (mgp_expert_conditional_f16_batch).
+struct CondFinLayer {
+  const float* stats;
+  const float* part;
+  const float* variance;
+  float* fmean;
+  float* fvar;
+};
+int mgp_launch_cond_finalize2(const CondFinLayer& l0, const CondFinLayer& l1, int64_t lds, int nTs, int64_t ldp,
+                              int nTp, int64_t N, int K, int64_t ldf, hipStream_t s);
 
 // ------------------------------------------------------------------ MFMA
 // D(32x32) += A(32x2) * B(2x32), exact f32 (fmaf chain).  Lane l supplies

@@ -2579,10 +2579,13 @@ extern "C" int mgp_expert_conditional_f16_batch(int32_t batch, const void* const
     hipLaunchKernelGGL(expert_cond16_pair_kernel<false>, grid, dim3(256), 0, s, l[0], l[1], per, ab, lb, nmk, nmb,
                        nTn, (int)K, N, ldp, (int64_t)0);
   int st = launch_status();
-  for (int b = 0; b < batch && !st; ++b)
-    st = mgp_launch_cond_finalize(stats[b], lds, mgp_stats_tiles(M), (const float*)workspace[b], ldp, nTp,
-                                  variance[b], N, K, fmean[b], fvar[b], ldf, s);
-  return st;
+  if (st) return st;
+  if (batch == 2)   // both layers' finalize in one launch too
+    return mgp_launch_cond_finalize2(CondFinLayer{stats[0], (const float*)workspace[0], variance[0], fmean[0], fvar[0]},
+                                     CondFinLayer{stats[1], (const float*)workspace[1], variance[1], fmean[1], fvar[1]},
+                                     lds, mgp_stats_tiles(M), ldp, nTp, N, K, ldf, s);
+  return mgp_launch_cond_finalize(stats[0], lds, mgp_stats_tiles(M), (const float*)workspace[0], ldp, nTp,
+                                  variance[0], N, K, fmean[0], fvar[0], ldf, s);
 }
 
 // Split-f16 images with the X8 plane (mgp_split_lower_f16, mgp_split_cols_f16,

@@ -367,6 +367,25 @@ __global__ __launch_bounds__(256) void cond_finalize_kernel(const float* __restr
   fvar[(int64_t)k * ldf + n] = (variance[0] - a2) + q;
 }
 
+// cond_finalize_kernel for two layers in one launch (blockIdx.z: the layer), the same
+// per-element sums in the same order (bit-identical).
+__global__ __launch_bounds__(256) void cond_finalize2_kernel(CondFinLayer l0, CondFinLayer l1, int64_t lds_, int nTs,
+                                                             int64_t ldp, int nT, int64_t N, int K, int64_t ldf) {
+  const CondFinLayer& l = blockIdx.z ? l1 : l0;
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (n >= N) return;
+  float a2 = 0.f, fm = 0.f, q = 0.f;
+  for (int t = 0; t < nTs; ++t) {
+    const float* st = l.stats + (int64_t)t * (K + 1) * lds_;
+    a2 += st[n];
+    fm += st[(int64_t)(1 + k) * lds_ + n];
+  }
+  for (int t = 0; t < nT; ++t) q += l.part[((int64_t)k * nT + t) * ldp + n];
+  l.fmean[(int64_t)k * ldf + n] = fm;
+  l.fvar[(int64_t)k * ldf + n] = (l.variance[0] - a2) + q;
+}
+
 }  // namespace mgp
 
 using namespace mgp;
@@ -442,6 +461,13 @@ int mgp::mgp_launch_cond_finalize(const float* stats, int64_t lds, int nTs, cons
                                   int64_t ldf, hipStream_t s) {
   hipLaunchKernelGGL(cond_finalize_kernel, dim3((unsigned)((N + 255) / 256), K), dim3(256), 0, s, stats, lds,
                      nTs, part, ldp, nTp, variance, N, K, fmean, fvar, ldf);
+  return launch_status();
+}
+
+int mgp::mgp_launch_cond_finalize2(const CondFinLayer& l0, const CondFinLayer& l1, int64_t lds, int nTs, int64_t ldp,
+                                   int nTp, int64_t N, int K, int64_t ldf, hipStream_t s) {
+  hipLaunchKernelGGL(cond_finalize2_kernel, dim3((unsigned)((N + 255) / 256), K, 2), dim3(256), 0, s, l0, l1, lds,
+                     nTs, ldp, nTp, N, K, ldf);
   return launch_status();
 }
 
