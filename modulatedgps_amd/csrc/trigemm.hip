@@ -348,6 +348,50 @@ __global__ __launch_bounds__((TgCfg<BM, BN>::THREADS), (TgCfg<BM, BN>::THREADS /
 
 // fmean[k][n] = sum_t stats[t][1+k][n];
 // fvar[k][n]  = var - sum_t stats[t][0][n] + sum_t part[k][t][n].
+// One (n, k) of the finalize: the tile sums in tile order, their loads issued eight
+// at a time ahead of the adds (the loop had one dependent load round trip per tile).
+__device__ __forceinline__ void cond_finalize_elem(const float* __restrict__ stats, int64_t lds_, int nTs,
+                                                   const float* __restrict__ part, int64_t ldp, int nT,
+                                                   const float* __restrict__ variance, int K,
+                                                   float* __restrict__ fmean, float* __restrict__ fvar, int64_t ldf,
+                                                   int64_t n, int k) {
+  constexpr int B = 8;
+  float a2 = 0.f, fm = 0.f, q = 0.f;
+  const int64_t ts = (int64_t)(K + 1) * lds_, fo = (int64_t)(1 + k) * lds_;
+  int t = 0;
+  for (; t + B <= nTs; t += B) {
+    float x[B], y[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const float* st = stats + (int64_t)(t + u) * ts;
+      x[u] = st[n];
+      y[u] = st[fo + n];
+    }
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      a2 += x[u];
+      fm += y[u];
+    }
+  }
+  for (; t < nTs; ++t) {
+    const float* st = stats + (int64_t)t * ts;
+    a2 += st[n];
+    fm += st[fo + n];
+  }
+  const float* pk = part + (int64_t)k * nT * ldp + n;
+  t = 0;
+  for (; t + B <= nT; t += B) {
+    float x[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) x[u] = pk[(int64_t)(t + u) * ldp];
+#pragma unroll
+    for (int u = 0; u < B; ++u) q += x[u];
+  }
+  for (; t < nT; ++t) q += pk[(int64_t)t * ldp];
+  fmean[(int64_t)k * ldf + n] = fm;
+  fvar[(int64_t)k * ldf + n] = (variance[0] - a2) + q;
+}
+
 __global__ __launch_bounds__(256) void cond_finalize_kernel(const float* __restrict__ stats, int64_t lds_,
                                                             int nTs, const float* __restrict__ part, int64_t ldp,
                                                             int nT, const float* __restrict__ variance,
@@ -356,15 +400,7 @@ __global__ __launch_bounds__(256) void cond_finalize_kernel(const float* __restr
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (n >= N) return;
-  float a2 = 0.f, fm = 0.f, q = 0.f;
-  for (int t = 0; t < nTs; ++t) {
-    const float* st = stats + (int64_t)t * (K + 1) * lds_;
-    a2 += st[n];
-    fm += st[(int64_t)(1 + k) * lds_ + n];
-  }
-  for (int t = 0; t < nT; ++t) q += part[((int64_t)k * nT + t) * ldp + n];
-  fmean[(int64_t)k * ldf + n] = fm;
-  fvar[(int64_t)k * ldf + n] = (variance[0] - a2) + q;
+  cond_finalize_elem(stats, lds_, nTs, part, ldp, nT, variance, K, fmean, fvar, ldf, n, k);
 }
 
 // cond_finalize_kernel for two layers in one launch (blockIdx.z: the layer), the same
@@ -375,15 +411,7 @@ __global__ __launch_bounds__(256) void cond_finalize2_kernel(CondFinLayer l0, Co
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (n >= N) return;
-  float a2 = 0.f, fm = 0.f, q = 0.f;
-  for (int t = 0; t < nTs; ++t) {
-    const float* st = l.stats + (int64_t)t * (K + 1) * lds_;
-    a2 += st[n];
-    fm += st[(int64_t)(1 + k) * lds_ + n];
-  }
-  for (int t = 0; t < nT; ++t) q += l.part[((int64_t)k * nT + t) * ldp + n];
-  l.fmean[(int64_t)k * ldf + n] = fm;
-  l.fvar[(int64_t)k * ldf + n] = (l.variance[0] - a2) + q;
+  cond_finalize_elem(l.stats, lds_, nTs, l.part, ldp, nT, l.variance, K, l.fmean, l.fvar, ldf, n, k);
 }
 
 }  // namespace mgp
