@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "mgp_hip.h"
@@ -64,8 +65,11 @@ void* dev_bytes(size_t n) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc != 2) {
-    std::fprintf(stderr, "usage: %s problem.bin\n", argv[0]);
+  // --batched: both layers' K4 and K5 through mgp_trsm_stats_f16_batch /
+  // mgp_expert_conditional_f16_batch (per-layer images), else one call per layer
+  const bool batched = argc == 3 && std::string(argv[2]) == "--batched";
+  if (argc != 2 && !batched) {
+    std::fprintf(stderr, "usage: %s problem.bin [--batched]\n", argv[0]);
     return 1;
   }
   std::FILE* f = std::fopen(argv[1], "rb");
@@ -122,29 +126,44 @@ int main(int argc, char** argv) {
 
   // K1, K4, K5 (split-f16 images) and K7 per layer
   const size_t colb = mgp_x6_cols_bytes(M, N), lowb = mgp_x6_lower_bytes(M, K), tb = mgp_x6_lower_bytes(M, 1);
-  void* Kfr = dev_bytes(colb);
-  void* Afr = dev_bytes(colb);
-  void* Tfr = dev_bytes(tb);
-  void* Lfr = dev_bytes(lowb);
   const int T = mgp_stats_tiles(M);
-  float* stats = (float*)dev_bytes(sizeof(float) * T * (K + 1) * ldn);
   const size_t xwb = mgp_expert_x6_workspace_bytes(M, N, K);
-  void* xws = dev_bytes(xwb);
   const size_t kwb = mgp_kl_workspace_bytes(M, K);
   void* kws = dev_bytes(kwb);
-  float *fmean[2], *fvar[2];
+  void *Kfr[2], *Afr[2], *Tfr[2], *Lfr[2], *xws[2];
+  float *stats[2], *fmean[2], *fvar[2];
   double* kl = (double*)dev_bytes(2 * sizeof(double));
   for (int l = 0; l < 2; ++l) {
+    Kfr[l] = dev_bytes(colb);
+    Afr[l] = dev_bytes(colb);
+    Tfr[l] = dev_bytes(tb);
+    Lfr[l] = dev_bytes(lowb);
+    stats[l] = (float*)dev_bytes(sizeof(float) * T * (K + 1) * ldn);
+    xws[l] = dev_bytes(xwb);
     fmean[l] = (float*)dev_bytes(sizeof(float) * K * ldn);
     fvar[l] = (float*)dev_bytes(sizeof(float) * K * ldn);
-    CHECK_MGP(mgp_rbf_kuf_f16(dX, D, dZ[l], D, N, M, (int32_t)D, dvar[l], dls[l], 1, Kfr, colb, s));
-    CHECK_MGP(mgp_split_upper_f16(LinvT + l * M * ldm, ldm, M, Tfr, tb, s));
-    CHECK_MGP(mgp_trsm_stats_f16(Tfr, tb, Kfr, colb, M, N, dqmu[l], K, K, dvar[l], Afr, colb, stats, ldn, nullptr, N,
-                                 s));
-    CHECK_MGP(mgp_split_lower_f16(dqs[l], ldm, M * ldm, M, K, Lfr, lowb, s));
-    CHECK_MGP(mgp_expert_conditional_f16(Afr, colb, Lfr, lowb, stats, ldn, dvar[l], M, N, K, fmean[l], fvar[l], ldn,
-                                         xws, xwb, s));
+    CHECK_MGP(mgp_rbf_kuf_f16(dX, D, dZ[l], D, N, M, (int32_t)D, dvar[l], dls[l], 1, Kfr[l], colb, s));
+    CHECK_MGP(mgp_split_upper_f16(LinvT + l * M * ldm, ldm, M, Tfr[l], tb, s));
+    CHECK_MGP(mgp_split_lower_f16(dqs[l], ldm, M * ldm, M, K, Lfr[l], lowb, s));
+    if (!batched) {
+      CHECK_MGP(mgp_trsm_stats_f16(Tfr[l], tb, Kfr[l], colb, M, N, dqmu[l], K, K, dvar[l], Afr[l], colb, stats[l], ldn,
+                                   nullptr, N, s));
+      CHECK_MGP(mgp_expert_conditional_f16(Afr[l], colb, Lfr[l], lowb, stats[l], ldn, dvar[l], M, N, K, fmean[l],
+                                           fvar[l], ldn, xws[l], xwb, s));
+    }
     CHECK_MGP(mgp_gauss_kl_white(dqmu[l], K, dqs[l], ldm, M * ldm, M, K, kl + l, kws, kwb, s));
+  }
+  if (batched) {
+    const void* cT[2] = {Tfr[0], Tfr[1]};
+    const void* cK[2] = {Kfr[0], Kfr[1]};
+    const void* cA[2] = {Afr[0], Afr[1]};
+    const void* cL[2] = {Lfr[0], Lfr[1]};
+    const float* q[2] = {dqmu[0], dqmu[1]};
+    const float* v[2] = {dvar[0], dvar[1]};
+    const float* st[2] = {stats[0], stats[1]};
+    CHECK_MGP(mgp_trsm_stats_f16_batch(2, cT, tb, cK, colb, M, N, q, K, K, v, Afr, colb, stats, ldn, nullptr, N, s));
+    CHECK_MGP(mgp_expert_conditional_f16_batch(2, cA, colb, cL, lowb, st, ldn, v, M, N, K, fmean, fvar, ldn, xws, xwb,
+                                               nullptr, 0, nullptr, s));
   }
 
   // K6 with the explicit noise, then the scalar ELBO

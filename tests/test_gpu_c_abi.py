@@ -67,3 +67,7 @@ def test_elbo_through_the_c_abi_alone(device, tmp_path, N, M, K, D, ls, S):
     print(f"C-ABI {elbo_c:.9g}  python {e_py:.9g}  oracle {ref:.9g}")
     assert elbo_c == pytest.approx(ref, rel=1e-4)
     assert elbo_c == pytest.approx(e_py, rel=1e-5)
+    # both layers' K4 / K5 through the batch entries: the same bits
+    rb = subprocess.run([BIN, str(prob), "--batched"], capture_output=True, text=True, timeout=120)
+    assert rb.returncode == 0, rb.stderr
+    assert rb.stdout == r.stdout
