@@ -46,6 +46,9 @@ from .config import (conditional_mode, default_device, default_jitter, expert_cr
 # both layers' K4, and both layers' K5, in one launch each in the step (False: one launch
 # per layer and kernel; A/B probes only)
 _K4_BATCHED = True
+# the training forward's colnorm_max (the C_k images' bound) on the side stream beside K3
+# (False: on the main stream right before K5; A/B probes only)
+_COLMAX_SIDE = True
 
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
@@ -233,11 +236,12 @@ class SVGPModified:
                                      stats=bufs.get("stats"), A=bufs.get("A32"),
                                      f16_variance=self.kernel.variance if fmt == "f16" else None, in_fmt=fmt)
 
-    def x6_expert(self, N, Afr, Lfr, stats, bufs, timing=None, fmt="x6"):
-        """K5 on images: fmean, fvar [K, N] (x6 mode)."""
+    def x6_expert(self, N, Afr, Lfr, stats, bufs, timing=None, fmt="x6", colmax_ready=False):
+        """K5 on images: fmean, fvar [K, N] (x6 mode).  colmax_ready: the C_k images'
+        column bound (colnorm_max of q_sqrt) is already in bufs["c_out"][1]."""
         with _Stage(timing, "expert_cond"):
             c_out = bufs.get("c_out")  # training (split-f16): C_k images for the backward
-            if c_out is not None:
+            if c_out is not None and not colmax_ready:
                 ops.colnorm_max(self.q_sqrt, out=c_out[1])
             return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, self.num_inducing, N,
                                              self.num_latent_gps, fmean=bufs.get("fmean"),
@@ -638,6 +642,8 @@ class SMGP(SGP):
                                            out=b["Kfr_" + L], fmt=fmt)
                     with _Stage(timing, "split_tri"):
                         ops.split_lower_x6(layer.q_sqrt, out=b["Lfr_" + L], fmt=fmt)
+                        if _COLMAX_SIDE and "colmax_" + L in b:   # training: the C_k bound, off the K3 -> K5 path
+                            ops.colnorm_max(layer.q_sqrt, out=b["colmax_" + L])
                     images[L] = (b["Kfr_" + L], b["Lfr_" + L])
                 if kl_out is not None:
                     with _Stage(timing, "gauss_kl"):
@@ -701,7 +707,7 @@ class SMGP(SGP):
                 Afr_f, st_f = pf.x6_trsm(N, LinvT["f"], images["f"][0], bf, timing, fmt, Tfr=Tfr["f"])
             if sched == "k1a_k5":            # beside the pred layer's K5
                 k1a_ev = side_kuf_a()
-                pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
+                pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt, colmax_ready=_COLMAX_SIDE)
             if k1a_ev is not None:
                 main.wait_event(k1a_ev)
             if not batched:
@@ -711,9 +717,10 @@ class SMGP(SGP):
                 with _Stage(timing, "expert_cond"):
                     c_outs = None
                     if bf.get("c_out") is not None and ba.get("c_out") is not None:
-                        c_outs = [bf["c_out"], ba["c_out"]]
-                        ops.colnorm_max(pf.q_sqrt, out=bf["c_out"][1])
-                        ops.colnorm_max(pa.q_sqrt, out=ba["c_out"][1])
+                        c_outs = [bf["c_out"], ba["c_out"]]   # bounds from the side stream's colnorm_max
+                        if not _COLMAX_SIDE:
+                            ops.colnorm_max(pf.q_sqrt, out=bf["c_out"][1])
+                            ops.colnorm_max(pa.q_sqrt, out=ba["c_out"][1])
                     ops.expert_conditional_f16_batch(
                         [Afr_f, Afr_a], [images["f"][1], images["a"][1]], [st_f, st_a],
                         [pf.kernel.variance, pa.kernel.variance], pf.num_inducing, N, pf.num_latent_gps,
@@ -721,8 +728,8 @@ class SMGP(SGP):
                         c_outs=c_outs)
             else:
                 if sched != "k1a_k5":
-                    pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt)
-                pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt)
+                    pf.x6_expert(N, Afr_f, images["f"][1], st_f, bufs["f"], timing, fmt, colmax_ready=_COLMAX_SIDE)
+                pa.x6_expert(N, Afr_a, images["a"][1], st_a, bufs["a"], timing, fmt, colmax_ready=_COLMAX_SIDE)
         else:
             for L, layer in layers:
                 if L in late:

@@ -16,6 +16,9 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     label = sys.argv[3] if len(sys.argv) > 3 else os.environ.get("MGP_HIP_LIB", "in-tree")
+    if "colmaxmain" in sys.argv[4:]:   # colnorm_max on the main stream before K5 (before round 4's move)
+        from modulatedgps_amd import models
+        models._COLMAX_SIDE = False
     if "k4single" in sys.argv[4:]:   # one K4 launch per layer (the round-4 default before the batch)
         from modulatedgps_amd import models
         models._K4_BATCHED = False
