@@ -137,6 +137,7 @@ SIGNATURES = {
                                        c_ptr, c_size, c_ptr]),
     "mgp_split_upper_f16": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_split_upper_f16_bounded": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_split_upper_f16_bounded_batch": (ctypes.c_int, [c_i32, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_x6_bound_ptr": (ctypes.c_void_p, [c_ptr, c_i64, c_i64, c_i32]),
     "mgp_trsm_stats_f16": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                           c_ptr, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),

@@ -93,6 +93,33 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
     store_split(img + f * 3 * 64 + lane, v);
 }
 
+// split_tri_kernel<false> (the split-f16 L^-T images) for two matrices at src and
+// src + stride into two images in one launch: blockIdx.y = the matrix (same fragments,
+// same arithmetic as two launches: bit-identical).
+__global__ __launch_bounds__(256) void split_upper2_kernel(const float* __restrict__ src, int64_t ld, int64_t stride,
+                                                           int64_t M, int nmb, int nmk, int64_t nfrag,
+                                                           bf16x8* __restrict__ img0, const float* __restrict__ bound0,
+                                                           bf16x8* __restrict__ img1,
+                                                           const float* __restrict__ bound1) {
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= nfrag) return;
+  const bool second = blockIdx.y != 0;
+  bf16x8* img = second ? img1 : img0;
+  const float* bound = second ? bound1 : bound0;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int mk = (int)(f % nmk);
+  const int mb = (int)((f / nmk) % nmb);
+  const int64_t mc = 32 * (int64_t)mb + r;
+  const float* S = src + (second ? stride : 0);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t m = 16 * (int64_t)mk + kperm(h, j);
+    v[j] = (m < M && mc < M && m <= mc) ? S[m * ld + mc] : 0.f;
+  }
+  store_split_f16<true>(img + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
+}
+
 // One wave per fragment block (nb, mk): grid.x = nnb * nmk / 4.
 __global__ __launch_bounds__(256) void split_cols_kernel(const float* __restrict__ A, int64_t lda, int64_t M,
                                                          int64_t N, int nmk, int64_t nfrag,
@@ -2440,6 +2467,34 @@ extern "C" int mgp_split_upper_f16_bounded(const float* LinvT, int64_t ldl, int6
   const float* bound = trailer(Tfr, lower_planes(M, 1));
   hipLaunchKernelGGL(split_tri_kernel<false>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      LinvT, ldl, (int64_t)0, M, nmb, nmk, nfrag, (bf16x8*)Tfr, bound);
+  return launch_status();
+}
+
+// mgp_split_upper_f16_bounded for `batch` (1 or 2) matrices at LinvT + b strideL into the
+// images Tfr[b] (host array of device pointers) in one launch; bit-identical.
+extern "C" int mgp_split_upper_f16_bounded_batch(int32_t batch, const float* LinvT, int64_t ldl, int64_t strideL,
+                                                 int64_t M, void* const* Tfr, size_t tfr_bytes,
+                                                 mgp_stream_t stream) {
+  if (batch < 1 || batch > 2) return -1;
+  if (!LinvT) return -2;
+  if (ldl < M) return -3;
+  if (batch > 1 && strideL < ldl * M) return -4;
+  if (M < 0) return -5;
+  if (!Tfr) return -6;
+  for (int b = 0; b < batch; ++b) {
+    if (!Tfr[b]) return -6;
+    if (!aligned16(Tfr[b])) return MGP_ERR_ALIGN;
+  }
+  if (M == 0) return MGP_OK;
+  if (tfr_bytes < mgp_x6_lower_bytes(M, 1)) return MGP_ERR_WORKSPACE;
+  const int64_t Mp = x6_mp(M);
+  const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
+  const int64_t nfrag = (int64_t)nmb * nmk;
+  void* t1 = Tfr[batch - 1];
+  hipLaunchKernelGGL(split_upper2_kernel, dim3((unsigned)((nfrag + 3) / 4), (unsigned)batch), dim3(256), 0,
+                     (hipStream_t)stream, LinvT, ldl, strideL, M, nmb, nmk, nfrag, (bf16x8*)Tfr[0],
+                     (const float*)trailer(Tfr[0], lower_planes(M, 1)), (bf16x8*)t1,
+                     (const float*)trailer(t1, lower_planes(M, 1)));
   return launch_status();
 }
 

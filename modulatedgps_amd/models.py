@@ -627,8 +627,11 @@ class SMGP(SGP):
         if b["x6"] and "Tfr_a" in b:
             # L^-T images straight after K3 on its stream (no cross-stream wait in front)
             with _Stage(timing, "split_tri"):
-                for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
-                    Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt, bounded=bounded)
+                if bounded and _K4_BATCHED:   # both layers' L^-T images in one launch (bit-identical)
+                    Tfr["f"], Tfr["a"] = ops.split_upper_f16_bounded_batch(b["LinvT2"], [b["Tfr_f"], b["Tfr_a"]])
+                else:
+                    for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
+                        Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt, bounded=bounded)
         sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
         late = {"overlap": (), "k1a_late": ("a",), "k1a_k5": ("a",), "k1_main": ("f", "a"),
                 "serial": ("f", "a")}[sched]

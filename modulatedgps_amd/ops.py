@@ -236,6 +236,19 @@ def split_upper_x6(LinvT, out=None, fmt="x6", bounded=False):
     return out
 
 
+def split_upper_f16_bounded_batch(LinvT, outs):
+    """split_upper_x6(LinvT[b], out=outs[b], fmt="f16", bounded=True) for every matrix of
+    LinvT [B, M, M] (B = len(outs) <= 2) in one launch (mgp_split_upper_f16_bounded_batch)."""
+    _check(LinvT, "LinvT", 3)
+    n, M = len(outs), LinvT.shape[1]
+    if LinvT.shape[0] < n:
+        raise ValueError("one LinvT matrix per image")
+    arr = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    _lib.call("mgp_split_upper_f16_bounded_batch", n, LinvT.data_ptr(), _ld(LinvT), LinvT.stride(0), M, arr,
+              min(o.numel() for o in outs), _stream())
+    return list(outs)
+
+
 def trsm_stats_x6(Tfr, Kfr, q_mu, M, N, Afr=None, stats=None, A=None, f16_variance=None, in_fmt="x6", cross=None):
     """K4 on images: A's image (for expert_conditional_x6) and the stats [T, K+1, N];
     also the f32 A when a buffer `A` [M, N] is given (training).  f16_variance

@@ -266,3 +266,22 @@ def test_expert_conditional_f16_batch_bit_identical(device, N, M, K, train):
         assert torch.equal(fvs[b], ref[b][1])
         if train:
             assert torch.equal(c_outs[b][0], ref[b][2])
+
+
+@pytest.mark.parametrize("M", [1024, 200])
+def test_split_upper_bounded_batch_bit_identical(device, M):
+    """mgp_split_upper_f16_bounded_batch (both layers' L^-T images in one launch) writes
+    the same image bits as one mgp_split_upper_f16_bounded call per layer."""
+    from modulatedgps_amd import ops
+    g = torch.Generator(device=device).manual_seed(3)
+    Zs = [torch.randn(M, 3, device=device, generator=g) for _ in range(2)]
+    var = [torch.tensor([0.8], device=device), torch.tensor([1.3], device=device)]
+    ls = [torch.tensor([0.9], device=device), torch.tensor([1.4], device=device)]
+    nb = ops.x6_lower_bytes(M, 1)
+    imgs = [torch.zeros(nb, dtype=torch.uint8, device=device) for _ in range(2)]
+    _, LinvT, _ = ops.kuu_potrf_trtri(Zs, var, ls, 1e-6, tfr_bound_images=imgs)
+    ref = [ops.split_upper_x6(LinvT[b], out=imgs[b].clone(), fmt="f16", bounded=True) for b in range(2)]
+    got = ops.split_upper_f16_bounded_batch(LinvT, [imgs[0].clone(), imgs[1].clone()])
+    torch.cuda.synchronize()
+    for b in range(2):
+        assert torch.equal(got[b], ref[b])
