@@ -1,5 +1,6 @@
 """CPU tests of the C-ABI boundary: libmgp_hip.so loads without a GPU and exports
 every function declared in include/mgp_hip.h (no compute calls are made)."""
+import os
 import ctypes
 
 import pytest
@@ -70,3 +71,11 @@ def test_library_reads_no_environment():
     imports no getenv (round 4 removed its per-call variant switches)."""
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"getenv\x00" not in data
+
+
+def test_integration_lists_every_entry():
+    """INTEGRATION.md §2a names every C-ABI entry of include/mgp_hip.h (with the
+    reference call site it replaces)."""
+    text = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "INTEGRATION.md")).read()
+    missing = [s for s in _lib.header_symbols() if f"`{s}`" not in text]
+    assert not missing, missing
