@@ -234,7 +234,7 @@ int mgp_split_upper_f16_bounded(const float* LinvT, int64_t ldl, int64_t M, void
  * (both layers' L^-T from one mgp_kuu_potrf_trtri_ex call) into the images Tfr[b]
  * (host array of device pointers) in one launch; bit-identical to one call each.
  * Replaces the operand preparation of triangular_solve(Lm, Kmn) in
- * base_conditional (models.py:141) for both layers. */
+ * base_conditional (models.py:141) for both layers.  -9: batch outside [1, 2]. */
 int mgp_split_upper_f16_bounded_batch(int32_t batch, const float* LinvT, int64_t ldl, int64_t strideL, int64_t M,
                                       void* const* Tfr, size_t tfr_bytes, mgp_stream_t stream);
 /* Device address of the split-f16 scale bound in an image's trailer: lower /

@@ -2475,7 +2475,7 @@ extern "C" int mgp_split_upper_f16_bounded(const float* LinvT, int64_t ldl, int6
 extern "C" int mgp_split_upper_f16_bounded_batch(int32_t batch, const float* LinvT, int64_t ldl, int64_t strideL,
                                                  int64_t M, void* const* Tfr, size_t tfr_bytes,
                                                  mgp_stream_t stream) {
-  if (batch < 1 || batch > 2) return -1;
+  if (batch < 1 || batch > 2) return -9;   // its own code (-1 .. -8 name the arguments)
   if (!LinvT) return -2;
   if (ldl < M) return -3;
   if (batch > 1 && strideL < ldl * M) return -4;

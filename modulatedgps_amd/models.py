@@ -270,16 +270,23 @@ class SVGPModified:
         return ops.expert_conditional_x6(Afr, Lfr, stats, self.kernel.variance, M, N, k1 - k0,
                                          planes=expert_planes(), fmt=fmt)
 
-    def _marginals_kn(self, Xnew):
+    def _marginals_kn(self, Xnew, tiled=None):
         """Xnew [..., N, D] -> (fmean, fvar, S, N, stride_s, lead): expert-major [K, cols]
         marginals where sample s of point n is column s * stride_s + n.  S tiled copies
         of one input (SGP.integrate, models.py:35-36) are computed once (stride_s = 0).
-        Tiling is recognised without a device sync: a device tensor whose sample axis
-        has stride 0 (what integrate() returns, an expand() view), or a host array
+        tiled=None recognises tiling without a device sync: a device tensor whose sample
+        axis has stride 0 (what integrate() returns, an expand() view), or a host array
         whose copies compare equal on the host; a materialised device copy of tiled
-        rows is computed row by row (the same values, S times the work)."""
+        rows (X[None].repeat(S, 1, 1), tf.tile's result) is then computed row by row (the
+        same values, S times the work and buffers).  tiled=True: the caller asserts the
+        S copies are equal and copy 0 is computed once (no check, no sync); tiled=False:
+        every row is computed."""
         host_tiled = False
-        if not isinstance(Xnew, torch.Tensor):
+        if tiled is not None:
+            if not isinstance(Xnew, torch.Tensor):
+                Xnew = torch.as_tensor(np.asarray(Xnew))
+            host_tiled = bool(tiled) and Xnew.dim() >= 3
+        elif not isinstance(Xnew, torch.Tensor):
             Xh = np.asarray(Xnew)
             if Xh.ndim >= 3:
                 Xh2 = Xh.reshape(-1, *Xh.shape[-2:])
@@ -320,11 +327,12 @@ class SVGPModified:
         and lengthscales (device tensors holding the constrained values)."""
         return (self.Z, self.q_mu, self.q_sqrt, self.kernel.variance, self.kernel.lengthscales)
 
-    def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
+    def predict_f(self, Xnew, full_cov=False, full_output_cov=False, tiled=None):
         """GPflow SVGP.predict_f(Xnew): posterior(NOCACHE).fused_predict_f, i.e. the
         Modified posterior's _conditional_fused (models.py:129-144).
-        Xnew [..., N, D] -> mean, var [..., N, K]."""
-        return self.posterior(PrecomputeCacheType.NOCACHE).fused_predict_f(Xnew, full_cov, full_output_cov)
+        Xnew [..., N, D] -> mean, var [..., N, K].  tiled: see _marginals_kn."""
+        return self.posterior(PrecomputeCacheType.NOCACHE).fused_predict_f(Xnew, full_cov, full_output_cov,
+                                                                          tiled=tiled)
 
 
 class PrecomputeCacheType:
@@ -353,23 +361,26 @@ class IndependentPosteriorSingleOutputModified:
         self.cache_type = precompute_cache
         self._layer = layer
 
-    def _conditional_fused(self, Xnew, full_cov=False, full_output_cov=False):
-        """(fmean, fvar) [..., N, K] of the whitened SVGP marginals (models.py:129-144)."""
+    def _conditional_fused(self, Xnew, full_cov=False, full_output_cov=False, tiled=None):
+        """(fmean, fvar) [..., N, K] of the whitened SVGP marginals (models.py:129-144).
+        tiled (extension): True when the caller's [S, N, D] input holds S equal copies
+        (computed once without a check), False to compute every row, None to detect
+        (SVGPModified._marginals_kn)."""
         if full_cov or full_output_cov:
             raise NotImplementedError("full_cov predictions are not used by the SMGP path")
-        fm, fv, S, N, stride, lead = self._layer._marginals_kn(Xnew)
+        fm, fv, S, N, stride, lead = self._layer._marginals_kn(Xnew, tiled=tiled)
         K = fm.shape[0]
         shape = (*lead, N, K)
         if stride == 0 and len(lead):
             return fm.t().expand(shape), fv.t().expand(shape)
         return fm.t().reshape(shape), fv.t().reshape(shape)
 
-    def fused_predict_f(self, Xnew, full_cov=False, full_output_cov=False):
+    def fused_predict_f(self, Xnew, full_cov=False, full_output_cov=False, tiled=None):
         """GPflow BasePosterior.fused_predict_f: _conditional_fused + the (Zero) mean function."""
-        return self._conditional_fused(Xnew, full_cov, full_output_cov)
+        return self._conditional_fused(Xnew, full_cov, full_output_cov, tiled=tiled)
 
-    def predict_f(self, Xnew, full_cov=False, full_output_cov=False):
-        return self.fused_predict_f(Xnew, full_cov, full_output_cov)
+    def predict_f(self, Xnew, full_cov=False, full_output_cov=False, tiled=None):
+        return self.fused_predict_f(Xnew, full_cov, full_output_cov, tiled=tiled)
 
 
 class RelaxedOneHotCategorical:
@@ -397,6 +408,8 @@ class RelaxedOneHotCategorical:
         per call); with W_dist(noise_z=...) and no seed every draw is fresh."""
         shape = tuple(sample_shape) if isinstance(sample_shape, (tuple, list)) else (int(sample_shape),)
         n = int(np.prod(shape)) if shape else 1
+        if n == 0:   # TFP: an empty sample, no draw (the RNG stream does not advance)
+            return self.logits.new_empty((*shape, *self.logits.shape))
         outs = []
         for i in range(n):
             u = None
@@ -517,7 +530,9 @@ class SMGP(SGP):
                                          ops.expert_x6_workspace_bytes(Mx, N, K)), dtype=torch.uint8,
                                      device=dev),
         }
-        if x6:  # the second layer's K5 workspace (both layers' K5 in one launch)
+        if x6 and Mf == Ma and forward_image_format(train) == "f16" and expert_cross() == "f16":
+            # the second layer's K5 workspace, only where both layers' K5 can run as one
+            # launch (split-f16 images with f16 cross terms, equal M)
             b["ws_expert2"] = torch.empty_like(b["ws_expert"])
         if x6:  # split-bf16 images: Kuf / tril(q_sqrt) per layer (built on the side
             # stream while K3 runs), A and L^-T shared by the layers (processed in turn)
@@ -753,29 +768,30 @@ class SMGP(SGP):
         return _splitmix64(self.seed * 0x100000001B3 + self._draws)
 
     # ------------------------------------------------------------------ reference methods
-    def W_dist(self, Xt, noise_z=None, seed=None, n_offset=0):
+    def W_dist(self, Xt, noise_z=None, seed=None, n_offset=0, tiled=None):
         """SMGP.W_dist (models.py:55-61): the assign layer's marginals, reparameterised
         with z ~ N(0, 1) [S, N, K] (utils.py:26-27) into logits [S * N, K], as a
         RelaxedOneHotCategorical(1e-2).  noise_z: explicit normals [S, N, K]; else
-        Philox with `seed` (a fresh key per call when None), K6's z stream."""
-        fm, fv, S, N, stride, _ = self.assign_layer._marginals_kn(Xt)
+        Philox with `seed` (a fresh key per call when None), K6's z stream.  tiled:
+        SVGPModified._marginals_kn's switch for materialised S-tiled inputs."""
+        fm, fv, S, N, stride, _ = self.assign_layer._marginals_kn(Xt, tiled=tiled)
         if seed is None and noise_z is None:
             seed = self.next_seed()
         logits = ops.assign_logits(fm, fv, S, N, stride, noise_z=noise_z, seed=seed or 0, n_offset=n_offset)
         return RelaxedOneHotCategorical(TAU, logits.reshape(S * N, self.K), (S, N), seed=seed, n_offset=n_offset,
                                         model=self)
 
-    def E_log_p_Y(self, Xt, Y, W_SND):
+    def E_log_p_Y(self, Xt, Y, W_SND, tiled=None):
         """SMGP.E_log_p_Y (models.py:63-67): logsumexp_S(sum_K W ve) - log S -> [N]
         (device float32), ve the pred likelihood's variational expectation."""
-        fm, fv, S, N, stride, _ = self.pred_layer._marginals_kn(Xt)
+        fm, fv, S, N, stride, _ = self.pred_layer._marginals_kn(Xt, tiled=tiled)
         Yd = _to_dev(Y, self.device).reshape(-1).contiguous()
         W = _to_dev(W_SND, self.device)
         mc = self._mc_eps()
         lik_var = None if mc is not None else self.likelihood.likelihood.variance.reshape(-1)
         extra = {}
         if self._assign_lik_var() is not None:   # SMGPModified.E_log_p_Y (models.py:112-123)
-            fa, va, Sa, Na, stride_a, _ = self.assign_layer._marginals_kn(Xt)
+            fa, va, Sa, Na, stride_a, _ = self.assign_layer._marginals_kn(Xt, tiled=tiled)
             if (Sa, Na, stride_a) != (S, N, stride):
                 raise ValueError("the two layers' marginals disagree in shape")
             extra = dict(mu_a=fa, var_a=va, assign_lik_var=self._assign_lik_var())

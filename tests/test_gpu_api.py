@@ -56,6 +56,11 @@ def test_posterior_conditional_fused(device, case):
     assert lay._marginals_kn(Xd)[4] == X.shape[0]
     fm4, fv4 = post._conditional_fused(Xe)
     assert normwise(to_np(fm4), to_np(fm)) < 1e-6 and normwise(to_np(fv4), to_np(fv)) < 1e-6
+    # explicit opt-in for a materialised tiled copy (tf.tile's result): computed once,
+    # the same bits as the stride-0 view; tiled=False computes every row
+    assert lay._marginals_kn(Xd, tiled=True)[4] == 0 and lay._marginals_kn(Xe, tiled=False)[4] == X.shape[0]
+    fm5, fv5 = post._conditional_fused(Xd, tiled=True)
+    assert torch.equal(fm5, fm4) and torch.equal(fv5, fv4)
     # distinct inputs per sample (no tiling): one conditional over all S * N rows
     rng = np.random.default_rng(3)
     Xr = X[None] + 0.1 * rng.standard_normal((S,) + X.shape)
@@ -88,6 +93,11 @@ def test_w_dist_and_sample(device):
     W3 = wd3.sample()
     assert tuple(W3.shape) == (S * N, K)
     assert tuple(wd3.sample((2, 2)).shape) == (2, 2, S * N, K)
+    # an empty sample (TFP: shape [0, S * N, K]) draws nothing: the model's key stream
+    # does not advance
+    draws = model._draws
+    assert tuple(wd3.sample(0).shape) == (0, S * N, K) and tuple(wd3.sample((0, 3)).shape) == (0, 3, S * N, K)
+    assert model._draws == draws
     # explicit normals and no seed: every sample() call draws a fresh key
     wd4 = model.W_dist(Xt, noise_z=z)
     assert not torch.equal(wd4.sample(), wd4.sample())

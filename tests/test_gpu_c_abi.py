@@ -41,7 +41,8 @@ def _write_problem(path, X, Y, p, z, u):
         f.write(f32(u).tobytes())
 
 
-@pytest.mark.parametrize("N,M,K,D,ls,S", [(2000, 64, 3, 2, 0.8, 5), (4099, 130, 4, 3, 1.0, 9)])
+@pytest.mark.parametrize("N,M,K,D,ls,S", [(2000, 64, 3, 2, 0.8, 5), (4099, 130, 4, 3, 1.0, 9),
+                                          (65536, 1024, 8, 8, 1.0, 25)])   # BASELINE config 3 in full
 def test_elbo_through_the_c_abi_alone(device, tmp_path, N, M, K, D, ls, S):
     if not os.path.exists(BIN):
         pytest.fail(f"{BIN} is missing: run __graft_entry__.build() (it builds the C-ABI host program)")

@@ -93,6 +93,17 @@ def test_elbo_and_grad(device, N, M, K, D, ls, S, modified, fmt):
         config.set_expert_cross(old_cross)
 
 
+def test_elbo_and_grad_c3_full(device):
+    """The gradient the bench's training line runs, at BASELINE config 3 in full
+    (N = 65536, M = 1024, K = 8, D = 8, S = 25, lengthscale 1.0) in the default
+    split-f16 format, against float64 autograd of oracle/grad_ref.py with the same
+    explicit noise and the same floors as test_elbo_and_grad (the oracle takes ~1 min
+    and ~25 GB on the host).  The per-block errors (HIP / float32 autograd) are printed."""
+    from modulatedgps_amd import config
+    assert config.expert_format() == "f16" and config.expert_cross() == "f16"
+    _check_elbo_and_grad(device, 65536, 1024, 8, 8, 1.0, 25, False)
+
+
 def _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, floor=None, floors=None):
     floor = FLOOR if floor is None else floor
     floors = floors or {}

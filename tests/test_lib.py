@@ -79,3 +79,13 @@ def test_integration_lists_every_entry():
     text = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "INTEGRATION.md")).read()
     missing = [s for s in _lib.header_symbols() if f"`{s}`" not in text]
     assert not missing, missing
+
+
+def test_batch_entries_reject_out_of_range_batch():
+    """The layer-batch entries take batch in [1, 2] and reject anything else with a
+    code of their own (documented in mgp_hip.h) before any HIP call."""
+    lib = _lib.load()
+    p = (ctypes.c_void_p * 3)(8, 8, 8)
+    assert lib.mgp_split_upper_f16_bounded_batch(3, ctypes.c_void_p(8), 64, 4096, 64, p, 1 << 20, None) == -9
+    assert lib.mgp_split_upper_f16_bounded_batch(0, ctypes.c_void_p(8), 64, 4096, 64, p, 1 << 20, None) == -9
+    assert lib.mgp_split_upper_f16_bounded_batch(1, None, 64, 4096, 64, p, 1 << 20, None) == -2
