@@ -114,6 +114,23 @@ int mgp_kuu_potrf_trtri_ex(const float* const* Z, int64_t ldz, int64_t M, int32_
                            float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                            void* workspace, size_t workspace_bytes, void* prep_done,
                            float* const* linvt_absmax, mgp_stream_t stream);
+/* mgp_kuu_potrf_trtri_ex that also writes the Kuf image of every batch entry,
+ * K(Z_b, X) (models.py:139, self.kernel.K(Z, Xnew), for pred_layer and assign_layer),
+ * exactly as mgp_rbf_kuf_f16 (kfr_format 1) / mgp_rbf_kuf_x6 (kfr_format 0) write it
+ * (bit-identical): the image blocks run on extra workgroups of the factorisation's
+ * step launches, on the CUs the latency-bound chain leaves idle, instead of as
+ * separate launches beside it.  X [N][ldx]; Kfr: host array of `batch` device
+ * pointers, each at least mgp_x6_cols_bytes(M, N) bytes (kfr_bytes), 16-B aligned.
+ * With M <= 64 (no step launches) the images are written by mgp_rbf_kuf_* launches
+ * on the stream after the Kuu build.  -19 .. -24: X, ldx, N, Kfr, kfr_bytes,
+ * kfr_format. */
+int mgp_kuu_potrf_trtri_kuf(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                            const float* const* variance, const float* const* lengthscales,
+                            const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                            float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                            void* workspace, size_t workspace_bytes, void* prep_done,
+                            float* const* linvt_absmax, const float* X, int64_t ldx, int64_t N,
+                            void* const* Kfr, size_t kfr_bytes, int32_t kfr_format, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K4
  * Whitened projection A = L^-1 Kuf (as the triangular GEMM LinvT^T . Kuf) plus

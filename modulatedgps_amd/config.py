@@ -21,7 +21,7 @@ import torch
 #              work.  The training step follows it (A's image, S_k A in the
 #              backward); the reduced-plane modes use "x6".
 _CFG = {"jitter": 1e-6, "device": None, "conditional": "x6", "expert_planes": 3, "expert_format": "f16",
-        "expert_cross": "f16", "step_schedule": "overlap"}
+        "expert_cross": "f16", "step_schedule": "k1_in_k3"}
 # expert_cross (f16 images): the precision of K5's two cross-term products
 #              a_hi b_lo + a_lo b_hi -- "f16" (three f16 products) or "f8" (one
 #              e4m3 MFMA per two k-steps for both, mgp_expert_conditional_f16x8:
@@ -96,8 +96,15 @@ def set_expert_cross(cross):
 # step_schedule (x6 mode): where the Cholesky-independent work of an ELBO step runs
 #              relative to the latency-bound K3 chain (host-side launch order only;
 #              every schedule computes the same bits):
+#   "k1_in_k3" (default since round 5) both layers' K1 run inside K3's step launches, on
+#              extra workgroups that take the CUs the latency-bound chain leaves idle
+#              (mgp_kuu_potrf_trtri_kuf: the same image blocks, bit-identical); the
+#              tril(q_sqrt) images and the KL on the side stream as in "overlap".  Beside
+#              the chain on a side stream, K1's 8192 workgroups held the CUs that the
+#              next step launch's workgroups waited for (32-41 us gaps, round 4 stamps);
+#              with batched K3 only (equal M for both layers), else as "overlap";
 #   "overlap"  K1 and the tril(q_sqrt) images of both layers and the KL on a side
-#              stream beside K3 (round 1-3 default);
+#              stream beside K3 (round 1-4 default);
 #   "k1a_late" the assign layer's K1 on the side stream after K3, beside the pred
 #              layer's K4 (one K1 beside the chain instead of two);
 #   "k1a_k5"   as k1a_late, but the layers run K4, K5 of the pred layer before the
@@ -105,7 +112,7 @@ def set_expert_cross(cross):
 #   "k1_main"  both K1 on the main stream after K3 (only the small images and
 #              the KL beside the chain);
 #   "serial"   everything on the main stream, K3 alone on the chip.
-STEP_SCHEDULES = ("overlap", "k1a_late", "k1a_k5", "k1_main", "serial")
+STEP_SCHEDULES = ("k1_in_k3", "overlap", "k1a_late", "k1a_k5", "k1_main", "serial")
 
 
 def step_schedule():

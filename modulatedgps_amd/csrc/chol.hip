@@ -31,7 +31,9 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <vector>
 
+#include "kuf_image.hpp"
 #include "mgp_common.hpp"
 
 namespace mgp {
@@ -78,6 +80,11 @@ struct CholArgs {
   float* lt_absmax[kMaxBatch];                    // optional per batch: max |L^-T| (float bits, atomicMax)
   double* ws; int64_t strideWS;                   // per batch: W, B tile-major [nb][nb][64][64], D [nb][64][64]
   int64_t M, Mp; int nb;
+  // optional Kuf side job (mgp_kuu_potrf_trtri_kuf): the Kuf image of every batch entry,
+  // K(Z_b, X) (kuf_image.hpp blocks), written by extra workgroups of the step launches
+  const float* kx; int64_t kldx, kN;
+  bf16x8* kfr[kMaxBatch]; float* kbound[kMaxBatch];
+  int kf16, knmk, krow_blocks; int64_t kblocks;   // blocks per batch entry
 };
 
 __device__ __forceinline__ double* ws_W(const CholArgs& a, int b) { return a.ws + (int64_t)b * a.strideWS; }
@@ -952,6 +959,48 @@ __global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j
   }
 }
 
+// ------------------------------------------------------------------ Kuf side job
+// Kuf image blocks [k0, k1) (batch-major: block b * kblocks + bid is block bid of entry b's
+// image) run by the `nkwg` extra workgroups of a step launch, two blocks per pass (one per
+// 256-thread group).  The step kernel's LDS holds one of its workgroups per CU, so these
+// workgroups take CUs the launch's tile workgroups leave idle; the blocks are the ones
+// rbf_kuf_x6_kernel runs (same function, same bits).  Every pass is uniform across the
+// workgroup (a group without a block joins the barriers).
+template <int DM>
+__device__ __forceinline__ void kuf_side_blocks(const CholArgs& a, int w, int64_t k0, int64_t k1, int nkwg,
+                                                float* lds) {
+  const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+  const int t = (int)(threadIdx.x & 255);
+  const int64_t per = 2 * (int64_t)nkwg;
+  const int64_t passes = (k1 - k0 + per - 1) / per;
+  for (int64_t it = 0; it < passes; ++it) {
+    const int64_t item = k0 + it * per + 2 * w + g;
+    const bool active = item < k1;
+    const int b = __builtin_amdgcn_readfirstlane(active ? (int)(item / a.kblocks) : 0);
+    // this batch entry's operands: scalar loads from the kernel-argument segment at a
+    // dynamic index (`a` is the by-value kernel argument at its offset 0; indexing `a`
+    // itself would copy the whole struct to scratch)
+    typedef const CholArgs __attribute__((address_space(4))) KernargCholArgs;
+    const KernargCholArgs& ag = *(const KernargCholArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const KufImageArgs ka = {a.kx, a.kldx, ag.Z[b], a.ldz, a.kN, a.M, a.D, ag.var[b], ag.ls[b], ag.n_ls[b],
+                             a.knmk, a.krow_blocks, ag.kfr[b], ag.kbound[b]};
+    const int64_t bid = item - b * a.kblocks;
+    if (a.kf16) kuf_image_block<DM, true>(ka, bid, t, active, lds);
+    else kuf_image_block<DM, false>(ka, bid, t, active, lds);
+  }
+}
+
+__device__ __forceinline__ void kuf_side_job(const CholArgs& a, int w, int64_t k0, int64_t k1, int nkwg, float* lds0,
+                                          float* lds1) {
+  float* lds = (threadIdx.x >> 8) ? lds1 : lds0;
+  if (a.D <= 1) kuf_side_blocks<1>(a, w, k0, k1, nkwg, lds);
+  else if (a.D <= 2) kuf_side_blocks<2>(a, w, k0, k1, nkwg, lds);
+  else if (a.D <= 4) kuf_side_blocks<4>(a, w, k0, k1, nkwg, lds);
+  else if (a.D <= 8) kuf_side_blocks<8>(a, w, k0, k1, nkwg, lds);
+  else if (a.D <= 16) kuf_side_blocks<16>(a, w, k0, k1, nkwg, lds);
+  else kuf_side_blocks<32>(a, w, k0, k1, nkwg, lds);
+}
+
 // ------------------------------------------------------------------ step launch j, tile pairs
 // chol_step with the trailing-update and forward-substitution tiles of step j taken two
 // at a time along a tile row i, one 256-thread group per tile in a 512-thread
@@ -962,10 +1011,11 @@ __global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j
 // two groups' MFMAs share every SIMD (two waves each), so a step's tiles take half the
 // workgroups for about the time of one.  Per tile the products are chol_step's, on the same
 // operands in the same order: L and L^-T are bit-identical.
-// After P_i the groups take their tiles' own paths: a __syncthreads on one path waits
-// for the live waves of both groups wherever they are, so it still orders that group's
-// own LDS hand-off (and a group that has ended is not waited for: a barrier counts only
-// the waves that have not terminated).
+// Barriers are uniform: every __syncthreads of the kernel is reached by all eight waves of
+// the workgroup on every path (the look-ahead's idle group joins each barrier of the
+// factorisation with no work, lookahead_factor's `active`; after P_i the pair's two groups
+// run their tiles' products barrier-free, and the diagonal tile's LDS hand-off barrier sits
+// outside the tile-kind branches), so no barrier depends on which waves are still live.
 // Row i's tiles in order: the heavy tiles first -- the off-diagonal update tiles (i, l),
 // l = j + 1 .. i - 1 (rows i > j + 1), then the forward-substitution tiles (i, c), c < j --,
 // then the two light ones, the diagonal tile (i, i) (rows i > j + 1) and (i, j) (X_jj = D_j,
@@ -988,8 +1038,16 @@ __host__ __device__ inline int step_pair_count(int nb, int j) {  // per batch en
 // the round-robin placement (speed only, nothing depends on it): a row's pairs then load
 // its panel tile W_ij into one L2 and a run's rows (of one batch entry where the run
 // does not straddle two) share the panel tiles W_lj, B_jc there.  No idle workgroups.
-__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb) {
+// Workgroups past batch (1 + Pb) (when the launch carries a Kuf side job): kuf_side_job
+// over the image blocks [k0, k1), nkwg of them.
+__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb, int64_t k0,
+                                                               int64_t k1, int nkwg) {
   __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB];
+  if ((int)blockIdx.x >= batch * (1 + Pb)) {   // uniform per workgroup
+    kuf_side_job(a, (int)blockIdx.x - batch * (1 + Pb), k0, k1, nkwg, reinterpret_cast<float*>(s1),
+                 reinterpret_cast<float*>(sD));
+    return;
+  }
   ENTRYTIME(t_entry);
   // the kernel arguments every workgroup reads, loaded at entry as one batch of scalar
   // loads behind one wait (the compiler had placed each at its first use: three dependent
@@ -1287,8 +1345,43 @@ extern "C" size_t mgp_chol_workspace_bytes(int64_t M, int32_t batch) {
   return (size_t)chol_ws_doubles_per_batch(M) * (size_t)batch * sizeof(double);
 }
 
+// The Kuf side job of a factorisation (mgp_kuu_potrf_trtri_kuf): X [N][ldx] and one image per
+// batch entry (split-f16 when f16, else split-bf16), each of at least mgp_x6_cols_bytes(M, N).
+struct KufSideJob {
+  const float* X; int64_t ldx, N;
+  void* const* Kfr; bool f16;
+};
+
+extern "C" size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
+
+// Share of the image blocks per step launch j: proportional to the CUs the launch's tile
+// workgroups leave idle (one workgroup per CU: the step kernel's LDS), at least an eighth
+// of the CUs each.
+static void kuf_side_split(int nb, int batch, int64_t total, std::vector<int64_t>& beg, std::vector<int>& nwg) {
+  int cus = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int steps = nb - 1;
+  std::vector<double> idle(steps);
+  double sum = 0.0;
+  for (int j = 0; j < steps; ++j) {
+    idle[j] = std::max<double>(cus - batch * (1 + step_pair_count(nb, j)), cus / 8.0);
+    sum += idle[j];
+  }
+  beg.assign(steps + 1, 0);
+  nwg.assign(steps, 0);
+  double acc = 0.0;
+  for (int j = 0; j < steps; ++j) {
+    acc += idle[j];
+    beg[j + 1] = j + 1 == steps ? total : std::min<int64_t>(total, (int64_t)(total * (acc / sum) + 0.5));
+    const int64_t cnt = beg[j + 1] - beg[j];
+    nwg[j] = (int)std::min<int64_t>((cnt + 1) / 2, (int64_t)idle[j]);
+  }
+}
+
 static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s,
-                    hipEvent_t prep_done = nullptr) {
+                    hipEvent_t prep_done = nullptr, const KufSideJob* kj = nullptr) {
   if (!workspace || workspace_bytes < mgp_chol_workspace_bytes(a.M, batch)) return MGP_ERR_WORKSPACE;
   if (!aligned16(workspace)) return MGP_ERR_ALIGN;
   // the diagonal tiles of L and L^-T are written with 16-byte stores
@@ -1299,6 +1392,20 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
   a.strideWS = chol_ws_doubles_per_batch(a.M);
   a.ws = (double*)workspace;
   const dim3 block(kCholThreads);
+  std::vector<int64_t> kbeg;
+  std::vector<int> knwg;
+  if (kj && kj->N > 0 && a.M > 0) {
+    a.kx = kj->X; a.kldx = kj->ldx; a.kN = kj->N; a.kf16 = kj->f16 ? 1 : 0;
+    const int64_t mp = (a.M + 127) / 128 * 128;
+    a.knmk = (int)(mp / 16);
+    a.krow_blocks = kuf_row_blocks(a.M);
+    a.kblocks = kuf_blocks(a.M, kj->N);
+    for (int b = 0; b < batch; ++b) {
+      a.kfr[b] = (bf16x8*)kj->Kfr[b];
+      a.kbound[b] = (float*)((char*)kj->Kfr[b] + mgp_x6_cols_bytes(a.M, kj->N) - 256);  // image trailer
+    }
+    if (a.nb >= 2) kuf_side_split(a.nb, batch, batch * a.kblocks, kbeg, knwg);
+  }
   hipLaunchKernelGGL(chol_prep, dim3(a.nb * a.nb + 1, batch), block, 0, s, a);
   int st = launch_status();
   if (st) return st;
@@ -1306,11 +1413,23 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
     st = hip_status(hipEventRecord(prep_done, s));
     if (st) return st;
   }
+  if (kj && kj->N > 0 && a.M > 0 && a.nb < 2) {   // no step launches to carry the job: K1's own launches
+    for (int b = 0; b < batch; ++b) {
+      st = kj->f16 ? mgp_rbf_kuf_f16(kj->X, kj->ldx, a.Z[b], a.ldz, kj->N, a.M, a.D, a.var[b], a.ls[b], a.n_ls[b],
+                                     kj->Kfr[b], mgp_x6_cols_bytes(a.M, kj->N), s)
+                   : mgp_rbf_kuf_x6(kj->X, kj->ldx, a.Z[b], a.ldz, kj->N, a.M, a.D, a.var[b], a.ls[b], a.n_ls[b],
+                                    kj->Kfr[b], mgp_x6_cols_bytes(a.M, kj->N), s);
+      if (st) return st;
+    }
+  }
   for (int j = 0; j < a.nb; ++j) {
     const int T = a.nb - j - 1;
     if (T > 0) {
       const int Pb = step_pair_count(a.nb, j);
-      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb)), dim3(kPairThreads), 0, s, a, j, batch, Pb);
+      const bool side = !kbeg.empty() && knwg[j] > 0;
+      const int nkwg = side ? knwg[j] : 0;
+      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb) + nkwg), dim3(kPairThreads), 0, s, a, j, batch, Pb,
+                         side ? kbeg[j] : (int64_t)0, side ? kbeg[j + 1] : (int64_t)0, nkwg);
     } else {
       hipLaunchKernelGGL(chol_last_step, dim3(a.nb, batch), block, 0, s, a, j);
     }
@@ -1345,7 +1464,8 @@ static int kuu_potrf_trtri_impl(const float* const* Z, int64_t ldz, int64_t M, i
                                    const int32_t* n_ls, float jitter, int32_t batch, float* L,
                                    float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                                    void* workspace, size_t workspace_bytes, hipEvent_t prep_done,
-                                   float* const* lt_absmax, mgp_stream_t stream) {
+                                   float* const* lt_absmax, mgp_stream_t stream,
+                                   const KufSideJob* kj = nullptr) {
   if (!Z) return -1;
   if (ldz < D) return -2;
   if (M < 0) return -3;
@@ -1370,7 +1490,7 @@ static int kuu_potrf_trtri_impl(const float* const* Z, int64_t ldz, int64_t M, i
   a.ldz = ldz; a.D = D; a.jitter = (double)jitter;
   a.L = L; a.LinvT = LinvT; a.ldl = ldl; a.strideL = strideL;
   a.info = info; a.M = M;
-  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream, prep_done);
+  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream, prep_done, kj);
 }
 
 extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
@@ -1400,6 +1520,32 @@ extern "C" int mgp_kuu_potrf_trtri_ex(const float* const* Z, int64_t ldz, int64_
                                       float* const* linvt_absmax, mgp_stream_t stream) {
   return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
                               info, workspace, workspace_bytes, (hipEvent_t)prep_done, linvt_absmax, stream);
+}
+
+extern "C" int mgp_kuu_potrf_trtri_kuf(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                                       const float* const* variance, const float* const* lengthscales,
+                                       const int32_t* n_ls, float jitter, int32_t batch, float* L,
+                                       float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
+                                       void* workspace, size_t workspace_bytes, void* prep_done,
+                                       float* const* linvt_absmax, const float* X, int64_t ldx, int64_t N,
+                                       void* const* Kfr, size_t kfr_bytes, int32_t kfr_format,
+                                       mgp_stream_t stream) {
+  if (!X) return -19;
+  if (ldx < D) return -20;
+  if (N < 0) return -21;
+  if (!Kfr) return -22;
+  if (kfr_format != 0 && kfr_format != 1) return -24;
+  if (D > 32) return MGP_ERR_UNSUPPORTED;
+  if (M > 0 && N > 0 && batch > 0 && batch <= kMaxBatch) {
+    if (kfr_bytes < mgp_x6_cols_bytes(M, N)) return -23;
+    for (int b = 0; b < batch; ++b) {
+      if (!Kfr[b]) return -22;
+      if (!aligned16(Kfr[b])) return MGP_ERR_ALIGN;
+    }
+  }
+  const KufSideJob kj = {X, ldx, N, Kfr, kfr_format == 1};
+  return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
+                              info, workspace, workspace_bytes, (hipEvent_t)prep_done, linvt_absmax, stream, &kj);
 }
 
 extern "C" size_t mgp_chol_backward_workspace_bytes(int64_t M) {

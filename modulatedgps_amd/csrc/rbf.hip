@@ -17,6 +17,7 @@
 // exp(-0.5 r2) is evaluated as exp2(-r2') with c_d = sqrt(0.5 log2 e) / l_d.
 #include <type_traits>
 
+#include "kuf_image.hpp"
 #include "mgp_common.hpp"
 
 namespace mgp {
@@ -81,105 +82,18 @@ __global__ __launch_bounds__(kRbfThreads) void rbf_kernel(
   }
 }
 
-// K1 writing Kuf's split-bf16 image (split3.hip layout) instead of f32 Kuf.
-// r2 = |z'|^2 + |x'|^2 - 2 z'.x' (scaled inputs, the expanded form GPflow's
-// square_distance uses) is ONE [32 x (D + 2)] x [(D + 2) x 32] product on
-// v_mfma_f32_32x32x2_f32 (exact f32 products): rows of Z carry (z', |z'|^2, 1),
-// columns of X carry (-2 x', 1, |x'|^2).  The accumulator of that MFMA holds
-// row (r & 3) + 8 (r >> 2) + 4 h of column l & 31 in register r -- exactly the
-// order of an image fragment: registers 0..7 / 8..15 of a 32x32 tile are the
-// lane's 8 elements of k-steps 2 mb / 2 mb + 1.  So each lane finishes its 16
-// values with one exp2 and one multiply each (variance and, split-f16, the
-// image's power-of-two scale folded into one per-lane multiplier that is 0 on
-// padded columns), splits them and stores 16-B fragments.
-// Workgroup = 4 waves x 32 columns x 128 rows (4 row tiles per wave); the
-// workgroups walk down a column group first (adjacent image windows).
-// Rows >= M and columns >= N of the padded image are written as zeros.
-// F16: split-f16 image instead (mgp_rbf_kuf_f16): Kuf <= variance, so the image
-// scale is 2^img_exp(variance) and the trailer `bound` receives the variance.
+// K1 writing Kuf's split-bf16 / split-f16 image (split3.hip layout) instead of f32
+// Kuf: one block of kuf_image.hpp per 256-thread workgroup (the body, its layout and
+// numerics are documented there; the K3 step launches run the same blocks as their
+// Kuf side job, mgp_kuu_potrf_trtri_kuf).
 template <int DMAX, bool F16 = false>
 __global__ __launch_bounds__(kRbfThreads) void rbf_kuf_x6_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ Z, int64_t ldz, int64_t N,
     int64_t M, int D, const float* __restrict__ variance, const float* __restrict__ ls, int n_ls, int nmk,
     bf16x8* __restrict__ Kfr, float* __restrict__ bound, int row_blocks) {
-  constexpr int KS = (DMAX + 1) / 2;     // MFMA k-steps over the dims (2 each) ...
-  constexpr int KA = KS + 1;             // ... + one for the (|z'|^2, 1) x (1, |x'|^2) terms
-  constexpr int DP = 2 * KA + 1;         // LDS row pitch (odd: spreads banks)
-  __shared__ float zs[128 * DP];
-  __shared__ float cs[2 * KS];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, c32 = lane & 31;
-  const int64_t bid = blockIdx.x;
-  const int64_t rb = bid % row_blocks, cg = bid / row_blocks;
-  const int64_t nb = cg * 4 + w;
-  const int64_t n = 32 * nb + c32;
-  const int64_t m0 = 128 * rb;
-  const float kHalfLog2e = 0.8493218002880191f;  // sqrt(0.5 * log2(e))
-  if (t < 2 * KS) cs[t] = (t < D) ? kHalfLog2e / ls[n_ls == 1 ? 0 : t] : 0.f;
-  __syncthreads();
-  for (int i = t; i < 128 * 2 * KS; i += kRbfThreads) {
-    const int r = i / (2 * KS), d = i % (2 * KS);
-    const int64_t m = m0 + r;
-    zs[r * DP + d] = (m < M && d < D) ? Z[m * ldz + d] * cs[d] : 0.f;
-  }
-  float xk[KA], xx = 0.f;
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int d = 2 * s + h;
-    const float xd = (n < N && d < D) ? X[n * ldx + d] * cs[d] : 0.f;
-    xx = fmaf(xd, xd, xx);
-    xk[s] = -2.f * xd;
-  }
-  xx += __shfl_xor(xx, 32, 64);  // the two lane halves hold the even / odd dims
-  xk[KS] = h ? xx : 1.f;         // k = 2 KS: |z'|^2 * 1, k = 2 KS + 1: 1 * |x'|^2
-  __syncthreads();
-  if (t < 128) {
-    float a = 0.f;
-#pragma unroll
-    for (int d = 0; d < 2 * KS; ++d) a = fmaf(zs[t * DP + d], zs[t * DP + d], a);
-    zs[t * DP + 2 * KS] = a;
-    zs[t * DP + 2 * KS + 1] = 1.f;
-  }
-  __syncthreads();
-  const float var = variance[0];
-  // the image scale (a power of two, split-f16) and the variance fold into one
-  // per-lane multiplier; padded columns (n >= N) get 0 (their r2 is finite)
-  float mult = var;
-  if constexpr (F16) {
-    mult = var * ldexpf(1.f, img_exp(var));
-    if (bid == 0 && t == 0) *bound = var;
-  }
-  if (n >= N) mult = 0.f;
-  auto tiles = [&](auto ragged) {
-    constexpr bool RAGGED = decltype(ragged)::value;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      floatx16 acc;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-      for (int s = 0; s < KA; ++s) acc = mfma32x32x2(zs[(32 * i + c32) * DP + 2 * s + h], xk[s], acc);
-      const int64_t mb = (m0 >> 5) + i;
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          // acc = r2 >= 0 up to rounding; raw v_exp_f32 (results below 2^-126 flush)
-          v[j] = __builtin_amdgcn_exp2f(-acc[8 * half + j]) * mult;
-          if constexpr (RAGGED)
-            if (m0 + 32 * i + acc_row(8 * half + j, lane) >= M) v[j] = 0.f;
-        }
-        if constexpr (F16)
-          store_split_f16(Kfr + ((nb * nmk + 2 * mb + half) * 3) * 64 + lane, v, 1.f);
-        else
-          store_split(Kfr + ((nb * nmk + 2 * mb + half) * 3) * 64 + lane, v);
-      }
-    }
-  };
-  if (m0 + 128 <= M)   // uniform: only the last row block is ragged
-    tiles(std::false_type{});
-  else
-    tiles(std::true_type{});
+  __shared__ float lds[kuf_block_lds_floats<DMAX>()];
+  const KufImageArgs a = {X, ldx, Z, ldz, N, M, D, variance, ls, n_ls, nmk, row_blocks, Kfr, bound};
+  kuf_image_block<DMAX, F16>(a, blockIdx.x, threadIdx.x, true, lds);
 }
 
 static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, int64_t N, int64_t M,

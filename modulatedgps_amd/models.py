@@ -566,12 +566,14 @@ class SMGP(SGP):
         self._bufs[key] = b
         return b
 
-    def _factorise(self, b, prep_event=None, tfr_bounds=False):
+    def _factorise(self, b, prep_event=None, tfr_bounds=False, kuf=None):
         """Kuu of both layers and their batched Cholesky + inverse (one K3 sweep).
         Training buffers also keep L (b["L_f"], b["L_a"]) for the backward pass.
         prep_event: recorded once Kuu is built (batched path only; else after K3).
         tfr_bounds: K3 also writes max |LinvT| into the L^-T split-f16 images'
-        trailers (b["Tfr_f"], b["Tfr_a"]; batched path), for bounded splits."""
+        trailers (b["Tfr_f"], b["Tfr_a"]; batched path), for bounded splits.
+        kuf: (X, fmt) -- K3's step launches also write both layers' Kuf images
+        (b["Kfr_f"], b["Kfr_a"]; batched path, schedule "k1_in_k3")."""
         pf, pa = self.pred_layer, self.assign_layer
         train = b.get("train", False)
         if "LinvT2" in b:
@@ -582,7 +584,8 @@ class SMGP(SGP):
                 [pf.Z, pa.Z], [pf.kernel.variance, pa.kernel.variance],
                 [pf.kernel.lengthscales, pa.kernel.lengthscales], default_jitter(), LinvT=b["LinvT2"],
                 L=b.get("L2"), want_L=train, prep_event=prep_event,
-                tfr_bound_images=[b["Tfr_f"], b["Tfr_a"]] if tfr_bounds else None)
+                tfr_bound_images=[b["Tfr_f"], b["Tfr_a"]] if tfr_bounds else None,
+                kuf=(kuf[0], [b["Kfr_f"], b["Kfr_a"]], kuf[1]) if kuf is not None else None)
             self.last_info = info
             if train:
                 b["L_f"], b["L_a"] = Lo[0], Lo[1]
@@ -636,8 +639,15 @@ class SMGP(SGP):
         # split-f16 L^-T images: K3 folds their scale bound (max |LinvT|) into its
         # writes of the inverse, so the split needs no reduction launches
         bounded = b["x6"] and "Tfr_a" in b and "LinvT2" in b and fmt == "f16"
+        sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
+        # schedule k1_in_k3: both layers' K1 as a side job of K3's step launches (batched K3)
+        k1_in_k3 = (sched == "k1_in_k3" and "LinvT2" in b and self.pred_layer.kernel._x(X) is X
+                    and self.assign_layer.kernel._x(X) is X)
+        if sched == "k1_in_k3" and not k1_in_k3:
+            sched = "overlap"
         with _Stage(timing, "kuu_chol"):
-            LinvT_f, LinvT_a = self._factorise(b, prep_event=prep, tfr_bounds=bounded)
+            LinvT_f, LinvT_a = self._factorise(b, prep_event=prep, tfr_bounds=bounded,
+                                               kuf=(X, fmt) if k1_in_k3 else None)
         Tfr = {}
         if b["x6"] and "Tfr_a" in b:
             # L^-T images straight after K3 on its stream (no cross-stream wait in front)
@@ -647,14 +657,13 @@ class SMGP(SGP):
                 else:
                     for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
                         Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt, bounded=bounded)
-        sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
-        late = {"overlap": (), "k1a_late": ("a",), "k1a_k5": ("a",), "k1_main": ("f", "a"),
+        late = {"k1_in_k3": (), "overlap": (), "k1a_late": ("a",), "k1a_k5": ("a",), "k1_main": ("f", "a"),
                 "serial": ("f", "a")}[sched]
         if b["x6"]:
             def side_work():
                 for L, layer in layers:
                     X_ = layer.kernel._x(X)
-                    if L not in late:
+                    if L not in late and not k1_in_k3:
                         with _Stage(timing, "rbf_kuf"):
                             ops.rbf_kuf_x6(X_, layer.Z, layer.kernel.variance, layer.kernel.lengthscales,
                                            out=b["Kfr_" + L], fmt=fmt)
@@ -708,7 +717,8 @@ class SMGP(SGP):
             bf, ba = bufs["f"], bufs["a"]
             # both layers' K4 in one launch (mgp_trsm_stats_f16_batch, bit-identical to
             # two): one kernel tail and dispatch-round boundary fewer (~25 us, measured)
-            batched = (_K4_BATCHED and sched in ("overlap", "k1_main", "serial") and fmt == "f16" and expert_cross() == "f16"
+            batched = (_K4_BATCHED and sched in ("k1_in_k3", "overlap", "k1_main", "serial") and fmt == "f16"
+                       and expert_cross() == "f16"
                        and pf.num_inducing == pa.num_inducing and pf.num_latent_gps == pa.num_latent_gps
                        and all(x.get("Afr") is not None and x.get("stats") is not None for x in (bf, ba))
                        and bf["Afr"].data_ptr() != ba["Afr"].data_ptr()

@@ -124,14 +124,17 @@ def potrf_trtri(A, L=None, LinvT=None, info=None, workspace=None):
 
 
 def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, info=None,
-                    workspace=None, want_L=False, prep_event=None, tfr_bound_images=None):
+                    workspace=None, want_L=False, prep_event=None, tfr_bound_images=None, kuf=None):
     """Kuu (float64, from Z) + Cholesky + inverse for a batch of layers sharing M, D.
     Zs / variances / lengthscales: lists of device tensors.  Returns L (or None),
     LinvT [B, M, M] and info int32 [B].  prep_event: a torch.cuda.Event (already
     created) recorded once Kuu is built (mgp_kuu_potrf_trtri_ev).
     tfr_bound_images: per layer, the L^-T split-f16 image buffer whose trailer
     receives max |LinvT| (mgp_kuu_potrf_trtri_ex; then split_upper_x6(...,
-    bounded=True) skips its reduction)."""
+    bounded=True) skips its reduction).
+    kuf: (X [N, D], [image per layer], fmt "f16" | "x6"): the factorisation's step
+    launches also write each layer's Kuf image K(Z_b, X), bit-identical to
+    rbf_kuf_x6(X, Z_b, ..., fmt=fmt) (mgp_kuu_potrf_trtri_kuf)."""
     import ctypes
     Bt = len(Zs)
     M, D = Zs[0].shape
@@ -155,7 +158,25 @@ def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, inf
     vp = P(*[v.data_ptr() for v in variances])
     lp = P(*[l.data_ptr() for l in lengthscales])
     nl = (ctypes.c_int32 * Bt)(*[l.numel() for l in lengthscales])
-    if tfr_bound_images is not None:
+    if kuf is not None:
+        lib = _lib.load()
+        X, imgs, fmt = kuf
+        _check(X, "X", 2)
+        if X.shape[1] != D or len(imgs) != Bt:
+            raise ValueError("kuf: X must have Z's D columns and one image per layer")
+        kb = lib.mgp_x6_cols_bytes(M, X.shape[0])
+        if min(t.numel() for t in imgs) < kb:
+            raise ValueError("kuf: an image buffer is smaller than mgp_x6_cols_bytes(M, N)")
+        bp = None
+        if tfr_bound_images is not None:
+            bp = P(*[lib.mgp_x6_bound_ptr(t.data_ptr(), M, 0, 1) for t in tfr_bound_images])
+        _lib.call("mgp_kuu_potrf_trtri_kuf", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
+                  L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
+                  LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(),
+                  prep_event.cuda_event if prep_event is not None else None, bp,
+                  X.data_ptr(), _ld(X), X.shape[0], P(*[t.data_ptr() for t in imgs]),
+                  min(t.numel() for t in imgs), {"x6": 0, "f16": 1}[fmt], _stream())
+    elif tfr_bound_images is not None:
         lib = _lib.load()
         bp = P(*[lib.mgp_x6_bound_ptr(t.data_ptr(), M, 0, 1) for t in tfr_bound_images])
         _lib.call("mgp_kuu_potrf_trtri_ex", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,

@@ -393,3 +393,30 @@ def test_expert_conditional_planes(device):
         assert normwise(fm.T, mu_ref) < 1e-4  # fmean comes from K4 (x6) in every mode
         assert errs[planes] < tol, (planes, errs[planes])
     print("K5 planes fvar normwise error vs float64:", errs)
+
+
+@pytest.mark.parametrize("N,M,D,ard", [(65536, 1024, 8, False), (4099, 130, 3, True), (777, 300, 1, False),
+                                       (1000, 40, 2, False), (513, 256, 20, True)])
+@pytest.mark.parametrize("fmt", ["f16", "x6"])
+def test_kuu_potrf_trtri_kuf_side_job(device, N, M, D, ard, fmt):
+    """mgp_kuu_potrf_trtri_kuf: the Kuf images K(Z_b, X) of both layers written by extra
+    workgroups of K3's step launches (M = 40: no step launches, K1's own launches) are
+    byte-identical to mgp_rbf_kuf_f16 / mgp_rbf_kuf_x6's (trailer included), and L, L^-T
+    and info are those of the factorisation without the job.  c3's shape in full first."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(N + M + D)
+    X = _t(rng.standard_normal((N, D)), device)
+    Zs = [_t(rng.standard_normal((M, D)), device) for _ in range(2)]
+    var = [_t([0.7], device), _t([0.3], device)]
+    ls = [_t(rng.uniform(0.8, 2.0, D) if ard else [1.1], device), _t(rng.uniform(0.8, 2.0, D) if ard else [0.9], device)]
+    nbytes = ops._lib.load().mgp_x6_cols_bytes(M, N)
+    ref = [torch.zeros(nbytes, dtype=torch.uint8, device=device) for _ in range(2)]
+    got = [torch.zeros(nbytes, dtype=torch.uint8, device=device) for _ in range(2)]
+    for b in range(2):
+        ops.rbf_kuf_x6(X, Zs[b], var[b], ls[b], out=ref[b], fmt=fmt)
+    L0, LinvT0, info0 = ops.kuu_potrf_trtri(Zs, var, ls, 1e-6, want_L=True)
+    L1, LinvT1, info1 = ops.kuu_potrf_trtri(Zs, var, ls, 1e-6, want_L=True, kuf=(X, got, fmt))
+    torch.cuda.synchronize()
+    for b in range(2):
+        assert torch.equal(got[b], ref[b]), b
+    assert torch.equal(L1, L0) and torch.equal(LinvT1, LinvT0) and torch.equal(info1, info0)

@@ -1,0 +1,26 @@
+# Round-5: K1 as a side job of K3's step launches (schedule k1_in_k3, now the default):
+# its bit-identity test first, then the new round-5 tests, the bench line in both
+# schedules on one box (A/B) and a kernel trace of the bench.
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05c
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_kernels.py -k "kuf_side_job or potrf" > $O/pytest_k3kuf.txt 2>&1 || { tail -40 $O/pytest_k3kuf.txt; exit 1; }
+tail -2 $O/pytest_k3kuf.txt
+timeout -k 10 60 tools/simd_share_probe > $O/simd_share_probe.log 2>&1 || { tail -5 $O/simd_share_probe.log; exit 1; }
+cat $O/simd_share_probe.log
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 400 --timeout-method thread -s tests -m gpu > $O/pytest_gpu.txt 2>&1 || { tail -40 $O/pytest_gpu.txt; exit 1; }
+grep -E "passed|failed|C-ABI" $O/pytest_gpu.txt | tail -6
+for r in 1 2; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-modes > $O/bench_k1k3_$r.json 2> $O/bench_k1k3_$r.err || { tail -5 $O/bench_k1k3_$r.err; exit 1; }
+  MGP_STEP_SCHEDULE=overlap timeout -k 10 300 python bench.py --no-cpu-baseline --no-modes > $O/bench_overlap_$r.json 2> $O/bench_overlap_$r.err || { tail -5 $O/bench_overlap_$r.err; exit 1; }
+done
+python - <<'PY'
+import json
+for n in ("k1k3_1", "overlap_1", "k1k3_2", "overlap_2"):
+    d = json.load(open(f"gpurun_out/r05c/bench_{n}.json"))
+    k = d["kernels"]
+    print(n, round(d["value"], 1), "kuu_chol", round(k["kuu_chol"]["avg_us"], 1), "K4", round(k["trsm_stats"]["avg_us"], 1),
+          "K5", round(k["expert_cond"]["avg_us"], 1), "train", round(d["train"]["value"], 2))
+PY
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --no-modes --steps 50 > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
+echo r05c-ok
