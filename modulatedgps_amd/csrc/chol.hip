@@ -78,7 +78,7 @@ struct CholArgs {
   float* L; float* LinvT; int64_t ldl, strideL;   // L may be NULL
   int32_t* info;
   float* lt_absmax[kMaxBatch];                    // optional per batch: max |L^-T| (float bits, atomicMax)
-  double* ws; int64_t strideWS;                   // per batch: W, B tile-major [nb][nb][64][64], D, LS [nb][64][64]
+  double* ws; int64_t strideWS;                   // per batch: W, B tile-major [nb][nb][64][64], D [nb][64][64]
   int64_t M, Mp; int nb;
   // optional Kuf side job (mgp_kuu_potrf_trtri_kuf): the Kuf image of every batch entry,
   // K(Z_b, X) (kuf_image.hpp blocks), written by extra workgroups of the step launches
@@ -97,12 +97,6 @@ __device__ __forceinline__ double* ws_tile(const CholArgs& a, double* base, int 
 }
 __device__ __forceinline__ double* ws_D(const CholArgs& a, int b, int j) {
   return ws_W(a, b) + 2 * a.Mp * a.Mp + (int64_t)j * CB * CB;
-}
-// LS[k] = L_{k+1,k} (float64, 64 x 64): the subdiagonal tile the look-ahead workgroup of
-// step launch k - 1 forms by triangular solves beside its factorisation (RowPrep), read as
-// the panel tile P of row k + 1 by step launch k (k >= 1; LS[0] = P of launch 0's look-ahead)
-__device__ __forceinline__ double* ws_LS(const CholArgs& a, int b, int k) {
-  return ws_W(a, b) + 2 * a.Mp * a.Mp + ((int64_t)a.nb + k) * CB * CB;
 }
 
 // Element (gr, gc) of the padded input matrix, in float64.
@@ -673,18 +667,11 @@ __device__ __forceinline__ doublex4 neg_x_times(const double* __restrict__ Xii, 
 // Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
 // sPend (optional, may alias sX): the caller's pending update sF -= sPend sPend^T
 // of the lower blocks right of column block 0 (column block 0 already applied).
-// hook: run by the caller's other waves (active = false) in phase ph = 0 .. 8 of the nine
-// between the barriers (S0 U0 S1 U1 S2 U2 S3 I1 I2 = 0 .. 8), beside the factorisation.
-struct NoHook {
-  __device__ __forceinline__ void operator()(int) const {}
-};
-template <typename Hook = NoHook>
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0,
-                                                 const double* sPend, bool active, Hook& hook) {
-  // active = false: the caller's other waves take part in every barrier and do no work of
-  // the factorisation (w = 4 matches no role; they run `hook`), so the barrier sequence is
-  // the same for all waves
+                                                 const double* sPend = nullptr, bool active = true) {
+  // active = false: the caller's idle waves take part in every barrier and do no work
+  // (w = 4 matches no role), so the barrier sequence is the same for all waves
   const int w = active ? (ctid() >> 6) : 4, lane = ctid() & 63;
   int bad = 0;
   const int js = (int)(gcol0 / CB) - 1;
@@ -695,8 +682,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     const int bi1 = (w == 3) ? 3 : 2, bj1 = (w == 1) ? 1 : (w == 2 ? 2 : 3);
     sub_outer_blk<4>(sF, 16 * bi0, 16 * bj0, sPend, sPend);
     sub_outer_blk<4>(sF, 16 * bi1, 16 * bj1, sPend, sPend);
-  } else if (w == 4) {
-    hook(0);
   }
   STAMP(js, 8);
   __syncthreads();
@@ -708,8 +693,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
       const int i = q < 3 ? 0 : (q < 5 ? 1 : 2), j = q < 3 ? q + 1 : (q < 5 ? q - 1 : 3);
       blk_store(sX + 16 * i * LDT + 16 * j, doublex4{0.0, 0.0, 0.0, 0.0});
     }
-  } else if (w == 4) {
-    hook(1);
   }
   __syncthreads();
   STAMP(js, 9);
@@ -722,24 +705,19 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     sub_outer_blk<1>(sF, 48, 32, P0, P0);
   } else if (w == 3) {
     sub_outer_blk<1>(sF, 48, 48, P0, P0);  // update 0 of (3,3)
-  } else if (w == 4) {
-    hook(2);
   }
   STAMP(js, 10);
   __syncthreads();
   if (w < 2) sub_outer_blk<1>(sF, 32 + 16 * w, 32, sF + 16, sF + 16);  // update 1 of (2,2), (3,2)
-  else if (w == 4) hook(3);
   __syncthreads();
   STAMP(js, 11);
   if (w == 0) panel_factor<2>(sF, col, lane, bad);
   else if (w == 1) inv_diag_block(sF, sX, col, 1, lane);
   else if (w == 2) sub_outer_blk<1>(sF, 48, 48, sF + 16, sF + 16);  // update 1 of (3,3)
-  else if (w == 4) hook(4);
   STAMP(js, 12);
   __syncthreads();
   if (w == 0) panel_update<2>(sF, 0, 1);
   else if (w == 1) inv_offdiag_block(sF, sX, 1, 0, lane);
-  else if (w == 4) hook(5);
   __syncthreads();
   auto L_ = [&](int bi, int bj) { return sF + 16 * bi * LDT + 16 * bj; };
   auto X_ = [&](int bi, int bj) { return sX + 16 * bi * LDT + 16 * bj; };
@@ -768,8 +746,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     doublex4 t = {0.0, 0.0, 0.0, 0.0};
     blk_mma<false>(t, L_(3, 1), X_(1, 1), 1.0);
     blk_store(S_(3, 1), t);
-  } else if (w == 4) {
-    hook(6);
   }
   __syncthreads();
   STAMP(js, 5);
@@ -787,8 +763,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     doublex4 y = blk_load(S_(3, 1));
     blk_mma<false>(y, L_(3, 2), X_(2, 1), 1.0);
     blk_store(S_(3, 1), y);
-  } else if (w == 4) {
-    hook(7);
   }
   __syncthreads();
   STAMP(js, 13);
@@ -805,8 +779,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     blk_store(S_(3, 0), zero4);
     blk_mma<false>(y, L_(3, 2), X_(2, 0), 1.0);
     blk_store(X_(3, 0), neg_x_times(X_(3, 3), y, lane));
-  } else if (w == 4) {
-    hook(8);
   }
   __syncthreads();
 }
@@ -912,8 +884,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     build_tile(s1, LDT, 0, 0, reinterpret_cast<float*>(s2));
     __syncthreads();
     STAMP(63, 1);
-    NoHook nh;
-    factor_diag_tile(s1, s2, col, a.info + b, 0, nullptr, true, nh);
+    factor_diag_tile(s1, s2, col, a.info + b, 0);
     __syncthreads();
     STAMP(63, 2);
     write_diag(a, b, 0, s1, s2);
@@ -935,203 +906,21 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ look-ahead row preparation
-// Group 1 of the look-ahead workgroup of step launch j (which factors tile s = j + 1) prepares
-// tile row r = j + 2 for launch j + 1, beside the factorisation -- its work is cut into the
-// factorisation's nine phases (factor_diag_tile's hook) and the write phase, so the barrier
-// sequence stays uniform and the chain does not wait for it:
-//   L_{r,j}   = W_{r,j} D_j^T                     (the pairs' P_i of row r: same products, same bits)
-//   W'_{r,s}  = W_{r,s} - L_{r,j} L_{s,j}^T          (step j's update of tile (r, s); L_{s,j} = LS[j])
-//   F         = W_{r,r} - L_{r,j} L_{r,j}^T          (step j's update of tile (r, r))
-//   L_{r,s}   = W'_{r,s} L_ss^-T by column blocks q as soon as panel q and X_qq = L_qq^-1 are
-//               final: Y_q = L_{r,s}[:, q]^T = X_qq (W'_{r,s}[:, q]^T - sum_{p<q} L_ss[q][p] Y_p)
-//   F        -= sum_q L_{r,s}[:, q] L_{r,s}[:, q]^T  (step s's update of tile (r, r))
-// and writes LS[j + 1] = L_{r,s} and W_{r,r} = F, updated through step s: the next launch's
-// look-ahead factors F at once (no P = W D^T, no update of its column block 0 on the chain),
-// and its pairs take LS[j + 1] as the panel tile P of row r.  Wave v of the group owns the
-// 16-column stripe v of the transposed tiles (row stripe v of W'_{r,s} and L_{r,s}): the
-// accumulators of W'^T and Y are then directly the B operands of the next products, and the
-// strips of Y_q pass through LDS (ys) for F's blocks.  F's ten lower blocks are dealt as in
-// diag_lower_update (v, v + 4, v + 8).
-constexpr int YP = CB + 2;   // pitch (doubles) of a Y strip [16][YP]
-
-struct RowPrep {
-  const double* LSj;   // L_{s,j} (global, 64 x 64, ld CB)
-  double* sL;          // W_{r,j} -> L_{r,j} (LDS)
-  const double* sDj;   // D_j (LDS)
-  const double* sF;    // the tile being factored: L_ss column blocks as the panels complete
-  const double* sX;    // its inverse: X_qq as the diagonal blocks complete
-  double* ys;          // three Y strips [16][YP] (LDS)
-  double* LSout;       // LS[j + 1] (global)
-  double* Wrr;         // tile (r, r) of W (global)
-  bool on;             // this wave prepares a row (group 1 of a launch with r < nb)
-  bool form_l;         // L_{r,j} still to form (launches with j >= 1: in phase 0)
-  doublex4 wt[4], y[4], f[3];
-
-  __device__ __forceinline__ int v() const { return ctid() >> 6; }
-  __device__ __forceinline__ int lane() const { return ctid() & 63; }
-  __device__ __forceinline__ void blk_of(int n, int& bi, int& bj) const {   // lower block n of 10
-    bi = 0;
-    while ((bi + 1) * (bi + 2) / 2 <= n) ++bi;
-    bj = n - bi * (bi + 1) / 2;
-  }
-  // initial accumulators: W_{r,s}^T blocks (q, v) and F's owned lower blocks, from global
-  __device__ __forceinline__ void load(const double* __restrict__ Wrs) {
-    const int l16 = lane() & 15, kq = lane() >> 4, vv = v();
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) wt[q][r] = Wrs[(16 * vv + l16) * CB + 16 * q + kq + 4 * r];
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int n = vv + 4 * m;
-      if (n < 10) {
-        int bi, bj;
-        blk_of(n, bi, bj);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) f[m][r] = Wrr[(16 * bi + kq + 4 * r) * CB + 16 * bj + l16];
-      }
-    }
-  }
-  // L_{r,j} = W_{r,j} D_j^T, row stripe v, in place (each wave reads and writes its own stripe)
-  __device__ __forceinline__ void form_L() {
-    Blk4 t = blk4_zero();
-    row_mma<true, 1>(t, sL, sDj, 1.0);
-    blk4_to_lds<true>(sL, t);
-  }
-  // W'^T[q][v] -= L_{s,j}[q rows] L_{r,j}[v rows]^T (L_{s,j} from global: LS[j])
-  template <int q>
-  __device__ __forceinline__ void upd_W() {
-    const int l16 = lane() & 15, kq = lane() >> 4, vv = v();
-    double av[16], bv[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      av[t] = LSj[(16 * q + l16) * CB + 4 * t + kq];
-      bv[t] = sL[(16 * vv + l16) * LDT + 4 * t + kq];
-    }
-#pragma unroll
-    for (int t = 0; t < 16; ++t) wt[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[t], bv[t], wt[q], 0, 0, 0);
-  }
-  // F -= L_{r,j} L_{r,j}^T on the owned lower blocks (all stripes of L_{r,j}: after a barrier)
-  __device__ __forceinline__ void upd_F_L() {
-    const int l16 = lane() & 15, kq = lane() >> 4, vv = v();
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int n = vv + 4 * m;
-      if (n < 10) {
-        int bi, bj;
-        blk_of(n, bi, bj);
-        double av[16], bv[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          av[t] = sL[(16 * bi + l16) * LDT + 4 * t + kq];
-          bv[t] = sL[(16 * bj + l16) * LDT + 4 * t + kq];
-        }
-#pragma unroll
-        for (int t = 0; t < 16; ++t) f[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[t], bv[t], f[m], 0, 0, 0);
-      }
-    }
-  }
-  // Y_q = X_qq (W'^T[q] - sum_{p<q} L_ss[q][p] Y_p) for stripe v, written to strip `st`
-  template <int q, int st>
-  __device__ __forceinline__ void form_Y() {
-    const int l16 = lane() & 15, kq = lane() >> 4, vv = v();
-    doublex4 t = wt[q];
-#pragma unroll
-    for (int p = 0; p < q; ++p) {
-      double av[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) av[k] = sF[(16 * q + l16) * LDT + 16 * p + 4 * k + kq];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) t = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[k], y[p][k], t, 0, 0, 0);
-    }
-    double xv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) xv[k] = sX[(16 * q + l16) * LDT + 16 * q + 4 * k + kq];
-    doublex4 yq = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) yq = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[k], t[k], yq, 0, 0, 0);
-    y[q] = yq;
-    double* sy = ys + st * 16 * YP;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sy[(kq + 4 * r) * YP + 16 * vv + l16] = yq[r];
-  }
-  // F -= L_{r,s}[:, q] L_{r,s}[:, q]^T on the owned lower blocks, from strip `st` (Y_q of every
-  // stripe: after a barrier)
-  template <int st>
-  __device__ __forceinline__ void upd_F_Y() {
-    const int l16 = lane() & 15, kq = lane() >> 4, vv = v();
-    const double* sy = ys + st * 16 * YP;
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int n = vv + 4 * m;
-      if (n < 10) {
-        int bi, bj;
-        blk_of(n, bi, bj);
-        double av[4], bv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          av[k] = sy[(4 * k + kq) * YP + 16 * bi + l16];
-          bv[k] = sy[(4 * k + kq) * YP + 16 * bj + l16];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[k], bv[k], f[m], 0, 0, 0);
-      }
-    }
-  }
-  __device__ __forceinline__ void store() {
-    const int l16 = lane() & 15, kq = lane() >> 4, vv = v();
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) LSout[(16 * vv + l16) * CB + 16 * q + kq + 4 * r] = y[q][r];
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int n = vv + 4 * m;
-      if (n < 10) {
-        int bi, bj;
-        blk_of(n, bi, bj);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Wrr[(16 * bi + kq + 4 * r) * CB + 16 * bj + l16] = f[m][r];
-      }
-    }
-  }
-  // phase ph of factor_diag_tile (0 .. 8), 9 = the write phase after it
-  __device__ __forceinline__ void operator()(int ph) {
-    if (!on) return;
-    switch (ph) {
-      case 0: if (form_l) form_L(); upd_W<0>(); break;                 // S0
-      case 2: upd_W<1>(); upd_W<2>(); upd_W<3>(); break;                // S1 (L_{r,j}: own stripe)
-      case 4: upd_F_L(); form_Y<0, 0>(); break;                         // S2: X_00 (S1), all of L_{r,j}
-      case 6: form_Y<1, 1>(); upd_F_Y<0>(); break;                      // S3: X_11 (S2), L_ss[1][0]
-      case 7: form_Y<2, 2>(); upd_F_Y<1>(); break;                      // I1: X_22 (S3), L_ss[2][0..1]
-      case 8: form_Y<3, 0>(); break;                                    // I2: X_33 (I1), L_ss[3][0..2]
-      case 9: upd_F_Y<2>(); upd_F_Y<0>(); store(); break;               // write phase
-      default: break;
-    }
-  }
-};
-
 // ------------------------------------------------------------------ step launch j
-// The look-ahead's factorisation of tile (j+1, j+1), group 0: with pend, s1 holds P =
-// L_{j+1,j} and s2 the tile with column block 0 of -P P^T still to apply (launch 0); else s2
-// holds the tile updated through step j (prepared by the previous launch's RowPrep).  rp:
-// group 1's row preparation beside it (rp->on false: group 1 idles).
+// The look-ahead's factorisation of tile (j+1, j+1): s1 holds P = L_{j+1,j}, s2 the
+// tile with column block 0 of -P P^T still to apply.
 __device__ __forceinline__ void lookahead_factor(const CholArgs& a, int b, int j, double* s1, double* s2,
-                                                 double* col, bool active, bool pend, RowPrep& rp) {
-  if (pend) {
-    // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
-    // lower blocks are applied beside the first panel sweep
-    if (active) sub_outer_blk<4>(s2, 16 * (ctid() >> 6), 0, s1, s1);
-    __syncthreads();
-  }
+                                                 double* col, bool active) {
+  // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
+  // lower blocks are applied beside the first panel sweep
+  if (active) sub_outer_blk<4>(s2, 16 * (ctid() >> 6), 0, s1, s1);
+  __syncthreads();
   STAMP(j, 3);
   STAMP(j, 4);
-  factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, pend ? s1 : nullptr, active, rp);
+  factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1, active);
   STAMP(j, 6);
   __syncthreads();
   if (active) write_diag(a, b, j + 1, s2, s1);
-  else rp(9);
   __syncthreads();
   STAMP(j, 7);
   RSTAMP(j, 15);
@@ -1235,9 +1024,7 @@ __device__ __forceinline__ void kuf_side_job(const CholArgs& a, int w, int64_t k
 // workgroup) on every row whose tile count is even, instead of each holding a heavy tile's
 // workgroup to the heavy tile's length with one group idle.
 constexpr int kPairThreads = 2 * kCholThreads;
-// Rows j + 1 and j + 2 have no trailing-update tiles in launch j: tile (j+1, j+1) is the
-// look-ahead's, tiles (j+2, j+1) and (j+2, j+2) are prepared beside it (RowPrep).
-__host__ __device__ inline int step_row_tiles(int i, int j) { return i <= j + 2 ? j + 1 : i + 1; }
+__host__ __device__ inline int step_row_tiles(int i, int j) { return i == j + 1 ? j + 1 : i + 1; }
 __host__ __device__ inline int step_row_pairs(int i, int j) { return (step_row_tiles(i, j) + 1) / 2; }
 __host__ __device__ inline int step_pair_count(int nb, int j) {  // per batch entry
   int n = 0;
@@ -1255,8 +1042,7 @@ __host__ __device__ inline int step_pair_count(int nb, int j) {  // per batch en
 // over the image blocks [k0, k1), nkwg of them.
 __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb, int64_t k0,
                                                                int64_t k1, int nkwg) {
-  // col: the pivots' reciprocal roots [CB], then RowPrep's three Y strips [3][16][YP]
-  __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB + 3 * 16 * YP];
+  __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB];
   if ((int)blockIdx.x >= batch * (1 + Pb)) {   // uniform per workgroup
     kuf_side_job(a, (int)blockIdx.x - batch * (1 + Pb), k0, k1, nkwg, reinterpret_cast<float*>(s1),
                  reinterpret_cast<float*>(sD));
@@ -1304,65 +1090,37 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     if (lt_max) wave_absmax_atomic(m, lt_max);
   };
   if (wg < batch) {
-    // look-ahead: tile s = j + 1 on group 0 (the chain), row r = j + 2 for the next launch on
-    // group 1 (RowPrep), every barrier taken by both groups.  Launch 0 forms P = W_{1,0} D_0^T
-    // and applies it (as every launch did before round 5); from launch 1 on the tile arrives
-    // updated through step j (the previous launch's RowPrep) and is factored at once.
+    // look-ahead: tile (j+1, j+1).  Both groups load and form P = W_{j+1,j} D_j^T (group 0
+    // column blocks 0 and 3, group 1 blocks 1 and 2: equal MFMA counts, as the pairs'
+    // P_i); the factorisation then runs on group 0 while group 1's waves take part in
+    // every barrier and do no work (uniform barrier sequence)
     const bool act = g == 0;
-    const int s = j + 1, r = j + 2;
-    const bool deep = j >= 1, prep = r < a.nb;
     RSTAMP(j, 14);
     STAMP(j, 0);
-    TileRegs rP, rF, rD, rW;
+    TileRegs r1, rD, r2;
     if (act) {
-      if (!deep) tile_fetch(rP, Wt(s, j), CB);
-      tile_fetch(rF, Wt(s, s), CB);
-    } else {
+      tile_fetch(r1, Wt(i, j), CB);
       tile_fetch_lower(rD, ws_D(a, b, j), CB);
-      if (prep) tile_fetch(rW, Wt(r, j), CB);
-    }
-    // group 1's LDS: L_{r,j} in s2[1], D_j in sD, the Y strips after the four tiles
-    double* ys = &col[CB];
-    RowPrep rp;
-    rp.on = !act && prep;
-    if (rp.on) {
-      rp.LSj = ws_LS(a, b, j);
-      rp.sL = s2[1];
-      rp.sDj = sD;
-      rp.sF = s2[0];
-      rp.sX = s1;
-      rp.ys = ys;
-      rp.LSout = ws_LS(a, b, j + 1);
-      rp.Wrr = Wt(r, r);
-      rp.form_l = deep;
-      rp.load(Wt(r, s));
+    } else {
+      tile_fetch(r2, Wt(i, i), CB);
     }
     if (act) {
-      if (!deep) tile_put(s1, rP);
-      tile_put(s2[0], rF);
-    } else {
+      tile_put(s1, r1);
       tile_put(sD, rD);
-      if (prep) tile_put(s2[1], rW);
+    } else {
+      tile_put(s2[0], r2);
     }
     __syncthreads();
     STAMP(j, 1);
-    if (!deep) {
-      // launch 0: P = L_{1,0} on group 0 (also to LS[0] for RowPrep), L_{2,0} on group 1
-      Blk4 pi = blk4_zero();
-      if (act) row_mma<true, 1>(pi, s1, sD, 1.0);
-      else if (prep) rp.form_L();
-      __syncthreads();
-      if (act) {
-        blk4_to_lds<true>(s1, pi);
-        if (prep) {
-          row_to_global(ws_LS(a, b, 0), CB, pi);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // performed before group 1 reads it
-        }
-      }
-      __syncthreads();
-      STAMP(j, 2);
-    }
-    lookahead_factor(a, b, j, s1, s2[0], col, act, !deep, rp);
+    Blk4 pi = blk4_zero();
+    if (act) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);
+    else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
+    __syncthreads();
+    if (act) blk4_to_lds<true, 0x9>(s1, pi);
+    else blk4_to_lds<true, 0x6>(s1, pi);
+    __syncthreads();
+    STAMP(j, 2);
+    lookahead_factor(a, b, j, s1, s2[0], col, act);
     return;
   }
   // pair q of row i: tiles e = 2 q, 2 q + 1 of the row
@@ -1372,32 +1130,27 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   const bool pst = i == a.nb - 1 && q == 0 && b == 0;   // debug stamps only
   PAIRSTAMP_AT(pst, j, 7, t_entry);
   PAIRSTAMP(pst, j, 0);
-  const bool lead = i <= j + 2;                    // rows without trailing-update tiles
-  const int nh = lead ? 0 : i - j - 1;             // off-diagonal update tiles of the row
+  const int nh = (i == j + 1) ? 0 : i - j - 1;  // off-diagonal update tiles of the row
   int l = -1, c = -1;                              // update tile (i, l) or B tile (i, c)
   if (e < nh) l = j + 1 + e;
   else if (e < nh + j) c = e - nh;
-  else if (!lead && e == nh + j) l = i;
+  else if (i > j + 1 && e == nh + j) l = i;
   else c = j;
   const bool upd = has && l >= 0;
   const bool fwd = has && c >= 0 && c < j;  // forward-substitution tile reading B_jc
-  // from launch 1 on, P of row j + 1 is LS[j] (the previous look-ahead's RowPrep): row j + 1's
-  // P_i and an update tile's P_l with l = j + 1 are loaded, not formed
-  const bool pre_i = j >= 1 && i == j + 1;
-  const bool pre_l = j >= 1 && upd && l == j + 1;
-  const bool first = (upd && l != i && !pre_l) || fwd;  // P_l / X_jc before the update
+  const bool first = (upd && l != i) || fwd;  // P_l / X_jc before the update
   double* sT = s2[g];
   // this tile's operands: sT's tile (when it reads one) and the updated tile (u)
   TileRegs r1, rD, r2;
   Blk4 u = blk4_zero();  // B_ij is zero before step j
   if (g == 0) {
-    tile_fetch(r1, pre_i ? ws_LS(a, b, j) : Wt(i, j), CB);
+    tile_fetch(r1, Wt(i, j), CB);
     tile_fetch_lower(rD, ws_D(a, b, j), CB);
   }
   // one fetch site per operand, its source chosen by tile kind (one site per kind had the
   // compiler merge the kinds' pending loads and wait for most of group 0's loads before a
   // forward-substitution tile issued its own)
-  const double* src2 = pre_l ? ws_LS(a, b, j) : upd ? Wt(l != i ? l : i, l != i ? j : i) : fwd ? Bt(j, c) : nullptr;
+  const double* src2 = upd ? Wt(l != i ? l : i, l != i ? j : i) : fwd ? Bt(j, c) : nullptr;
   const double* srcu = (upd && l != i) ? Wt(i, l) : fwd ? Bt(i, c) : nullptr;
   if (src2) tile_fetch(r2, src2, CB);
   if (srcu) row_from_global(u, srcu, CB);
@@ -1417,20 +1170,16 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   // block tj takes 4 (tj + 1) k-steps): group 0 blocks 0 and 3, group 1 blocks 1 and 2;
   // each group then forms its tile's own first product
   Blk4 pi = blk4_zero(), t = blk4_zero();
-  if (!pre_i) {   // (uniform per workgroup)
-    if (g == 0) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);  // P_i = W_ij D_j^T = L_ij
-    else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
-  }
+  if (g == 0) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);  // P_i = W_ij D_j^T = L_ij
+  else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
   if (first) {
     if (upd) row_mma<true, 1>(t, sT, sD, 1.0);   // P_l = W_lj D_j^T
     else col_mma_lower(t, sD, sT);               // X_jc = D_j B_jc
   }
   __syncthreads();
   PAIRSTAMP(pst, j, 2);
-  if (!pre_i) {
-    if (g == 0) blk4_to_lds<true, 0x9>(s1, pi);
-    else blk4_to_lds<true, 0x6>(s1, pi);
-  }
+  if (g == 0) blk4_to_lds<true, 0x9>(s1, pi);
+  else blk4_to_lds<true, 0x6>(s1, pi);
   if (first) upd ? blk4_to_lds<true>(sT, t) : blk4_to_lds<false>(sT, t);
   __syncthreads();
   PAIRSTAMP(pst, j, 3);
@@ -1576,9 +1325,9 @@ __global__ __launch_bounds__(256) void chol_bwd_elem_kernel(int mode, const floa
 using namespace mgp;
 
 static int64_t chol_mp(int64_t M) { return (M + CB - 1) / CB * CB; }
-static int64_t chol_ws_doubles_per_batch(int64_t M) {   // W, B [Mp][Mp]; D, LS [nb][64][64]
+static int64_t chol_ws_doubles_per_batch(int64_t M) {
   const int64_t Mp = chol_mp(M);
-  return 2 * Mp * Mp + 2 * (Mp / CB) * CB * CB;
+  return 2 * Mp * Mp + (Mp / CB) * CB * CB;
 }
 
 #ifdef MGP_DBG_STAMPS
