@@ -960,6 +960,9 @@ __global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j
 }
 
 // ------------------------------------------------------------------ Kuf side job
+#ifndef MGP_KUF_SIDE_POLICY
+#define MGP_KUF_SIDE_POLICY 1   // the side job's image stores (kuf_image.hpp img_store): non-temporal
+#endif
 // Kuf image blocks [k0, k1) (batch-major: block b * kblocks + bid is block bid of entry b's
 // image) run by the `nkwg` extra workgroups of a step launch, two blocks per pass (one per
 // 256-thread group).  The step kernel's LDS holds one of its workgroups per CU, so these
@@ -985,8 +988,8 @@ __device__ __forceinline__ void kuf_side_blocks(const CholArgs& a, int w, int64_
     const KufImageArgs ka = {a.kx, a.kldx, ag.Z[b], a.ldz, a.kN, a.M, a.D, ag.var[b], ag.ls[b], ag.n_ls[b],
                              a.knmk, a.krow_blocks, ag.kfr[b], ag.kbound[b]};
     const int64_t bid = item - b * a.kblocks;
-    if (a.kf16) kuf_image_block<DM, true>(ka, bid, t, active, lds);
-    else kuf_image_block<DM, false>(ka, bid, t, active, lds);
+    if (a.kf16) kuf_image_block<DM, true, MGP_KUF_SIDE_POLICY>(ka, bid, t, active, lds);
+    else kuf_image_block<DM, false, MGP_KUF_SIDE_POLICY>(ka, bid, t, active, lds);
   }
 }
 

@@ -44,12 +44,50 @@ constexpr int kuf_block_lds_floats() {
   return 128 * (2 * ((DMAX + 1) / 2 + 1) + 1) + 2 * ((DMAX + 1) / 2);
 }
 
+// Stores of the image fragments (16 B per lane): POL 0 plain, 1 non-temporal (streaming:
+// fewer dirty L2 lines left for the kernel boundary to write back -- the K3 step
+// launches' side job, where every boundary is on the Cholesky chain's critical path).
+template <int POL>
+__device__ __forceinline__ void img_store(bf16x8* p, bf16x8 v) {
+  if constexpr (POL == 0) *p = v;
+  else __builtin_nontemporal_store(v, p);
+}
+
+template <bool F16, int POL>
+__device__ __forceinline__ void store_fragment(bf16x8* __restrict__ dst, const float (&v)[8]) {
+  if constexpr (POL == 0) {
+    if constexpr (F16) store_split_f16(dst, v, 1.f);
+    else store_split(dst, v);
+  } else if constexpr (F16) {   // store_split_f16 (no e4m3 plane) with POL stores
+    halfx8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const _Float16 hi = (_Float16)v[j];
+      h[j] = hi;
+      l[j] = (_Float16)(v[j] - (float)hi);
+    }
+    img_store<POL>(dst, __builtin_bit_cast(bf16x8, h));
+    img_store<POL>(dst + 64, __builtin_bit_cast(bf16x8, l));
+  } else {                      // store_split with POL stores
+    bf16x8 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __bf16 a, b, c;
+      split3(v[j], a, b, c);
+      h[j] = a; m[j] = b; l[j] = c;
+    }
+    img_store<POL>(dst, h);
+    img_store<POL>(dst + 64, m);
+    img_store<POL>(dst + 128, l);
+  }
+}
+
 // One block by the 256 threads of a group (t = thread index within the group).  Every
 // thread of the WORKGROUP must call it the same number of times: it takes three
 // __syncthreads(); a group with nothing to do passes active = false (it joins the
 // barriers, loads and stores nothing).  lds: kuf_block_lds_floats<DMAX>() floats of
 // this group's own.
-template <int DMAX, bool F16>
+template <int DMAX, bool F16, int POL = 0>
 __device__ __forceinline__ void kuf_image_block(const KufImageArgs& a, int64_t bid, int t, bool active,
                                                 float* __restrict__ lds) {
   constexpr int KS = (DMAX + 1) / 2;     // MFMA k-steps over the dims (2 each) ...
@@ -121,10 +159,7 @@ __device__ __forceinline__ void kuf_image_block(const KufImageArgs& a, int64_t b
           if constexpr (RAGGED)
             if (m0 + 32 * i + acc_row(8 * half + j, lane) >= a.M) v[j] = 0.f;
         }
-        if constexpr (F16)
-          store_split_f16(a.Kfr + ((nb * a.nmk + 2 * mb + half) * 3) * 64 + lane, v, 1.f);
-        else
-          store_split(a.Kfr + ((nb * a.nmk + 2 * mb + half) * 3) * 64 + lane, v);
+        store_fragment<F16, POL>(a.Kfr + ((nb * a.nmk + 2 * mb + half) * 3) * 64 + lane, v);
       }
     }
   };

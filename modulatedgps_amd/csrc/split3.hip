@@ -45,6 +45,10 @@
 
 #include "mgp_common.hpp"
 
+#ifndef MGP_K4_STORE_NT
+#define MGP_K4_STORE_NT 1   // K4's A-image stores non-temporal (0: plain, for A/B builds)
+#endif
+
 namespace mgp {
 
 // Debug builds only (-DMGP_DBG_STAMPS, tools/k4_stamps.py): K4 phase times per
@@ -1916,8 +1920,13 @@ __device__ __forceinline__ void trsm_stats16_item(
         const u32x4v fh = u32x4v{h0[0], h0[1], h1[0], h1[1]};
         const u32x4v fl = u32x4v{l0[0], l0[1], l1[0], l1[1]};
         bf16x8* dst = Afr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib0 + d) * 3) * 64 + pos;
+#if MGP_K4_STORE_NT   // streaming stores: fewer dirty L2 lines for the kernel boundary
+        __builtin_nontemporal_store(__builtin_bit_cast(bf16x8, fh), dst);
+        __builtin_nontemporal_store(__builtin_bit_cast(bf16x8, fl), dst + 64);
+#else
         dst[0] = __builtin_bit_cast(bf16x8, fh);
         dst[64] = __builtin_bit_cast(bf16x8, fl);
+#endif
       }
     // q_mu^T A of this row-block pair: B operand slot j = row 4q + j of block ib0 (j < 4),
     // row 4q + j - 4 of block ib0 + 1
