@@ -105,6 +105,8 @@ def main():
                                                                          [var, var], M, N, K, [fm6, fmB], [fv6, fvB],
                                                                          wsx),
         "kuu_chol_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info),
+        "kuu_chol_kuf_x2": lambda: ops.kuu_potrf_trtri([Z, Z], [var, var], [lsc, lsc], 1e-6, LinvT=LinvT, info=info,
+                                                       kuf=(X, [Khr, Khr2], "f16")),
         "kuu_chol_x1": lambda: ops.kuu_potrf_trtri([Z], [var], [lsc], 1e-6, LinvT=LinvT[0:1], info=info[0:1]),
         "rbf_kuf": lambda: ops.rbf_kuf(X, Z, var, lsc, out=Kuf),
         "trsm_stats": lambda: ops.trsm_stats(LinvT[0], Kuf, q_mu, A=A, stats=stats),

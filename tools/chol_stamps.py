@@ -3,7 +3,10 @@ Rebuilds libmgp_hip.so with -DMGP_DBG_STAMPS in this (scratch) tree, runs one
 batched Kuu Cholesky + inverse at M = 1024, batch 2, and prints per-step
 deltas (s_memtime ticks, 100 MHz) of the look-ahead workgroup:
   0 start, 1 tiles loaded, 2 P_i stored, 3 update done, 4 staged, 5 panels
-  factored, 6 inverse done, 7 diag written."""
+  factored, 6 inverse done, 7 diag written.
+--elbo: the stamps of K3 inside bench.py's c3 ELBO step (20 evaluations back to back,
+the last one's K3: it follows the previous evaluation's K5, with the step's side work
+and the K1 side job as in the bench)."""
 import ctypes
 import os
 import sys
@@ -29,7 +32,17 @@ if with_k1:
     ev = torch.cuda.Event()
     ev.record()
     kfr = [ops.rbf_kuf_x6(X, Z, var, ls, fmt="f16") for _ in range(2)]
-for _ in range(3):
+elbo = "--elbo" in sys.argv
+if elbo:
+    import bench
+    cfg = bench.CONFIGS["c3"]
+    M = cfg[1]
+    Xn, Yn, layers = bench.synthetic(cfg, 0, dev)
+    model = bench.build_model(cfg, layers, dev, num_data=cfg[0])
+    Xe, Ye = torch.from_numpy(Xn).to(dev), torch.from_numpy(Yn).to(dev)
+    for _ in range(20):
+        model._build_likelihood(Xe, Ye, n_offset=0, n_total=cfg[0], process_group=None)
+for _ in range(0 if elbo else 3):
     if with_k1:
         torch.cuda.synchronize()
         ops.kuu_potrf_trtri([Z, Z], [var, var], [ls, ls], 1e-6, prep_event=ev)
@@ -60,6 +73,18 @@ for j in range(steps):
     clk = (s[7] - s[0]) / max(1, s[15] - s[14]) / 10.0
     gap = (n[14] - s[15]) * 1e-2 if n and n[14] else float("nan")
     print(f"{j:2d} wall {wall:6.2f} us  clock {clk:5.2f} GHz  gap {gap:6.2f} us")
+# row preparation (batch entry 0), us after the step's look-ahead start: prep kind 0 start,
+# prep kinds 0 / 1 published, the row finish saw both flags (and the S2 phase's start: stamp 11)
+rf = (ctypes.c_ulonglong * (64 * 4))()
+if hasattr(lib, "mgp_dbg_rf_stamps"):
+    lib.mgp_dbg_rf_stamps(rf)
+    print("row preparation (us after the look-ahead's start): prep start, kind 0 done, kind 1 done, finish saw flags")
+    for j in range(steps):
+        t0 = st[j][14]
+        v = [rf[j * 4 + k] for k in range(4)]
+        if t0 and v[1]:
+            print(f"{j:2d} prep {(v[3] - t0) * 1e-2:6.2f}  W' {(v[1] - t0) * 1e-2:6.2f}  F {(v[2] - t0) * 1e-2:6.2f}"
+                  f"  seen {(v[0] - t0) * 1e-2 if v[0] else float('nan'):6.2f}")
 # one pair workgroup per step (first pair of the last tile row, batch 0): shader cycles per phase
 pb = (ctypes.c_ulonglong * (64 * 8))()
 lib.mgp_dbg_pair_stamps(pb)
