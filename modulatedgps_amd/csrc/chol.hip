@@ -61,12 +61,7 @@ __device__ unsigned long long g_pair_stamps[64 * 8];
 // the time at kernel entry (held in a register until the workgroup knows whether it stamps)
 #define ENTRYTIME(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
 #define PAIRSTAMP_AT(on, j, k, t) do { if ((on) && threadIdx.x == 0) g_pair_stamps[(j) * 8 + (k)] = (t); } while (0)
-// row preparation (batch entry 0), 100 MHz clock: [0] row finish saw both flags, [1] / [2] prep
-// kind 0 / 1 published, [3] prep kind 0 started
-__device__ unsigned long long g_rf_stamps[64 * 4];
-#define RFSTAMP(on, j, k) do { if ((on) && (threadIdx.x & 63) == 0) g_rf_stamps[(j) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
-#define RFSTAMP(on, j, k) do {} while (0)
 #define ENTRYTIME(t) do {} while (0)
 #define PAIRSTAMP_AT(on, j, k, t) do {} while (0)
 #define STAMP(j, k) do {} while (0)
@@ -102,18 +97,6 @@ __device__ __forceinline__ double* ws_tile(const CholArgs& a, double* base, int 
 }
 __device__ __forceinline__ double* ws_D(const CholArgs& a, int b, int j) {
   return ws_W(a, b) + 2 * a.Mp * a.Mp + (int64_t)j * CB * CB;
-}
-
-// LS[k] = L_{k+1,k} (float64, 64 x 64, row-major): tile row k + 1's panel tile, formed by the
-// look-ahead workgroup of step launch k - 1 beside its factorisation (row finish, below) and
-// read by launch k's pairs in place of W_{k+1,k} D_k^T (k >= 1)
-__device__ __forceinline__ double* ws_LS(const CholArgs& a, int b, int k) {
-  return ws_W(a, b) + 2 * a.Mp * a.Mp + ((int64_t)a.nb + k) * CB * CB;
-}
-// Hand-off flags of the row preparation: [nb][3] ints per batch entry (launch j, kind),
-// zeroed by chol_prep
-__device__ __forceinline__ int* ws_flags(const CholArgs& a, int b) {
-  return reinterpret_cast<int*>(ws_W(a, b) + 2 * a.Mp * a.Mp + 2 * (int64_t)a.nb * CB * CB);
 }
 
 // Element (gr, gc) of the padded input matrix, in float64.
@@ -481,45 +464,34 @@ __device__ __forceinline__ void blk_store(double* __restrict__ s, const doublex4
   for (int r = 0; r < 4; ++r) s[((lane >> 4) + 4 * r) * LDT + (lane & 15)] = v[r];
 }
 
-// acc -= block (bi, bj) of P P^T (sum over the 64 columns of sP; one wave, accumulator layout);
-// the operands of the next 16 columns read before the current four MFMAs.
-__device__ __forceinline__ void lower_blk_mma(doublex4& acc, const double* __restrict__ sP, int bi, int bj) {
-  const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
-  double av[2][4], bv[2][4];
-  auto load = [&](int buf, int c) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      av[buf][q] = sP[(16 * bi + l16) * LDT + 16 * c + 4 * q + kq];
-      bv[buf][q] = sP[(16 * bj + l16) * LDT + 16 * c + 4 * q + kq];
-    }
-  };
-  load(0, 0);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    if (c + 1 < 4) load((c + 1) & 1, c + 1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[c & 1][q], bv[c & 1][q], acc, 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// Lower 16x16 block n (0 .. 9, row-major over bi >= bj) of a 64x64 tile
-__device__ __forceinline__ void lower_blk_of(int n, int& bi, int& bj) {
-  bi = 0;
-  while ((bi + 1) * (bi + 2) / 2 <= n) ++bi;
-  bj = n - bi * (bi + 1) / 2;
-}
-
 // Lower 16x16 blocks (bi >= bj) of the diagonal tile s -= P P^T, in place in LDS;
 // the 10 blocks dealt 3/3/2/2 over the waves (48 MFMAs at most per wave).
 __device__ __forceinline__ void diag_lower_update(double* __restrict__ s, const double* __restrict__ sP) {
   const int w = ctid() >> 6;
   for (int q = w; q < 10; q += 4) {
-    int bi, bj;
-    lower_blk_of(q, bi, bj);
+    int bi = 0;
+    while ((bi + 1) * (bi + 2) / 2 <= q) ++bi;
+    const int bj = q - bi * (bi + 1) / 2;
     doublex4 acc = blk_load(s + 16 * bi * LDT + 16 * bj);
-    lower_blk_mma(acc, sP, bi, bj);
+    const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
+    // operands of the next four k-steps read before the current four MFMAs
+    double av[2][4], bv[2][4];
+    auto load = [&](int buf, int c) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        av[buf][q] = sP[(16 * bi + l16) * LDT + 16 * c + 4 * q + kq];
+        bv[buf][q] = sP[(16 * bj + l16) * LDT + 16 * c + 4 * q + kq];
+      }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c + 1 < 4) load((c + 1) & 1, c + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[c & 1][q], bv[c & 1][q], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     blk_store(s + 16 * bi * LDT + 16 * bj, acc);
   }
 }
@@ -695,18 +667,11 @@ __device__ __forceinline__ doublex4 neg_x_times(const double* __restrict__ Xii, 
 // Records the first non-positive pivot (LAPACK info, 1-based, + gcol0).
 // sPend (optional, may alias sX): the caller's pending update sF -= sPend sPend^T
 // of the lower blocks right of column block 0 (column block 0 already applied).
-// hook: run by the caller's other waves (active = false) in phase ph = 0 .. 8 of the nine
-// between the barriers (S0 U0 S1 U1 S2 U2 S3 I1 I2 = 0 .. 8), beside the factorisation.
-struct NoHook {
-  __device__ __forceinline__ void operator()(int) const {}
-};
-template <typename Hook = NoHook>
 __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double* sX,
                                                  double* __restrict__ col, int32_t* info, int64_t gcol0,
-                                                 const double* sPend, bool active, Hook& hook) {
-  // active = false: the caller's other waves take part in every barrier and do no work of
-  // the factorisation (w = 4 matches no role; they run `hook`), so the barrier sequence is
-  // the same for all waves
+                                                 const double* sPend = nullptr, bool active = true) {
+  // active = false: the caller's idle waves take part in every barrier and do no work
+  // (w = 4 matches no role), so the barrier sequence is the same for all waves
   const int w = active ? (ctid() >> 6) : 4, lane = ctid() & 63;
   int bad = 0;
   const int js = (int)(gcol0 / CB) - 1;
@@ -717,8 +682,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     const int bi1 = (w == 3) ? 3 : 2, bj1 = (w == 1) ? 1 : (w == 2 ? 2 : 3);
     sub_outer_blk<4>(sF, 16 * bi0, 16 * bj0, sPend, sPend);
     sub_outer_blk<4>(sF, 16 * bi1, 16 * bj1, sPend, sPend);
-  } else if (w == 4) {
-    hook(0);
   }
   STAMP(js, 8);
   __syncthreads();
@@ -730,8 +693,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
       const int i = q < 3 ? 0 : (q < 5 ? 1 : 2), j = q < 3 ? q + 1 : (q < 5 ? q - 1 : 3);
       blk_store(sX + 16 * i * LDT + 16 * j, doublex4{0.0, 0.0, 0.0, 0.0});
     }
-  } else if (w == 4) {
-    hook(1);
   }
   __syncthreads();
   STAMP(js, 9);
@@ -744,24 +705,19 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     sub_outer_blk<1>(sF, 48, 32, P0, P0);
   } else if (w == 3) {
     sub_outer_blk<1>(sF, 48, 48, P0, P0);  // update 0 of (3,3)
-  } else if (w == 4) {
-    hook(2);
   }
   STAMP(js, 10);
   __syncthreads();
   if (w < 2) sub_outer_blk<1>(sF, 32 + 16 * w, 32, sF + 16, sF + 16);  // update 1 of (2,2), (3,2)
-  else if (w == 4) hook(3);
   __syncthreads();
   STAMP(js, 11);
   if (w == 0) panel_factor<2>(sF, col, lane, bad);
   else if (w == 1) inv_diag_block(sF, sX, col, 1, lane);
   else if (w == 2) sub_outer_blk<1>(sF, 48, 48, sF + 16, sF + 16);  // update 1 of (3,3)
-  else if (w == 4) hook(4);
   STAMP(js, 12);
   __syncthreads();
   if (w == 0) panel_update<2>(sF, 0, 1);
   else if (w == 1) inv_offdiag_block(sF, sX, 1, 0, lane);
-  else if (w == 4) hook(5);
   __syncthreads();
   auto L_ = [&](int bi, int bj) { return sF + 16 * bi * LDT + 16 * bj; };
   auto X_ = [&](int bi, int bj) { return sX + 16 * bi * LDT + 16 * bj; };
@@ -790,8 +746,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     doublex4 t = {0.0, 0.0, 0.0, 0.0};
     blk_mma<false>(t, L_(3, 1), X_(1, 1), 1.0);
     blk_store(S_(3, 1), t);
-  } else if (w == 4) {
-    hook(6);
   }
   __syncthreads();
   STAMP(js, 5);
@@ -809,8 +763,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     doublex4 y = blk_load(S_(3, 1));
     blk_mma<false>(y, L_(3, 2), X_(2, 1), 1.0);
     blk_store(S_(3, 1), y);
-  } else if (w == 4) {
-    hook(7);
   }
   __syncthreads();
   STAMP(js, 13);
@@ -827,8 +779,6 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     blk_store(S_(3, 0), zero4);
     blk_mma<false>(y, L_(3, 2), X_(2, 0), 1.0);
     blk_store(X_(3, 0), neg_x_times(X_(3, 3), y, lane));
-  } else if (w == 4) {
-    hook(8);
   }
   __syncthreads();
 }
@@ -931,14 +881,10 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
         if (b == i) lt = a.lt_absmax[i];
       if (lt) *lt = 0.f;
     }
-    int* fl = ws_flags(a, b);   // the row preparation's hand-off flags of this factorisation
-    for (int k = threadIdx.x; k < 3 * a.nb; k += kCholThreads)
-      __hip_atomic_store(fl + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     build_tile(s1, LDT, 0, 0, reinterpret_cast<float*>(s2));
     __syncthreads();
     STAMP(63, 1);
-    NoHook nh;
-    factor_diag_tile(s1, s2, col, a.info + b, 0, nullptr, true, nh);
+    factor_diag_tile(s1, s2, col, a.info + b, 0);
     __syncthreads();
     STAMP(63, 2);
     write_diag(a, b, 0, s1, s2);
@@ -960,294 +906,21 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ row preparation
-// Step launch j factors tile s = j + 1 on the look-ahead workgroup's group 0 (the chain).
-// Tile row r = j + 2 is made ready for launch j + 1 beside it, so that launch j + 1's chain
-// starts factoring at once (no P = W D^T and no P P^T column-block update on it):
-//   three prep workgroups per batch entry, each forming L_{r,j} = W_{r,j} D_j^T:
-//     kinds 0, 1:  W'_{r,s} = W_{r,s} - L_{r,j} L_{s,j}^T, column blocks 0-1 / 2-3
-//                  (L_{s,j} = LS[j]; launch 0 forms it)
-//     kind 2:      F_r = W_{r,r} - L_{r,j} L_{r,j}^T      (the ten lower blocks)
-//   each written in place and published by a flag;
-//   the look-ahead's group 1 beside the factorisation of tile s (RowFinish, its hook):
-//     L_{r,s} = W'_{r,s} L_ss^-T, right-looking by column blocks: with T_q = W'^T[q] (the
-//       transposed column block q), as panel p and X_pp = L_pp^-1 become final
-//       Y_p = L_{r,s}[:, p]^T = X_pp T_p,   T_q -= L_ss[q][p] Y_p   (q > p)
-//     F_r[:, 0] -= sum_p Y_p^T Y_p[:, 0]   (step s's update of tile (r, r), column block 0)
-//   and writes LS[j + 1] = L_{r,s} and F_r's column block 0; launch j + 1's chain then
-//   applies the rest of step s's update (-LS LS^T on the six other lower blocks) beside its
-//   first panel sweep, as launch 0 does with its own P.
-// Only waves 1-3 of group 1 do the row finish: wave 0 of the group shares the panel wave's
-// SIMD, and f64 MFMAs there slow the VALU panel sweep 6x (profiles/r05d_simd_share_probe.log).
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, the first row of the table of
-// sc1 forms): every byte of W'_{r,s} and F_r is stored sc1 by its prep workgroup, every storing
-// wave drains vmcnt(0), the workgroup barrier, then one lane's relaxed agent-scope flag store;
-// each reading wave polls the flags itself (relaxed agent-scope loads, bounded) and loads every
-// one of those bytes with sc1 buffer loads.  Nothing else reads or writes the two tiles in
-// launch j (the pairs of row r take only its other tiles).
-typedef __attribute__((address_space(1))) int gint;
-constexpr int kSc1 = 16;                    // buffer instruction aux bits: sc1
-constexpr uint32_t kSpinLimit = 1u << 22;   // polls (s_sleep 2 each) before a wait gives up
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const double* t) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)t, (short)0, CB * CB * 8, 0x00020000);
-}
-__device__ __forceinline__ double ld8c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kSc1));
-}
-__device__ __forceinline__ void st8c(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double x) {
-  typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, x), r, voff, soff, kSc1);
-}
-// One wave waits until *flag != 0 (relaxed agent-scope loads, bounded); false on a give-up.
-__device__ __forceinline__ bool wait_flag(const int* flag) {
-  for (uint32_t it = 0; it < kSpinLimit; ++it) {
-    const int v = __hip_atomic_load((gint*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__builtin_amdgcn_readfirstlane(v) != 0) return true;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return false;
-}
-template <int BLK>
-__device__ __forceinline__ void row_from_global_blk(Blk4& r, const double* __restrict__ g, int64_t ld) {
-  auto get = [&](int t, int q, int row, int col) { r.c[t][q] = g[(int64_t)row * ld + col]; };
-  blk4_foreach<true, decltype(get), BLK>(get);
-}
-
-// Prep workgroup of `kind` for step launch j and batch entry b (512 threads, groups g = 0, 1).
-constexpr int kPrepKinds = 3;
-__device__ __forceinline__ void row_prep_wg(const CholArgs& a, int b, int j, int kind, double* s1, double* sD,
-                                            double* sT) {
-  const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
-  const int s = j + 1, r = j + 2;
-  double* W = ws_W(a, b);
-  auto Wt = [&](int bi, int bl) { return ws_tile(a, W, bi, bl); };
-  const bool wk = kind < 2;                 // a W'_{r,s} half (else F_r)
-  const bool form_ls = j == 0 && wk;        // launch 0: L_{1,0} = W_{1,0} D_0^T here (no LS[0])
-  double* out = wk ? Wt(r, s) : Wt(r, r);
-  const int tb = 2 * kind + g;              // W' halves: this group's column block
-  RFSTAMP(b == 0 && kind == 0 && threadIdx.x == 0, j, 3);
-  TileRegs r1, rT;
-  Blk4 u = blk4_zero();
-  if (g == 0) {
-    tile_fetch(r1, Wt(r, j), CB);
-    tile_fetch_lower(rT, ws_D(a, b, j), CB);
-  } else {
-    tile_fetch(rT, wk ? (form_ls ? Wt(s, j) : ws_LS(a, b, j)) : Wt(r, r), CB);
-  }
-  if (wk) {   // W_{r,s}: row stripe w, column block tb
-    if (tb == 0) row_from_global_blk<0x1>(u, out, CB);
-    else if (tb == 1) row_from_global_blk<0x2>(u, out, CB);
-    else if (tb == 2) row_from_global_blk<0x4>(u, out, CB);
-    else row_from_global_blk<0x8>(u, out, CB);
-  }
-  if (g == 0) {
-    tile_put(s1, r1);
-    tile_put(sD, rT);
-  } else {
-    tile_put(sT, rT);
-  }
-  __syncthreads();
-  // L_{r,j} = W_{r,j} D_j^T (column blocks 0, 3 on group 0 and 1, 2 on group 1, as the pairs' P_i)
-  Blk4 pi = blk4_zero(), pl = blk4_zero();
-  if (g == 0) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);
-  else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
-  if (form_ls) {
-    if (g == 0) row_mma<true, 1, 0x9>(pl, sT, sD, 1.0);
-    else row_mma<true, 1, 0x6>(pl, sT, sD, 1.0);
-  }
-  __syncthreads();
-  if (g == 0) blk4_to_lds<true, 0x9>(s1, pi);
-  else blk4_to_lds<true, 0x6>(s1, pi);
-  if (form_ls) {
-    if (g == 0) blk4_to_lds<true, 0x9>(sT, pl);
-    else blk4_to_lds<true, 0x6>(sT, pl);
-  }
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t R = tile_rsrc(out);
-  const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
-  if (wk) {
-    // W'_{r,s} = W_{r,s} - L_{r,j} L_{s,j}^T: row stripe w, column block tb
-    if (tb == 0) row_mma<true, 0, 0x1>(u, s1, sT, -1.0);
-    else if (tb == 1) row_mma<true, 0, 0x2>(u, s1, sT, -1.0);
-    else if (tb == 2) row_mma<true, 0, 0x4>(u, s1, sT, -1.0);
-    else row_mma<true, 0, 0x8>(u, s1, sT, -1.0);
-    const int w = ctid() >> 6;
-    const uint32_t voff = (uint32_t)(((16 * w + kq) * CB + l16) * 8);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (t == tb)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) st8c(R, voff, (uint32_t)((4 * q * CB + 16 * t) * 8), u.c[t][q]);
-  } else {
-    // F_r = W_{r,r} - L_{r,j} L_{r,j}^T, lower blocks w8 and w8 + 8 (w8 = the wave, 0 .. 7)
-    const int w8 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t voff = (uint32_t)((kq * CB + l16) * 8);
-    for (int n = w8; n < 10; n += 8) {
-      int bi, bj;
-      lower_blk_of(n, bi, bj);
-      doublex4 acc = blk_load(sT + 16 * bi * LDT + 16 * bj);
-      lower_blk_mma(acc, s1, bi, bj);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) st8c(R, voff, (uint32_t)(((16 * bi + 4 * rr) * CB + 16 * bj) * 8), acc[rr]);
-    }
-  }
-  // publish: every storing wave drains its sc1 stores, the barrier, then one lane's flag store
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store((gint*)(ws_flags(a, b) + kPrepKinds * j + kind), 1, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  RFSTAMP(b == 0 && kind != 1 && threadIdx.x == 0, j, 1 + kind / 2);
-}
-
-// The row finish of step launch j (factor_diag_tile's hook on the look-ahead's group 1).
-// Waves vw = 0 .. 2 (waves 1 .. 3 of the group; vw = -1: wave 0, idle) own the 16-column
-// stripes v of Y (vw 0: stripes 0 and 3, vw 1: 1, vw 2: 2); a stripe's chain T_q -> Y_q only
-// reads its own stripe, so it stays in registers (accumulator layout = the next product's B
-// operand).  Each Y_q goes to LDS (ys) for F's update and to LS[j + 1] from the registers.
-// F_r's column-block-0 blocks (1,0)..: vw 1 blocks (0,0), (1,0), vw 2 (2,0), (3,0).  Phases:
-//   S2 (4): wait for the three prep flags, sc1-load W'^T and F's blocks; Y_0 (X_00 final
-//           after S1), T_q -= L_ss[q][0] Y_0
-//   S3 (6): Y_1 (X_11 after S2), T_q -= L_ss[q][1] Y_1; F[:, 0] -= Y_0^T Y_0[:, 0]
-//   I1 (7): Y_2 (X_22 after S3), T_3 -= L_ss[3][2] Y_2;  F[:, 0] -= Y_1^T Y_1[:, 0]
-//   I2 (8): Y_3 (X_33 after I1);                        F[:, 0] -= Y_2^T Y_2[:, 0]
-//   write (9): F[:, 0] -= Y_3^T Y_3[:, 0] and its stores
-struct RowFinish {
-  const double* sF;    // the tile being factored (group 0): L_ss as the panels complete
-  const double* sX;    // its inverse: X_qq as the diagonal blocks complete
-  double* ys;          // Y = L_{r,s}^T, strip q = rows 16 q .. 16 q + 15 (LDS, leading dimension LDT)
-  const double* Wrs;   // W'_{r,s} (kinds 0, 1)
-  double* Wrr;         // F_r (kind 2; column block 0 then this finish's)
-  double* LSout;       // LS[j + 1]
-  const int* flags;    // this launch's three flags
-  int32_t* info;
-  int j;
-  bool stamp;          // debug stamps (batch entry 0)
-  bool on;             // group 1 of a look-ahead whose launch prepares a row
-  int vw;
-  doublex4 wt[2][4];   // T_q of the owned stripes (W'^T[q][v] at the start)
-  doublex4 f[2];       // owned column-block-0 blocks of F_r
-
-  __device__ __forceinline__ int nst() const { return vw == 0 ? 2 : 1; }
-  __device__ __forceinline__ int stripe(int si) const { return si == 0 ? vw : 3; }
-  __device__ __forceinline__ bool has_f() const { return vw > 0; }
-  __device__ __forceinline__ int fbi(int m) const { return 2 * (vw - 1) + m; }   // block (fbi, 0)
-
-  __device__ __forceinline__ void acquire() {
-    const bool ok = wait_flag(flags) && wait_flag(flags + 1) && wait_flag(flags + 2);
-    RFSTAMP(stamp && vw == 0, j, 0);
-    if (!ok && (ctid() & 63) == 0) atomicCAS(info, 0, -1);   // hand-off lost: reported, never silent
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
-    const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
-    const __amdgpu_buffer_rsrc_t RW = tile_rsrc(Wrs), RF = tile_rsrc(Wrr);
-    const uint32_t vo_w = (uint32_t)((l16 * CB + kq) * 8), vo_f = (uint32_t)((kq * CB + l16) * 8);
-#pragma unroll
-    for (int si = 0; si < 2; ++si)
-      if (si < nst()) {
-        const int v = stripe(si);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) wt[si][q][rr] = ld8c(RW, vo_w, (uint32_t)((16 * v * CB + 16 * q + 4 * rr) * 8));
-      }
-    if (has_f()) {
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) f[m][rr] = ld8c(RF, vo_f, (uint32_t)(((16 * fbi(m) + 4 * rr) * CB) * 8));
-    }
-  }
-  // Y_p = X_pp T_p for owned stripe SI (to LDS strip p and LS[j + 1]), then T_q -= L_ss[q][p] Y_p
-  template <int p, int SI>
-  __device__ __forceinline__ void step_Y() {
-    const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4, v = stripe(SI);
-    double xv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) xv[k] = sX[(16 * p + l16) * LDT + 16 * p + 4 * k + kq];
-    double av[4][4];   // L_ss[q][p] for q = p + 1 .. 3, read before the first MFMA
-#pragma unroll
-    for (int q = p + 1; q < 4; ++q)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) av[q][k] = sF[(16 * q + l16) * LDT + 16 * p + 4 * k + kq];
-    doublex4 y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) y = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[k], wt[SI][p][k], y, 0, 0, 0);
-#pragma unroll
-    for (int q = p + 1; q < 4; ++q)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) wt[SI][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[q][k], y[k], wt[SI][q], 0, 0, 0);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      ys[(16 * p + kq + 4 * rr) * LDT + 16 * v + l16] = y[rr];
-      LSout[(16 * v + l16) * CB + 16 * p + kq + 4 * rr] = y[rr];   // LS[j + 1] = Y^T
-    }
-  }
-  template <int p>
-  __device__ __forceinline__ void step_Yp() {
-    step_Y<p, 0>();
-    if (nst() > 1) step_Y<p, 1>();
-  }
-  // F[:, 0] -= Y_p^T Y_p[:, 0] on the owned blocks (strip p complete: after a barrier)
-  template <int p>
-  __device__ __forceinline__ void upd_F() {
-    if (!has_f()) return;
-    const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
-    double bv[4], av[2][4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bv[k] = ys[(16 * p + 4 * k + kq) * LDT + l16];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) av[m][k] = ys[(16 * p + 4 * k + kq) * LDT + 16 * fbi(m) + l16];
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) f[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[m][k], bv[k], f[m], 0, 0, 0);
-  }
-  __device__ __forceinline__ void store_F() {
-    if (!has_f()) return;
-    const int lane = ctid() & 63, l16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) Wrr[(16 * fbi(m) + kq + 4 * rr) * CB + l16] = f[m][rr];
-  }
-  __device__ __forceinline__ void operator()(int ph) {
-    if (!on || vw < 0) return;
-    switch (ph) {
-      case 4: acquire(); step_Yp<0>(); break;
-      case 6: step_Yp<1>(); upd_F<0>(); break;
-      case 7: step_Yp<2>(); upd_F<1>(); break;
-      case 8: step_Yp<3>(); upd_F<2>(); break;
-      case 9: upd_F<3>(); store_F(); break;
-      default: break;
-    }
-  }
-};
-
 // ------------------------------------------------------------------ step launch j
-// The look-ahead's factorisation of tile (j+1, j+1), group 0 (active): s1 holds P = L_{j+1,j}
-// and s2 the tile with -P P^T still to apply -- in launch 0 (pend) all of it, whose column
-// block 0 is applied first; from launch 1 on the six blocks right of column block 0 only (P =
-// LS[j], column block 0 applied by the previous launch's row finish).  The six blocks are
-// applied beside the first panel sweep.  Group 1 runs `hook` (the row finish) beside it.
-template <typename Hook>
+// The look-ahead's factorisation of tile (j+1, j+1): s1 holds P = L_{j+1,j}, s2 the
+// tile with column block 0 of -P P^T still to apply.
 __device__ __forceinline__ void lookahead_factor(const CholArgs& a, int b, int j, double* s1, double* s2,
-                                                 double* col, bool active, bool pend, Hook& hook) {
-  if (pend) {
-    // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
-    // lower blocks are applied beside the first panel sweep
-    if (active) sub_outer_blk<4>(s2, 16 * (ctid() >> 6), 0, s1, s1);
-    __syncthreads();
-  }
+                                                 double* col, bool active) {
+  // column block 0 of W_ii -= P_i P_i^T (one block per wave); the other six
+  // lower blocks are applied beside the first panel sweep
+  if (active) sub_outer_blk<4>(s2, 16 * (ctid() >> 6), 0, s1, s1);
+  __syncthreads();
   STAMP(j, 3);
   STAMP(j, 4);
-  factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1, active, hook);
+  factor_diag_tile(s2, s1, col, a.info + b, (int64_t)(j + 1) * CB, s1, active);
   STAMP(j, 6);
   __syncthreads();
   if (active) write_diag(a, b, j + 1, s2, s1);
-  else hook(9);
   __syncthreads();
   STAMP(j, 7);
   RSTAMP(j, 15);
@@ -1354,38 +1027,28 @@ __device__ __forceinline__ void kuf_side_job(const CholArgs& a, int w, int64_t k
 // workgroup) on every row whose tile count is even, instead of each holding a heavy tile's
 // workgroup to the heavy tile's length with one group idle.
 constexpr int kPairThreads = 2 * kCholThreads;
-// Rows j + 1 and j + 2 have no trailing-update tiles in launch j: tile (j+1, j+1) is the
-// look-ahead's, tiles (j+2, j+1) and (j+2, j+2) the prep workgroups' (row preparation).
-__host__ __device__ inline int step_row_tiles(int i, int j) { return i <= j + 2 ? j + 1 : i + 1; }
-__host__ __device__ inline int step_prep_wgs(int nb, int j) { return j + 2 < nb ? 3 : 0; }  // per batch entry
+__host__ __device__ inline int step_row_tiles(int i, int j) { return i == j + 1 ? j + 1 : i + 1; }
 __host__ __device__ inline int step_row_pairs(int i, int j) { return (step_row_tiles(i, j) + 1) / 2; }
 __host__ __device__ inline int step_pair_count(int nb, int j) {  // per batch entry
   int n = 0;
   for (int i = j + 1; i < nb; ++i) n += step_row_pairs(i, j);
   return n;
 }
-// Workgroups of a step launch (one dimension, batch (1 + step_prep_wgs + step_pair_count) of
-// them): the batch's look-ahead workgroups first (workgroup b: batch entry b), then the prep
-// workgroups (batch entry p / 2, kind p % 2), then one per pair.
+// Workgroups of a step launch (one dimension, batch (1 + step_pair_count) of them): the
+// batch's look-ahead workgroups first (workgroup b: batch entry b), then one per pair.
 // The pairs, in the order (batch entry, tile row, pair), are cut into 8 consecutive runs,
 // and run x goes to the workgroups w with (w - batch) % 8 == x, which share an XCD under
 // the round-robin placement (speed only, nothing depends on it): a row's pairs then load
 // its panel tile W_ij into one L2 and a run's rows (of one batch entry where the run
 // does not straddle two) share the panel tiles W_lj, B_jc there.  No idle workgroups.
-// Workgroups past batch (1 + step_prep_wgs + Pb) (when the launch carries a Kuf side job):
-// kuf_side_job over the image blocks [k0, k1), nkwg of them.
+// Workgroups past batch (1 + Pb) (when the launch carries a Kuf side job): kuf_side_job
+// over the image blocks [k0, k1), nkwg of them.
 __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb, int64_t k0,
                                                                int64_t k1, int nkwg) {
   __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB];
-  const int nlead = batch * (1 + step_prep_wgs(a.nb, j));   // look-ahead + prep workgroups
-  if ((int)blockIdx.x >= nlead + batch * Pb) {   // uniform per workgroup
-    kuf_side_job(a, (int)blockIdx.x - nlead - batch * Pb, k0, k1, nkwg, reinterpret_cast<float*>(s1),
+  if ((int)blockIdx.x >= batch * (1 + Pb)) {   // uniform per workgroup
+    kuf_side_job(a, (int)blockIdx.x - batch * (1 + Pb), k0, k1, nkwg, reinterpret_cast<float*>(s1),
                  reinterpret_cast<float*>(sD));
-    return;
-  }
-  if ((int)blockIdx.x >= batch && (int)blockIdx.x < nlead) {
-    const int p = (int)blockIdx.x - batch;
-    row_prep_wg(a, p / kPrepKinds, j, p % kPrepKinds, s1, sD, s2[0]);
     return;
   }
   ENTRYTIME(t_entry);
@@ -1403,8 +1066,8 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   if (wg >= batch) {
     // Pb = step_pair_count(nb, j) from the host; position k in the pair order: run x
     // starts after the runs y < x, (P - y + 7) / 8 pairs each (m + 1 for y < P % 8, else m)
-    const int P = batch * Pb, m = P >> 3, x = (wg - nlead) & 7;
-    int k = ((wg - nlead) >> 3) + x * m + min(x, P & 7);
+    const int P = batch * Pb, m = P >> 3, x = (wg - batch) & 7;
+    int k = ((wg - batch) >> 3) + x * m + min(x, P & 7);
     b = k / Pb;
     k -= b * Pb;
     for (;; ++i) {
@@ -1430,62 +1093,37 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     if (lt_max) wave_absmax_atomic(m, lt_max);
   };
   if (wg < batch) {
-    // look-ahead: tile s = j + 1 on group 0 (the chain), the row finish of row j + 2 on waves
-    // 1-3 of group 1 (RowFinish), every barrier taken by both groups.  Launch 0: both groups
-    // load and form P = W_{1,0} D_0^T (group 0 column blocks 0 and 3, group 1 blocks 1 and
-    // 2: equal MFMA counts, as the pairs' P_i) and the chain applies it; from launch 1 on the
-    // tile arrives updated through step j (the previous launch's row preparation).
+    // look-ahead: tile (j+1, j+1).  Both groups load and form P = W_{j+1,j} D_j^T (group 0
+    // column blocks 0 and 3, group 1 blocks 1 and 2: equal MFMA counts, as the pairs'
+    // P_i); the factorisation then runs on group 0 while group 1's waves take part in
+    // every barrier and do no work (uniform barrier sequence)
     const bool act = g == 0;
-    const bool deep = j >= 1;
-    const int r = j + 2;
-    RowFinish rf;
-    rf.on = !act && r < a.nb;
-    rf.vw = __builtin_amdgcn_readfirstlane((int)(ctid() >> 6)) - 1;
-    rf.sF = s2[0];
-    rf.sX = s1;
-    rf.ys = s2[1];
-    rf.Wrs = rf.on ? Wt(r, j + 1) : nullptr;
-    rf.Wrr = rf.on ? Wt(r, r) : nullptr;
-    rf.LSout = rf.on ? ws_LS(a, b, j + 1) : nullptr;
-    rf.flags = ws_flags(a, b) + kPrepKinds * j;
-    rf.info = a.info + b;
-    rf.j = j;
-    rf.stamp = b == 0;
     RSTAMP(j, 14);
     STAMP(j, 0);
-    if (deep) {   // F (group 0) and P = LS[j] (group 1)
-      TileRegs rF;
-      tile_fetch(rF, act ? Wt(i, i) : ws_LS(a, b, j), CB);
-      tile_put(act ? s2[0] : s1, rF);
-      __syncthreads();
-      STAMP(j, 1);
-      STAMP(j, 2);
+    TileRegs r1, rD, r2;
+    if (act) {
+      tile_fetch(r1, Wt(i, j), CB);
+      tile_fetch_lower(rD, ws_D(a, b, j), CB);
     } else {
-      TileRegs r1, rD, r2;
-      if (act) {
-        tile_fetch(r1, Wt(i, j), CB);
-        tile_fetch_lower(rD, ws_D(a, b, j), CB);
-      } else {
-        tile_fetch(r2, Wt(i, i), CB);
-      }
-      if (act) {
-        tile_put(s1, r1);
-        tile_put(sD, rD);
-      } else {
-        tile_put(s2[0], r2);
-      }
-      __syncthreads();
-      STAMP(j, 1);
-      Blk4 pi = blk4_zero();
-      if (act) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);
-      else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
-      __syncthreads();
-      if (act) blk4_to_lds<true, 0x9>(s1, pi);
-      else blk4_to_lds<true, 0x6>(s1, pi);
-      __syncthreads();
-      STAMP(j, 2);
+      tile_fetch(r2, Wt(i, i), CB);
     }
-    lookahead_factor(a, b, j, s1, s2[0], col, act, !deep, rf);
+    if (act) {
+      tile_put(s1, r1);
+      tile_put(sD, rD);
+    } else {
+      tile_put(s2[0], r2);
+    }
+    __syncthreads();
+    STAMP(j, 1);
+    Blk4 pi = blk4_zero();
+    if (act) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);
+    else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
+    __syncthreads();
+    if (act) blk4_to_lds<true, 0x9>(s1, pi);
+    else blk4_to_lds<true, 0x6>(s1, pi);
+    __syncthreads();
+    STAMP(j, 2);
+    lookahead_factor(a, b, j, s1, s2[0], col, act);
     return;
   }
   // pair q of row i: tiles e = 2 q, 2 q + 1 of the row
@@ -1495,32 +1133,27 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   const bool pst = i == a.nb - 1 && q == 0 && b == 0;   // debug stamps only
   PAIRSTAMP_AT(pst, j, 7, t_entry);
   PAIRSTAMP(pst, j, 0);
-  const bool lead = i <= j + 2;                    // rows without trailing-update tiles
-  const int nh = lead ? 0 : i - j - 1;             // off-diagonal update tiles of the row
+  const int nh = (i == j + 1) ? 0 : i - j - 1;  // off-diagonal update tiles of the row
   int l = -1, c = -1;                              // update tile (i, l) or B tile (i, c)
   if (e < nh) l = j + 1 + e;
   else if (e < nh + j) c = e - nh;
-  else if (!lead && e == nh + j) l = i;
+  else if (i > j + 1 && e == nh + j) l = i;
   else c = j;
   const bool upd = has && l >= 0;
   const bool fwd = has && c >= 0 && c < j;  // forward-substitution tile reading B_jc
-  // from launch 1 on, P of row j + 1 is LS[j] (the previous look-ahead's row finish): row
-  // j + 1's P_i and an update tile's P_l with l = j + 1 are loaded, not formed
-  const bool pre_i = j >= 1 && i == j + 1;
-  const bool pre_l = j >= 1 && upd && l == j + 1;
-  const bool first = (upd && l != i && !pre_l) || fwd;  // P_l / X_jc before the update
+  const bool first = (upd && l != i) || fwd;  // P_l / X_jc before the update
   double* sT = s2[g];
   // this tile's operands: sT's tile (when it reads one) and the updated tile (u)
   TileRegs r1, rD, r2;
   Blk4 u = blk4_zero();  // B_ij is zero before step j
   if (g == 0) {
-    tile_fetch(r1, pre_i ? ws_LS(a, b, j) : Wt(i, j), CB);
+    tile_fetch(r1, Wt(i, j), CB);
     tile_fetch_lower(rD, ws_D(a, b, j), CB);
   }
   // one fetch site per operand, its source chosen by tile kind (one site per kind had the
   // compiler merge the kinds' pending loads and wait for most of group 0's loads before a
   // forward-substitution tile issued its own)
-  const double* src2 = pre_l ? ws_LS(a, b, j) : upd ? Wt(l != i ? l : i, l != i ? j : i) : fwd ? Bt(j, c) : nullptr;
+  const double* src2 = upd ? Wt(l != i ? l : i, l != i ? j : i) : fwd ? Bt(j, c) : nullptr;
   const double* srcu = (upd && l != i) ? Wt(i, l) : fwd ? Bt(i, c) : nullptr;
   if (src2) tile_fetch(r2, src2, CB);
   if (srcu) row_from_global(u, srcu, CB);
@@ -1540,20 +1173,16 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   // block tj takes 4 (tj + 1) k-steps): group 0 blocks 0 and 3, group 1 blocks 1 and 2;
   // each group then forms its tile's own first product
   Blk4 pi = blk4_zero(), t = blk4_zero();
-  if (!pre_i) {   // (uniform per workgroup)
-    if (g == 0) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);  // P_i = W_ij D_j^T = L_ij
-    else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
-  }
+  if (g == 0) row_mma<true, 1, 0x9>(pi, s1, sD, 1.0);  // P_i = W_ij D_j^T = L_ij
+  else row_mma<true, 1, 0x6>(pi, s1, sD, 1.0);
   if (first) {
     if (upd) row_mma<true, 1>(t, sT, sD, 1.0);   // P_l = W_lj D_j^T
     else col_mma_lower(t, sD, sT);               // X_jc = D_j B_jc
   }
   __syncthreads();
   PAIRSTAMP(pst, j, 2);
-  if (!pre_i) {
-    if (g == 0) blk4_to_lds<true, 0x9>(s1, pi);
-    else blk4_to_lds<true, 0x6>(s1, pi);
-  }
+  if (g == 0) blk4_to_lds<true, 0x9>(s1, pi);
+  else blk4_to_lds<true, 0x6>(s1, pi);
   if (first) upd ? blk4_to_lds<true>(sT, t) : blk4_to_lds<false>(sT, t);
   __syncthreads();
   PAIRSTAMP(pst, j, 3);
@@ -1699,9 +1328,9 @@ __global__ __launch_bounds__(256) void chol_bwd_elem_kernel(int mode, const floa
 using namespace mgp;
 
 static int64_t chol_mp(int64_t M) { return (M + CB - 1) / CB * CB; }
-static int64_t chol_ws_doubles_per_batch(int64_t M) {   // W, B [Mp][Mp]; D, LS [nb][64][64]; flags [nb][3] ints
-  const int64_t Mp = chol_mp(M), nb = Mp / CB;
-  return 2 * Mp * Mp + 2 * nb * CB * CB + (3 * nb + 3) / 4 * 2;
+static int64_t chol_ws_doubles_per_batch(int64_t M) {
+  const int64_t Mp = chol_mp(M);
+  return 2 * Mp * Mp + (Mp / CB) * CB * CB;
 }
 
 #ifdef MGP_DBG_STAMPS
@@ -1710,9 +1339,6 @@ extern "C" int mgp_dbg_chol_stamps(unsigned long long* host) {
 }
 extern "C" int mgp_dbg_pair_stamps(unsigned long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_stamps), sizeof(g_pair_stamps));
-}
-extern "C" int mgp_dbg_rf_stamps(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rf_stamps), sizeof(g_rf_stamps));
 }
 #endif
 
@@ -1743,7 +1369,7 @@ static void kuf_side_split(int nb, int batch, int64_t total, std::vector<int64_t
   std::vector<double> idle(steps);
   double sum = 0.0;
   for (int j = 0; j < steps; ++j) {
-    idle[j] = std::max<double>(cus - batch * (1 + step_prep_wgs(nb, j) + step_pair_count(nb, j)), cus / 8.0);
+    idle[j] = std::max<double>(cus - batch * (1 + step_pair_count(nb, j)), cus / 8.0);
     sum += idle[j];
   }
   beg.assign(steps + 1, 0);
@@ -1805,8 +1431,7 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
       const int Pb = step_pair_count(a.nb, j);
       const bool side = !kbeg.empty() && knwg[j] > 0;
       const int nkwg = side ? knwg[j] : 0;
-      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + step_prep_wgs(a.nb, j) + Pb) + nkwg), dim3(kPairThreads), 0,
-                         s, a, j, batch, Pb,
+      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb) + nkwg), dim3(kPairThreads), 0, s, a, j, batch, Pb,
                          side ? kbeg[j] : (int64_t)0, side ? kbeg[j + 1] : (int64_t)0, nkwg);
     } else {
       hipLaunchKernelGGL(chol_last_step, dim3(a.nb, batch), block, 0, s, a, j);

@@ -33,7 +33,7 @@ def test_status_strings_and_argument_checks():
     assert lib.mgp_rbf_kuf(None, 1, None, 1, 10, 10, 1, None, None, 1, None, 12, None) == -1
     assert lib.mgp_trsm_stats(None, 0, None, 0, 4, 4, None, 0, 1, None, 0, None, 0, None) == -1
     # per matrix float64 W, B [Mp][Mp] + D [nb][64][64]
-    assert lib.mgp_chol_workspace_bytes(1024, 2) == 2 * (2 * 1024 * 1024 + 2 * 16 * 64 * 64 + 24) * 8
+    assert lib.mgp_chol_workspace_bytes(1024, 2) == 2 * (2 * 1024 * 1024 + 16 * 64 * 64) * 8
     assert lib.mgp_stats_tiles(1024) in (8, 16)   # 128- or 64-row tiles
 
 
