@@ -285,6 +285,46 @@ __device__ void rl_mode(double* sF, double* col, int r, int& bad) {
   for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
 }
 
+// V11: DPP broadcasts.  Every lane keeps, beside its own row a[], a copy d[] of row (lane & 15)
+// of the panel's diagonal block; the column values a row needs come from the copy in its own
+// 16-lane row by v_mov_b64_dpp row_newbcast (one op per value instead of two readlanes), and
+// the copy gets the same update (one more FMA per value).
+template <int S>
+__device__ __forceinline__ double bcast16(double x) {
+  return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + S, 0xF, 0xF, false);
+}
+template <int C, int S>
+__device__ __forceinline__ void dpp_upd(double (&a)[16], double (&d)[16], double t, double td) {
+  if constexpr (S < 16) {
+    const double v = bcast16<S>(d[C]);
+    a[S] = fma(-t, v, a[S]);
+    d[S] = fma(-td, v, d[S]);
+    dpp_upd<C, S + 1>(a, d, t, td);
+  }
+}
+template <int C>
+__device__ __forceinline__ void dpp_col(double (&a)[16], double (&d)[16], double (&rs)[16]) {
+  if constexpr (C < 16) {
+    const double piv = bcast16<C>(d[C]);
+    rs[C] = rsqrt_f64(piv);
+    const double rs2 = rs[C] * rs[C];
+    const double t = a[C] * rs2, td = d[C] * rs2;
+    dpp_upd<C, C + 1>(a, d, t, td);
+    dpp_col<C + 1>(a, d, rs);
+  }
+}
+__device__ void dpp_sweep(double* sF, double* col, int r, int& bad) {
+  double a[16], d[16], rs[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    a[j] = sF[r * LDT + j];
+    d[j] = sF[(r & 15) * LDT + j];
+  }
+  dpp_col<0>(a, d, rs);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+}
+
 __global__ void run(const double* src, double* dst, unsigned long long* t, int variant) {
   __shared__ double sF[CB * LDT], col[3 * CB];
   const int r = threadIdx.x;
@@ -301,6 +341,8 @@ __global__ void run(const double* src, double* dst, unsigned long long* t, int v
   else if (variant == 6) rl_pipe<false>(sF, col, r, bad);
   else if (variant == 7) rs1<false>(sF, col, r, bad);
   else if (variant == 8) rl_mode<0>(sF, col, r, bad);
+  else if (variant == 11) dpp_sweep(sF, col, r, bad);
+  else if (variant == 12) panel_factor<0>(sF, col, r, bad);
   else if (variant == 9) rl_mode<1>(sF, col, r, bad);
   else rl_mode<2>(sF, col, r, bad);
   unsigned long long t1 = stamp();
@@ -321,14 +363,14 @@ int main() {
   (void)hipMalloc(&t, 16 * sizeof(unsigned long long));
   (void)hipMemcpy(src, h, sizeof(h), hipMemcpyHostToDevice);
   unsigned long long ht[16] = {0};
-  const char* names[11] = {"panel_factor (LDS broadcast, rcp chain)", "readlane sweep (kernel)", "chain only",
-                          "trailing updates only", "readlane + rcp chain", "pipelined, pinned", "pipelined", "rsq1 chain", "readlane, rsq f64 + 1 Newton", "readlane, rsq f32 + 2 Newton", "readlane, rsq f32 + 1 Newton"};
+  const char* names[13] = {"panel_factor (LDS broadcast, rcp chain)", "readlane sweep (kernel)", "chain only",
+                          "trailing updates only", "readlane + rcp chain", "pipelined, pinned", "pipelined", "rsq1 chain", "readlane, rsq f64 + 1 Newton", "readlane, rsq f32 + 2 Newton", "readlane, rsq f32 + 1 Newton", "DPP row_newbcast + row copies", "panel_factor<0> (kernel)"};
   for (int rep = 0; rep < 3; ++rep)
-    for (int v = 0; v < 11; ++v) hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
+    for (int v = 0; v < 13; ++v) hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
   (void)hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
   // agreement of the variants' L panels
   double ref[64 * 64], out[64 * 64];
-  for (int v = 0; v < 11; ++v) {
+  for (int v = 0; v < 13; ++v) {
     if (v == 2 || v == 3) continue;
     hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
     (void)hipMemcpy(v == 0 ? ref : out, dst, sizeof(ref), hipMemcpyDeviceToHost);
@@ -337,6 +379,6 @@ int main() {
     for (int i = 0; i < 64; ++i) for (int j = 0; j < 16; ++j) e = fmax(e, fabs(out[i * 64 + j] - ref[i * 64 + j]));
     printf("variant %d max |diff| vs 0: %.3e\n", v, e);
   }
-  for (int v = 0; v < 11; ++v) printf("%-42s %6llu cycles (%.0f per column)\n", names[v], ht[v], ht[v] / 16.0);
+  for (int v = 0; v < 13; ++v) printf("%-42s %6llu cycles (%.0f per column)\n", names[v], ht[v], ht[v] / 16.0);
   return 0;
 }
