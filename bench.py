@@ -422,7 +422,7 @@ def main():
     chol_flops = 2 * (2.0 * M ** 3 / 3.0)        # potrf + trtri, both layers (one batched sweep)
     kernels = {}
     from modulatedgps_amd.config import step_schedule
-    if "rbf_kuf" in st or (x6 and step_schedule() in ("k1_in_k3", "k1_in_k3_qside")):
+    if "rbf_kuf" in st or (x6 and step_schedule() == "k1_in_k3"):
         ms = probe_kuf(model, X, x6, fmt="f16" if f16 else "x6")
         kernels["rbf_kuf"] = {"bound": "hbm", "avg_us": ms * 1e3, "bytes": kuf_bytes,
                               "achieved": kuf_bytes / (ms * 1e-3) / 1e9, "unit": "GB/s",
@@ -449,10 +449,6 @@ def main():
         kernels["kuu_chol"] = {"bound": "latency", "avg_us": ms * 1e3, "flops": chol_flops,
                                "achieved": chol_flops / (ms * 1e-3) / 1e12, "unit": "TFLOP/s",
                                "peak": PEAK_F64 / 1e12, "frac": chol_flops / (ms * 1e-3) / PEAK_F64}
-        if x6 and step_schedule() in ("k1_in_k3", "k1_in_k3_qside"):
-            q = f16 and step_schedule() == "k1_in_k3"
-            kernels["kuu_chol"]["side_work"] = ("both layers' Kuf images" + (", tril(q_sqrt) images and KL terms"
-                                                if q else "") + " on idle CUs of the step launches")
     for name in ("elbo_terms", "gauss_kl", "allreduce", "split_tri"):
         if name in st:
             kernels[name] = {"avg_us": st[name][0] * 1e3}

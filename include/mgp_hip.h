@@ -123,30 +123,14 @@ int mgp_kuu_potrf_trtri_ex(const float* const* Z, int64_t ldz, int64_t M, int32_
  * pointers, each at least mgp_x6_cols_bytes(M, N) bytes (kfr_bytes), 16-B aligned.
  * With M <= 64 (no step launches) the images are written by mgp_rbf_kuf_* launches
  * on the stream after the Kuu build.  -19 .. -24: X, ldx, N, Kfr, kfr_bytes,
- * kfr_format.
- * Optional q_sqrt job (q_sqrt non-NULL): per batch entry the whitened KL
- * (models.py:79, prior_kl) into kl_out[b] (one device double) and the split-f16 image of
- * tril(q_sqrt) into Lfr[b] -- the results of mgp_gauss_kl_white and
- * mgp_split_lower_f16 on the same operands, written by the same extra workgroups: the
- * KL partial sums, which also fold the image's scale bound, in the first step launch,
- * the image and the final KL sums in later ones.  q_mu [M][ldq >= K], q_sqrt
- * [K][M][ldqs] (stride strideq; ldqs, strideq multiples of 4, 16-B aligned), Lfr at
- * least mgp_x6_lower_bytes(M, K) bytes (lfr_bytes, 16-B aligned), kl_workspace at
- * least batch * mgp_kl_workspace_bytes(M, K) bytes (entry b at b times that size).
- * With M <= 128 (fewer than two step launches) mgp_split_lower_f16 and
- * mgp_gauss_kl_white run after the factorisation on the stream.  -25 .. -33: q_mu,
- * ldq, ldqs, strideq, K, Lfr, lfr_bytes, kl_out, kl_workspace. */
+ * kfr_format. */
 int mgp_kuu_potrf_trtri_kuf(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
                             const float* const* variance, const float* const* lengthscales,
                             const int32_t* n_ls, float jitter, int32_t batch, float* L,
                             float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                             void* workspace, size_t workspace_bytes, void* prep_done,
                             float* const* linvt_absmax, const float* X, int64_t ldx, int64_t N,
-                            void* const* Kfr, size_t kfr_bytes, int32_t kfr_format,
-                            const float* const* q_mu, int64_t ldq, const float* const* q_sqrt,
-                            int64_t ldqs, int64_t strideq, int32_t K, void* const* Lfr, size_t lfr_bytes,
-                            double* const* kl_out, void* kl_workspace, size_t kl_workspace_bytes,
-                            mgp_stream_t stream);
+                            void* const* Kfr, size_t kfr_bytes, int32_t kfr_format, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K4
  * Whitened projection A = L^-1 Kuf (as the triangular GEMM LinvT^T . Kuf) plus

@@ -60,8 +60,7 @@ SIGNATURES = {
     "mgp_kuu_potrf_trtri_kuf": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_ptr,
                                             ctypes.c_float, c_i32, c_ptr, c_ptr, c_i64, c_i64, c_ptr,
                                             c_ptr, c_size, c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_size,
-                                            c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_size,
-                                            c_ptr, c_ptr, c_size, c_ptr]),
+                                            c_i32, c_ptr]),
     "mgp_stats_tiles": (ctypes.c_int, [c_i64]),
     "mgp_trsm_stats": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                       c_ptr, c_i64, c_ptr, c_i64, c_ptr]),

@@ -98,14 +98,11 @@ def set_expert_cross(cross):
 #              every schedule computes the same bits):
 #   "k1_in_k3" (default since round 5) both layers' K1 run inside K3's step launches, on
 #              extra workgroups that take the CUs the latency-bound chain leaves idle
-#              (mgp_kuu_potrf_trtri_kuf: the same image blocks, bit-identical), and with
-#              the split-f16 images so do both layers' tril(q_sqrt) images and KL terms
-#              (its q_sqrt job).  Beside the chain on a side stream, K1's 8192 workgroups
-#              held the CUs that the next step launch's workgroups waited for (32-41 us
-#              gaps, round 4 stamps), and the q_sqrt work slowed its first six steps;
+#              (mgp_kuu_potrf_trtri_kuf: the same image blocks, bit-identical); the
+#              tril(q_sqrt) images and the KL on the side stream as in "overlap".  Beside
+#              the chain on a side stream, K1's 8192 workgroups held the CUs that the
+#              next step launch's workgroups waited for (32-41 us gaps, round 4 stamps);
 #              with batched K3 only (equal M for both layers), else as "overlap";
-#   "k1_in_k3_qside" as k1_in_k3, with the tril(q_sqrt) images and the KL on the side
-#              stream (the first round-5 form);
 #   "overlap"  K1 and the tril(q_sqrt) images of both layers and the KL on a side
 #              stream beside K3 (round 1-4 default);
 #   "k1a_late" the assign layer's K1 on the side stream after K3, beside the pred
@@ -115,7 +112,7 @@ def set_expert_cross(cross):
 #   "k1_main"  both K1 on the main stream after K3 (only the small images and
 #              the KL beside the chain);
 #   "serial"   everything on the main stream, K3 alone on the chip.
-STEP_SCHEDULES = ("k1_in_k3", "k1_in_k3_qside", "overlap", "k1a_late", "k1a_k5", "k1_main", "serial")
+STEP_SCHEDULES = ("k1_in_k3", "overlap", "k1a_late", "k1a_k5", "k1_main", "serial")
 
 
 def step_schedule():

@@ -35,7 +35,6 @@
 
 #include "kuf_image.hpp"
 #include "mgp_common.hpp"
-#include "qsqrt_jobs.hpp"
 
 namespace mgp {
 
@@ -86,21 +85,6 @@ struct CholArgs {
   const float* kx; int64_t kldx, kN;
   bf16x8* kfr[kMaxBatch]; float* kbound[kMaxBatch];
   int kf16, knmk, krow_blocks; int64_t kblocks;   // blocks per batch entry
-  // optional q_sqrt side job (the same entry): per batch entry the whitened-KL partial sums
-  // and the tril(q_sqrt) image bound (launch 0), then the split-f16 image of tril(q_sqrt)
-  // and the KL itself (later launches) -- qsqrt_jobs.hpp, the bodies of the K7 and
-  // mgp_split_lower_f16 launches
-  const float* qm[kMaxBatch]; const float* qs[kMaxBatch];
-  bf16x8* lfr[kMaxBatch]; float* lbound[kMaxBatch]; double* klp[kMaxBatch]; double* klo[kMaxBatch];
-  int64_t ldq, ldqs, strideq; int qK, qnrb, qnmb, qnmk; int64_t qnkl, qnfrag;   // KL items, fragments per entry
-};
-
-// The side work of one step launch: Kuf image blocks [k0, k1), KL items [q0, q1), q_sqrt
-// image fragments [f0, f1) (batch-major global indices), the final KL sums (fin), on nkwg
-// workgroups past the launch's tile workgroups.
-struct SideRange {
-  int64_t k0, k1, q0, q1, f0, f1;
-  int nkwg, fin;
 };
 
 __device__ __forceinline__ double* ws_W(const CholArgs& a, int b) { return a.ws + (int64_t)b * a.strideWS; }
@@ -892,12 +876,10 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     if (threadIdx.x == 0) {
       a.info[b] = 0;
       float* lt = a.lt_absmax[0];
-      float* lb = a.lbound[0];
 #pragma unroll
       for (int i = 1; i < kMaxBatch; ++i)
-        if (b == i) { lt = a.lt_absmax[i]; lb = a.lbound[i]; }
+        if (b == i) lt = a.lt_absmax[i];
       if (lt) *lt = 0.f;
-      if (lb) *lb = 0.f;   // the q_sqrt side job's image bound (atomicMax from launch 0 on)
     }
     build_tile(s1, LDT, 0, 0, reinterpret_cast<float*>(s2));
     __syncthreads();
@@ -1022,72 +1004,6 @@ __device__ __forceinline__ void kuf_side_job(const CholArgs& a, int w, int64_t k
   else kuf_side_blocks<32>(a, w, k0, k1, nkwg, lds);
 }
 
-// Sum over a 256-thread group of the 512-thread workgroup (block_sum's order for 256 threads:
-// the wave sums added in wave order by the group's thread 0).  scratch: 8 doubles.
-__device__ __forceinline__ double group_sum(double v, double* scratch) {
-  v = wave_sum(v);
-  const int g = threadIdx.x >> 8, w = (threadIdx.x >> 6) & 3, lane = threadIdx.x & 63;
-  if (lane == 0) scratch[4 * g + w] = v;
-  __syncthreads();
-  double r = 0;
-  if ((threadIdx.x & 255) == 0)
-    for (int i = 0; i < 4; ++i) r += scratch[4 * g + i];
-  __syncthreads();
-  return r;
-}
-
-// The q_sqrt side job of a step launch (workgroup w of nkwg).  KL items and the final sums
-// run two per pass (one per group, the pass uniform across the workgroup: every group takes
-// the same barriers); image fragments one per wave, no barriers.
-__device__ __forceinline__ void q_side_job(const CholArgs& a, int w, int batch, const SideRange& sr, double* red) {
-  typedef const CholArgs __attribute__((address_space(4))) KernargCholArgs;
-  const KernargCholArgs& ag = *(const KernargCholArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
-  const int t = (int)(threadIdx.x & 255), lane = (int)(threadIdx.x & 63);
-  if (sr.q1 > sr.q0) {   // KL partial sums + the image bound (launch 0)
-    const int64_t per = 2 * (int64_t)sr.nkwg;
-    const int64_t passes = (sr.q1 - sr.q0 + per - 1) / per;
-    for (int64_t it = 0; it < passes; ++it) {
-      const int64_t item = sr.q0 + it * per + 2 * w + g;
-      const bool active = item < sr.q1;
-      const int b = __builtin_amdgcn_readfirstlane(active ? (int)(item / a.qnkl) : 0);
-      const int blk = (int)(item - (int64_t)b * a.qnkl);
-      KlPartial r = {0.f, 0.f, 0.f, 0.f};
-      if (active) r = kl_partials_thread(ag.qm[b], a.ldq, ag.qs[b], a.ldqs, a.strideq, a.M, a.qK, a.qnrb, blk, t, 256);
-      const float m = wave_max_f32(r.amax);
-      if (active && lane == 0 && m > 0.f) atomicMax(reinterpret_cast<unsigned int*>(ag.lbound[b]), __float_as_uint(m));
-      const double s0 = group_sum((double)r.tr, red), s1 = group_sum((double)r.ld, red),
-                   s2 = group_sum((double)r.mh, red);
-      if (active && t == 0) {
-        double* p = ag.klp[b] + 3 * (int64_t)blk;
-        p[0] = s0;
-        p[1] = s1;
-        p[2] = s2;
-      }
-    }
-  }
-  if (sr.fin && w == 0) {   // the KL of every batch entry (kl_final_kernel's sums)
-    for (int b0 = 0; b0 < batch; b0 += 2) {
-      const int b = b0 + g;
-      const bool active = b < batch;
-      double tr = 0.0, ld = 0.0, mh = 0.0;
-      if (active) kl_final_thread(ag.klp[b], (int)a.qnkl, t, 256, tr, ld, mh);
-      tr = group_sum(tr, red);
-      ld = group_sum(ld, red);
-      mh = group_sum(mh, red);
-      if (active && t == 0) *ag.klo[b] = 0.5 * (mh - (double)a.M * (double)a.qK - ld + tr);
-    }
-  }
-  if (sr.f1 > sr.f0) {   // split-f16 image fragments of tril(q_sqrt) (launches >= 1: the bound is final)
-    const int64_t stride = (int64_t)sr.nkwg * 8;
-    for (int64_t fi = sr.f0 + (int64_t)w * 8 + (int64_t)(threadIdx.x >> 6); fi < sr.f1; fi += stride) {
-      const int b = __builtin_amdgcn_readfirstlane((int)(fi / a.qnfrag));
-      split_tri_frag<true>(ag.qs[b], a.ldqs, a.strideq, a.M, a.qnmb, a.qnmk, fi - (int64_t)b * a.qnfrag, lane, ag.lfr[b],
-                           ag.lbound[b]);
-    }
-  }
-}
-
 // ------------------------------------------------------------------ step launch j, tile pairs
 // chol_step with the trailing-update and forward-substitution tiles of step j taken two
 // at a time along a tile row i, one 256-thread group per tile in a 512-thread
@@ -1125,15 +1041,14 @@ __host__ __device__ inline int step_pair_count(int nb, int j) {  // per batch en
 // the round-robin placement (speed only, nothing depends on it): a row's pairs then load
 // its panel tile W_ij into one L2 and a run's rows (of one batch entry where the run
 // does not straddle two) share the panel tiles W_lj, B_jc there.  No idle workgroups.
-// Workgroups past batch (1 + Pb) (when the launch carries side work): q_side_job and
-// kuf_side_job over the ranges of `sr`, sr.nkwg of them.
-__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb, SideRange sr) {
+// Workgroups past batch (1 + Pb) (when the launch carries a Kuf side job): kuf_side_job
+// over the image blocks [k0, k1), nkwg of them.
+__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb, int64_t k0,
+                                                               int64_t k1, int nkwg) {
   __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB];
   if ((int)blockIdx.x >= batch * (1 + Pb)) {   // uniform per workgroup
-    const int w = (int)blockIdx.x - batch * (1 + Pb);
-    if (sr.q1 > sr.q0 || sr.fin || sr.f1 > sr.f0) q_side_job(a, w, batch, sr, col);
-    if (sr.k1 > sr.k0)
-      kuf_side_job(a, w, sr.k0, sr.k1, sr.nkwg, reinterpret_cast<float*>(s1), reinterpret_cast<float*>(sD));
+    kuf_side_job(a, (int)blockIdx.x - batch * (1 + Pb), k0, k1, nkwg, reinterpret_cast<float*>(s1),
+                 reinterpret_cast<float*>(sD));
     return;
   }
   ENTRYTIME(t_entry);
@@ -1442,33 +1357,10 @@ struct KufSideJob {
 
 extern "C" size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
 
-// The q_sqrt side job of a factorisation (mgp_kuu_potrf_trtri_kuf): per batch entry q_mu
-// [M][ldq >= K], q_sqrt [K][M][ldqs] (stride strideq), the split-f16 image Lfr (at least
-// mgp_x6_lower_bytes(M, K)), the KL out (one double) and its partial sums (kl_ws, entry b at
-// b * mgp_kl_workspace_bytes(M, K)).
-struct QSideJob {
-  const float* const* q_mu; int64_t ldq;
-  const float* const* q_sqrt; int64_t ldqs, strideq; int K;
-  void* const* Lfr; double* const* kl_out; char* kl_ws;
-};
-
-extern "C" size_t mgp_x6_lower_bytes(int64_t M, int32_t K);
-extern "C" size_t mgp_kl_workspace_bytes(int64_t M, int32_t K);
-extern "C" int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
-                                   void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
-extern "C" int mgp_gauss_kl_white(const float* q_mu, int64_t ldq, const float* q_sqrt, int64_t ldqs,
-                                  int64_t strideq, int64_t M, int32_t K, double* kl_out,
-                                  void* workspace, size_t workspace_bytes, mgp_stream_t stream);
-
-// The side work per step launch j.  Work units (from the step launches' durations with each
-// kind of side work, profiles/r05q_*): a Kuf image block 1, a KL item 1, an image fragment
-// 1/8.  Each launch
-// takes a share of the units proportional to the CUs its tile workgroups leave idle (one
-// workgroup per CU: the step kernel's LDS; at least an eighth of the CUs).  The KL items
-// (which fold the image bound) run first, spread over as many launches as their units fill,
-// the image fragments and the final KL sums after them (the bound is final at the launch
-// boundary), the Kuf blocks in what is left of every launch's share.
-static void side_plan(int nb, int batch, int64_t ktot, int64_t qtot, int64_t ftot, std::vector<SideRange>& plan) {
+// Share of the image blocks per step launch j: proportional to the CUs the launch's tile
+// workgroups leave idle (one workgroup per CU: the step kernel's LDS), at least an eighth
+// of the CUs each.
+static void kuf_side_split(int nb, int batch, int64_t total, std::vector<int64_t>& beg, std::vector<int>& nwg) {
   int cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -1480,45 +1372,19 @@ static void side_plan(int nb, int batch, int64_t ktot, int64_t qtot, int64_t fto
     idle[j] = std::max<double>(cus - batch * (1 + step_pair_count(nb, j)), cus / 8.0);
     sum += idle[j];
   }
-  constexpr double kQ = 1.0, kF = 1.0 / 8.0;
-  const double total = (double)ktot + kQ * (double)qtot + kF * (double)ftot;
-  const double per = total / steps;
-  // launches [0, lq) carry the KL items, [lq, steps) the fragments, spread thin (a fragment
-  // is a few dependent load round trips of one wave: many per wave would outlast the chain)
-  int lq = 0, lf = 0;
-  if (qtot > 0) {
-    lq = std::max(1, std::min(steps - 1, (int)(kQ * qtot / per + 0.5)));
-    lf = steps - lq;
-  }
-  plan.assign(steps, SideRange{0, 0, 0, 0, 0, 0, 0, 0});
-  int64_t k = 0;
-  double acc = 0.0, used = 0.0;
+  beg.assign(steps + 1, 0);
+  nwg.assign(steps, 0);
+  double acc = 0.0;
   for (int j = 0; j < steps; ++j) {
-    SideRange& r = plan[j];
     acc += idle[j];
-    if (j < lq) {
-      r.q0 = qtot * j / lq;
-      r.q1 = qtot * (j + 1) / lq;
-    } else if (j < lq + lf) {
-      r.f0 = ftot * (j - lq) / lf;
-      r.f1 = ftot * (j - lq + 1) / lf;
-      r.fin = (j == lq) ? 1 : 0;
-    }
-    const double q_units = kQ * (double)(r.q1 - r.q0) + kF * (double)(r.f1 - r.f0);
-    const double room = total * (acc / sum) - used - q_units;   // this launch's share (and any earlier shortfall)
-    const int64_t nk = j + 1 == steps ? ktot - k : std::min<int64_t>(ktot - k, (int64_t)std::max(0.0, room + 0.5));
-    r.k0 = k;
-    r.k1 = k + nk;
-    k += nk;
-    used += q_units + (double)nk;
-    const int64_t need = std::max<int64_t>(std::max<int64_t>((nk + 1) / 2, (r.q1 - r.q0 + 1) / 2),
-                                           std::max<int64_t>((r.f1 - r.f0 + 7) / 8, r.fin));
-    r.nkwg = (int)std::min<int64_t>(need, (int64_t)idle[j]);
+    beg[j + 1] = j + 1 == steps ? total : std::min<int64_t>(total, (int64_t)(total * (acc / sum) + 0.5));
+    const int64_t cnt = beg[j + 1] - beg[j];
+    nwg[j] = (int)std::min<int64_t>((cnt + 1) / 2, (int64_t)idle[j]);
   }
 }
 
 static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_bytes, hipStream_t s,
-                    hipEvent_t prep_done = nullptr, const KufSideJob* kj = nullptr, const QSideJob* qj = nullptr) {
+                    hipEvent_t prep_done = nullptr, const KufSideJob* kj = nullptr) {
   if (!workspace || workspace_bytes < mgp_chol_workspace_bytes(a.M, batch)) return MGP_ERR_WORKSPACE;
   if (!aligned16(workspace)) return MGP_ERR_ALIGN;
   // the diagonal tiles of L and L^-T are written with 16-byte stores
@@ -1529,7 +1395,8 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
   a.strideWS = chol_ws_doubles_per_batch(a.M);
   a.ws = (double*)workspace;
   const dim3 block(kCholThreads);
-  int64_t ktot = 0, qtot = 0, ftot = 0;
+  std::vector<int64_t> kbeg;
+  std::vector<int> knwg;
   if (kj && kj->N > 0 && a.M > 0) {
     a.kx = kj->X; a.kldx = kj->ldx; a.kN = kj->N; a.kf16 = kj->f16 ? 1 : 0;
     const int64_t mp = (a.M + 127) / 128 * 128;
@@ -1540,32 +1407,8 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
       a.kfr[b] = (bf16x8*)kj->Kfr[b];
       a.kbound[b] = (float*)((char*)kj->Kfr[b] + mgp_x6_cols_bytes(a.M, kj->N) - 256);  // image trailer
     }
-    if (a.nb >= 2) ktot = batch * a.kblocks;
+    if (a.nb >= 2) kuf_side_split(a.nb, batch, batch * a.kblocks, kbeg, knwg);
   }
-  // the q_sqrt side job needs a launch after the one that folds the bound (nb >= 3);
-  // otherwise its own launches follow the factorisation on the stream
-  const bool q_side = qj && a.M > 0 && a.nb >= 3;
-  if (q_side) {
-    const int64_t mp = (a.M + 127) / 128 * 128;
-    a.ldq = qj->ldq; a.ldqs = qj->ldqs; a.strideq = qj->strideq; a.qK = qj->K;
-    a.qnrb = (int)((a.M + kKlRows - 1) / kKlRows);
-    a.qnmb = (int)(mp / 32);
-    a.qnmk = (int)(mp / 16);
-    a.qnkl = (int64_t)a.qK * a.qnrb + 1;
-    a.qnfrag = (int64_t)a.qK * a.qnmb * a.qnmk;
-    for (int b = 0; b < batch; ++b) {
-      a.qm[b] = qj->q_mu[b];
-      a.qs[b] = qj->q_sqrt[b];
-      a.lfr[b] = (bf16x8*)qj->Lfr[b];
-      a.lbound[b] = (float*)((char*)qj->Lfr[b] + mgp_x6_lower_bytes(a.M, a.qK) - 256);   // image trailer
-      a.klp[b] = (double*)(qj->kl_ws + (size_t)b * mgp_kl_workspace_bytes(a.M, a.qK));
-      a.klo[b] = qj->kl_out[b];
-    }
-    qtot = batch * a.qnkl;
-    ftot = batch * a.qnfrag;
-  }
-  std::vector<SideRange> plan;
-  if (ktot + qtot + ftot > 0) side_plan(a.nb, batch, ktot, qtot, ftot, plan);
   hipLaunchKernelGGL(chol_prep, dim3(a.nb * a.nb + 1, batch), block, 0, s, a);
   int st = launch_status();
   if (st) return st;
@@ -1586,25 +1429,15 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
     const int T = a.nb - j - 1;
     if (T > 0) {
       const int Pb = step_pair_count(a.nb, j);
-      const SideRange sr = plan.empty() ? SideRange{0, 0, 0, 0, 0, 0, 0, 0} : plan[j];
-      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb) + sr.nkwg), dim3(kPairThreads), 0, s, a, j, batch, Pb,
-                         sr);
+      const bool side = !kbeg.empty() && knwg[j] > 0;
+      const int nkwg = side ? knwg[j] : 0;
+      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb) + nkwg), dim3(kPairThreads), 0, s, a, j, batch, Pb,
+                         side ? kbeg[j] : (int64_t)0, side ? kbeg[j + 1] : (int64_t)0, nkwg);
     } else {
       hipLaunchKernelGGL(chol_last_step, dim3(a.nb, batch), block, 0, s, a, j);
     }
     st = launch_status();
     if (st) return st;
-  }
-  if (qj && a.M > 0 && !q_side) {   // too few step launches to carry the q_sqrt job: its own launches
-    const size_t klb = mgp_kl_workspace_bytes(a.M, qj->K);
-    for (int b = 0; b < batch; ++b) {
-      st = mgp_split_lower_f16(qj->q_sqrt[b], qj->ldqs, qj->strideq, a.M, qj->K, qj->Lfr[b],
-                               mgp_x6_lower_bytes(a.M, qj->K), s);
-      if (st) return st;
-      st = mgp_gauss_kl_white(qj->q_mu[b], qj->ldq, qj->q_sqrt[b], qj->ldqs, qj->strideq, a.M, qj->K, qj->kl_out[b],
-                              qj->kl_ws + (size_t)b * klb, klb, s);
-      if (st) return st;
-    }
   }
   return MGP_OK;
 }
@@ -1635,7 +1468,7 @@ static int kuu_potrf_trtri_impl(const float* const* Z, int64_t ldz, int64_t M, i
                                    float* LinvT, int64_t ldl, int64_t strideL, int32_t* info,
                                    void* workspace, size_t workspace_bytes, hipEvent_t prep_done,
                                    float* const* lt_absmax, mgp_stream_t stream,
-                                   const KufSideJob* kj = nullptr, const QSideJob* qj = nullptr) {
+                                   const KufSideJob* kj = nullptr) {
   if (!Z) return -1;
   if (ldz < D) return -2;
   if (M < 0) return -3;
@@ -1660,7 +1493,7 @@ static int kuu_potrf_trtri_impl(const float* const* Z, int64_t ldz, int64_t M, i
   a.ldz = ldz; a.D = D; a.jitter = (double)jitter;
   a.L = L; a.LinvT = LinvT; a.ldl = ldl; a.strideL = strideL;
   a.info = info; a.M = M;
-  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream, prep_done, kj, qj);
+  return chol_run(a, batch, workspace, workspace_bytes, (hipStream_t)stream, prep_done, kj);
 }
 
 extern "C" int mgp_kuu_potrf_trtri(const float* const* Z, int64_t ldz, int64_t M, int32_t D,
@@ -1699,9 +1532,6 @@ extern "C" int mgp_kuu_potrf_trtri_kuf(const float* const* Z, int64_t ldz, int64
                                        void* workspace, size_t workspace_bytes, void* prep_done,
                                        float* const* linvt_absmax, const float* X, int64_t ldx, int64_t N,
                                        void* const* Kfr, size_t kfr_bytes, int32_t kfr_format,
-                                       const float* const* q_mu, int64_t ldq, const float* const* q_sqrt,
-                                       int64_t ldqs, int64_t strideq, int32_t K, void* const* Lfr, size_t lfr_bytes,
-                                       double* const* kl_out, void* kl_workspace, size_t kl_workspace_bytes,
                                        mgp_stream_t stream) {
   if (!X) return -19;
   if (ldx < D) return -20;
@@ -1717,30 +1547,8 @@ extern "C" int mgp_kuu_potrf_trtri_kuf(const float* const* Z, int64_t ldz, int64
     }
   }
   const KufSideJob kj = {X, ldx, N, Kfr, kfr_format == 1};
-  if (!q_sqrt)   // no q_sqrt job
-    return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
-                                info, workspace, workspace_bytes, (hipEvent_t)prep_done, linvt_absmax, stream, &kj);
-  if (!q_mu) return -25;
-  if (ldq < K) return -26;
-  if (ldqs < M) return -27;
-  if (K > 1 && strideq < ldqs * M) return -28;
-  if (K < 1) return -29;
-  if (!Lfr) return -30;
-  if (!kl_out) return -32;
-  if ((ldqs & 3) || (strideq & 3)) return MGP_ERR_ALIGN;   // the KL sums' float4 rows
-  if (M > 0 && batch > 0 && batch <= kMaxBatch) {
-    if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return -31;
-    if (!kl_workspace || kl_workspace_bytes < (size_t)batch * mgp_kl_workspace_bytes(M, K)) return -33;
-    for (int b = 0; b < batch; ++b) {
-      if (!q_mu[b] || !q_sqrt[b]) return -25;
-      if (!Lfr[b]) return -30;
-      if (!kl_out[b]) return -32;
-      if (!aligned16(q_sqrt[b]) || !aligned16(Lfr[b])) return MGP_ERR_ALIGN;
-    }
-  }
-  const QSideJob qj = {q_mu, ldq, q_sqrt, ldqs, strideq, K, Lfr, kl_out, (char*)kl_workspace};
   return kuu_potrf_trtri_impl(Z, ldz, M, D, variance, lengthscales, n_ls, jitter, batch, L, LinvT, ldl, strideL,
-                              info, workspace, workspace_bytes, (hipEvent_t)prep_done, linvt_absmax, stream, &kj, &qj);
+                              info, workspace, workspace_bytes, (hipEvent_t)prep_done, linvt_absmax, stream, &kj);
 }
 
 extern "C" size_t mgp_chol_backward_workspace_bytes(int64_t M) {

@@ -44,7 +44,6 @@
 #include <type_traits>
 
 #include "mgp_common.hpp"
-#include "qsqrt_jobs.hpp"
 
 #ifndef MGP_K4_STORE_NT
 #define MGP_K4_STORE_NT 1   // K4's A-image stores non-temporal (0: plain, for A/B builds)
@@ -78,7 +77,24 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
                                                         const float* __restrict__ bound = nullptr) {
   const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= nfrag) return;
-  split_tri_frag<LOWER, TRANS, FULL>(src, ld, stride, M, nmb, nmk, f, threadIdx.x & 63, img, bound);
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int mk = (int)(f % nmk);
+  const int64_t kb = f / nmk;
+  const int mb = (int)(kb % nmb);
+  const int b = (int)(kb / nmb);
+  const int64_t mc = 32 * (int64_t)mb + r;
+  const float* S = src + (int64_t)b * stride;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t m = 16 * (int64_t)mk + kperm(h, j);
+    const bool keep = FULL || (LOWER ? (m >= mc) : (m <= mc));
+    v[j] = (m < M && mc < M && keep) ? S[TRANS ? mc * ld + m : m * ld + mc] : 0.f;
+  }
+  if (bound)
+    store_split_f16<true>(img + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
+  else
+    store_split(img + f * 3 * 64 + lane, v);
 }
 
 // split_tri_kernel<false> (the split-f16 L^-T images) for two matrices at src and

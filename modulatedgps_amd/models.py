@@ -566,16 +566,14 @@ class SMGP(SGP):
         self._bufs[key] = b
         return b
 
-    def _factorise(self, b, prep_event=None, tfr_bounds=False, kuf=None, qjob=None):
+    def _factorise(self, b, prep_event=None, tfr_bounds=False, kuf=None):
         """Kuu of both layers and their batched Cholesky + inverse (one K3 sweep).
         Training buffers also keep L (b["L_f"], b["L_a"]) for the backward pass.
         prep_event: recorded once Kuu is built (batched path only; else after K3).
         tfr_bounds: K3 also writes max |LinvT| into the L^-T split-f16 images'
         trailers (b["Tfr_f"], b["Tfr_a"]; batched path), for bounded splits.
         kuf: (X, fmt) -- K3's step launches also write both layers' Kuf images
-        (b["Kfr_f"], b["Kfr_a"]; batched path, schedule "k1_in_k3").
-        qjob: [KL out per layer] -- with kuf and the split-f16 format, the same launches
-        also write both layers' tril(q_sqrt) images (b["Lfr_f"], b["Lfr_a"]) and KL terms."""
+        (b["Kfr_f"], b["Kfr_a"]; batched path, schedule "k1_in_k3")."""
         pf, pa = self.pred_layer, self.assign_layer
         train = b.get("train", False)
         if "LinvT2" in b:
@@ -587,9 +585,7 @@ class SMGP(SGP):
                 [pf.kernel.lengthscales, pa.kernel.lengthscales], default_jitter(), LinvT=b["LinvT2"],
                 L=b.get("L2"), want_L=train, prep_event=prep_event,
                 tfr_bound_images=[b["Tfr_f"], b["Tfr_a"]] if tfr_bounds else None,
-                kuf=(kuf[0], [b["Kfr_f"], b["Kfr_a"]], kuf[1]) if kuf is not None else None,
-                qjob=([pf.q_mu, pa.q_mu], [pf.q_sqrt, pa.q_sqrt], [b["Lfr_f"], b["Lfr_a"]], qjob,
-                      b.get("kl_ws")) if qjob is not None else None)
+                kuf=(kuf[0], [b["Kfr_f"], b["Kfr_a"]], kuf[1]) if kuf is not None else None)
             self.last_info = info
             if train:
                 b["L_f"], b["L_a"] = Lo[0], Lo[1]
@@ -645,27 +641,13 @@ class SMGP(SGP):
         bounded = b["x6"] and "Tfr_a" in b and "LinvT2" in b and fmt == "f16"
         sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
         # schedule k1_in_k3: both layers' K1 as a side job of K3's step launches (batched K3)
-        k1_in_k3 = (sched in ("k1_in_k3", "k1_in_k3_qside") and "LinvT2" in b and self.pred_layer.kernel._x(X) is X
+        k1_in_k3 = (sched == "k1_in_k3" and "LinvT2" in b and self.pred_layer.kernel._x(X) is X
                     and self.assign_layer.kernel._x(X) is X)
-        if sched in ("k1_in_k3", "k1_in_k3_qside") and not k1_in_k3:
+        if sched == "k1_in_k3" and not k1_in_k3:
             sched = "overlap"
-        # ... and with the split-f16 images, both layers' tril(q_sqrt) images and KL terms too
-        q_in_k3 = k1_in_k3 and sched == "k1_in_k3" and fmt == "f16" and "Lfr_f" in b
-        qjob = None
-        if q_in_k3:
-            if kl_out is not None:
-                qjob = [kl_out[0:1], kl_out[1:2]]
-            else:   # prediction: the KL values are not wanted, the images are
-                if "kl_scratch" not in b:
-                    b["kl_scratch"] = torch.empty(2, dtype=torch.float64, device=X.device)
-                qjob = [b["kl_scratch"][0:1], b["kl_scratch"][1:2]]
-            if "kl_ws" not in b:
-                M, K = self.pred_layer.q_mu.shape
-                b["kl_ws"] = torch.empty(2 * ops._lib.load().mgp_kl_workspace_bytes(M, K), dtype=torch.uint8,
-                                         device=X.device)
         with _Stage(timing, "kuu_chol"):
             LinvT_f, LinvT_a = self._factorise(b, prep_event=prep, tfr_bounds=bounded,
-                                               kuf=(X, fmt) if k1_in_k3 else None, qjob=qjob)
+                                               kuf=(X, fmt) if k1_in_k3 else None)
         Tfr = {}
         if b["x6"] and "Tfr_a" in b:
             # L^-T images straight after K3 on its stream (no cross-stream wait in front)
@@ -675,11 +657,9 @@ class SMGP(SGP):
                 else:
                     for L, lt in (("f", LinvT_f), ("a", LinvT_a)):
                         Tfr[L] = ops.split_upper_x6(lt, out=b["Tfr_" + L], fmt=fmt, bounded=bounded)
-        late = {"k1_in_k3": (), "k1_in_k3_qside": (), "overlap": (), "k1a_late": ("a",), "k1a_k5": ("a",), "k1_main": ("f", "a"),
+        late = {"k1_in_k3": (), "overlap": (), "k1a_late": ("a",), "k1a_k5": ("a",), "k1_main": ("f", "a"),
                 "serial": ("f", "a")}[sched]
         if b["x6"]:
-            colmax = _COLMAX_SIDE and "colmax_f" in b   # training: the C_k bounds, off the K3 -> K5 path
-
             def side_work():
                 for L, layer in layers:
                     X_ = layer.kernel._x(X)
@@ -688,16 +668,15 @@ class SMGP(SGP):
                             ops.rbf_kuf_x6(X_, layer.Z, layer.kernel.variance, layer.kernel.lengthscales,
                                            out=b["Kfr_" + L], fmt=fmt)
                     with _Stage(timing, "split_tri"):
-                        if not q_in_k3:
-                            ops.split_lower_x6(layer.q_sqrt, out=b["Lfr_" + L], fmt=fmt)
-                        if colmax:
+                        ops.split_lower_x6(layer.q_sqrt, out=b["Lfr_" + L], fmt=fmt)
+                        if _COLMAX_SIDE and "colmax_" + L in b:   # training: the C_k bound, off the K3 -> K5 path
                             ops.colnorm_max(layer.q_sqrt, out=b["colmax_" + L])
                     images[L] = (b["Kfr_" + L], b["Lfr_" + L])
-                if kl_out is not None and not q_in_k3:
+                if kl_out is not None:
                     with _Stage(timing, "gauss_kl"):
                         self.pred_layer.prior_kl(out=kl_out[0:1])
                         self.assign_layer.prior_kl(out=kl_out[1:2])
-            if sched == "serial" or (q_in_k3 and not colmax):   # (the latter: nothing left for a side stream)
+            if sched == "serial":
                 side_work()
             else:
                 side.wait_event(prep)   # after Kuu's build (and so after everything before K3 on main)
@@ -738,8 +717,7 @@ class SMGP(SGP):
             bf, ba = bufs["f"], bufs["a"]
             # both layers' K4 in one launch (mgp_trsm_stats_f16_batch, bit-identical to
             # two): one kernel tail and dispatch-round boundary fewer (~25 us, measured)
-            batched = (_K4_BATCHED and sched in ("k1_in_k3", "k1_in_k3_qside", "overlap", "k1_main", "serial")
-                       and fmt == "f16"
+            batched = (_K4_BATCHED and sched in ("k1_in_k3", "overlap", "k1_main", "serial") and fmt == "f16"
                        and expert_cross() == "f16"
                        and pf.num_inducing == pa.num_inducing and pf.num_latent_gps == pa.num_latent_gps
                        and all(x.get("Afr") is not None and x.get("stats") is not None for x in (bf, ba))

@@ -124,8 +124,7 @@ def potrf_trtri(A, L=None, LinvT=None, info=None, workspace=None):
 
 
 def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, info=None,
-                    workspace=None, want_L=False, prep_event=None, tfr_bound_images=None, kuf=None,
-                    qjob=None):
+                    workspace=None, want_L=False, prep_event=None, tfr_bound_images=None, kuf=None):
     """Kuu (float64, from Z) + Cholesky + inverse for a batch of layers sharing M, D.
     Zs / variances / lengthscales: lists of device tensors.  Returns L (or None),
     LinvT [B, M, M] and info int32 [B].  prep_event: a torch.cuda.Event (already
@@ -135,10 +134,7 @@ def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, inf
     bounded=True) skips its reduction).
     kuf: (X [N, D], [image per layer], fmt "f16" | "x6"): the factorisation's step
     launches also write each layer's Kuf image K(Z_b, X), bit-identical to
-    rbf_kuf_x6(X, Z_b, ..., fmt=fmt) (mgp_kuu_potrf_trtri_kuf).
-    qjob (with kuf): ([q_mu per layer], [q_sqrt per layer], [split-f16 image per layer],
-    [KL out per layer: float64 [1]], KL workspace or None): the same launches also write
-    split_lower_x6(q_sqrt, fmt="f16") and gauss_kl_white(q_mu, q_sqrt) of every layer."""
+    rbf_kuf_x6(X, Z_b, ..., fmt=fmt) (mgp_kuu_potrf_trtri_kuf)."""
     import ctypes
     Bt = len(Zs)
     M, D = Zs[0].shape
@@ -174,30 +170,12 @@ def kuu_potrf_trtri(Zs, variances, lengthscales, jitter, LinvT=None, L=None, inf
         bp = None
         if tfr_bound_images is not None:
             bp = P(*[lib.mgp_x6_bound_ptr(t.data_ptr(), M, 0, 1) for t in tfr_bound_images])
-        q = (None, 0, None, 0, 0, 0, None, 0, None, None, 0)
-        if qjob is not None:
-            q_mus, q_sqrts, lfrs, kls, klws = qjob
-            q_sqrts = [as_padded(t) for t in q_sqrts]   # float4 rows (no copy for the layers' storage)
-            K = q_mus[0].shape[1]
-            for qm, qs in zip(q_mus, q_sqrts):
-                _check(qm, "q_mu", 2), _check(qs, "q_sqrt", 3)
-                if (tuple(qm.shape) != (M, K) or tuple(qs.shape) != (K, M, M) or _ld(qm) != _ld(q_mus[0])
-                        or _ld(qs) != _ld(q_sqrts[0]) or qs.stride(0) != q_sqrts[0].stride(0)):
-                    raise ValueError("qjob: every layer's q_mu [M, K] / q_sqrt [K, M, M] must share shape and strides")
-            klb = lib.mgp_kl_workspace_bytes(M, K) * Bt
-            if klws is None or klws.numel() < klb:
-                klws = _ws(klb, dev)
-            qjob_keep = (q_sqrts, klws)   # alive until the call below returns
-            q = (P(*[t.data_ptr() for t in q_mus]), _ld(q_mus[0]), P(*[t.data_ptr() for t in q_sqrts]),
-                 _ld(q_sqrts[0]), q_sqrts[0].stride(0), K, P(*[t.data_ptr() for t in lfrs]),
-                 min(t.numel() for t in lfrs), (ctypes.c_void_p * Bt)(*[t.data_ptr() for t in kls]),
-                 klws.data_ptr(), klws.numel())
         _lib.call("mgp_kuu_potrf_trtri_kuf", zp, ldz, M, D, vp, lp, nl, float(jitter), Bt,
                   L.data_ptr() if L is not None else None, LinvT.data_ptr(), _ld(LinvT),
                   LinvT.stride(0), info.data_ptr(), workspace.data_ptr(), workspace.numel(),
                   prep_event.cuda_event if prep_event is not None else None, bp,
                   X.data_ptr(), _ld(X), X.shape[0], P(*[t.data_ptr() for t in imgs]),
-                  min(t.numel() for t in imgs), {"x6": 0, "f16": 1}[fmt], *q, _stream())
+                  min(t.numel() for t in imgs), {"x6": 0, "f16": 1}[fmt], _stream())
     elif tfr_bound_images is not None:
         lib = _lib.load()
         bp = P(*[lib.mgp_x6_bound_ptr(t.data_ptr(), M, 0, 1) for t in tfr_bound_images])
