@@ -295,6 +295,20 @@ int mgp_trsm_stats_f16x8(const void* Tfr, size_t tfr_bytes, const void* Kfr, siz
                          mgp_stream_t stream);
 int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
                         void* Lfr, size_t lfr_bytes, mgp_stream_t stream);
+/* Both SMGP layers' tril(q_sqrt) work in three launches: the split-f16 image of
+ * tril(q_sqrt) into Lfr[b] (bit-identical to mgp_split_lower_f16) and the whitened KL
+ * (models.py:79, prior_kl) into kl_out[b] (bit-identical to mgp_gauss_kl_white) for
+ * b < batch (1 or 2), replacing the five per-layer launches of those two calls (the KL
+ * partial sums also fold the image's scale bound).  q_mu [M][ldq >= K], q_sqrt
+ * [K][M][ldqs] (stride strideq; ldqs and strideq multiples of 4, 16-B aligned; shared
+ * by the layers), Lfr at least mgp_x6_lower_bytes(M, K) bytes (lfr_bytes, 16-B aligned),
+ * workspace at least batch * mgp_qsqrt_workspace_bytes(M, K) bytes (16-B aligned).
+ * -1 .. -11: batch, q_mu, ldq, q_sqrt, ldqs, strideq, M, K, Lfr, lfr_bytes, kl_out. */
+size_t mgp_qsqrt_workspace_bytes(int64_t M, int32_t K);
+int mgp_qsqrt_images_kl_f16_batch(int32_t batch, const float* const* q_mu, int64_t ldq,
+                                  const float* const* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M,
+                                  int32_t K, void* const* Lfr, size_t lfr_bytes, double* const* kl_out,
+                                  void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 int mgp_split_cols_f16(const float* A, int64_t lda, int64_t M, int64_t N, void* Afr, size_t afr_bytes,
                        mgp_stream_t stream);
 int mgp_trsm_stats_x6_f16(const void* Tfr, size_t tfr_bytes, const void* Kfr, size_t kfr_bytes, int64_t M,

@@ -157,6 +157,9 @@ SIGNATURES = {
     "mgp_expert_conditional_f16x8": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
                                                     c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_kl_workspace_bytes": (c_size, [c_i64, c_i32]),
+    "mgp_qsqrt_workspace_bytes": (c_size, [c_i64, c_i32]),
+    "mgp_qsqrt_images_kl_f16_batch": (ctypes.c_int, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr,
+                                                     c_size, c_ptr, c_ptr, c_size, c_ptr]),
     "mgp_gauss_kl_white": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr,
                                           c_ptr, c_size, c_ptr]),
     "mgp_elbo_workspace_bytes": (c_size, [c_i64]),

@@ -19,6 +19,7 @@
 #include <math.h>
 
 #include "mgp_common.hpp"
+#include "qsqrt_jobs.hpp"
 
 namespace mgp {
 
@@ -510,53 +511,19 @@ __global__ __launch_bounds__(1024) void sum_partials_kernel(const double* __rest
 }
 
 // ------------------------------------------------------------------ K7
-constexpr int kKlRows = 16;
-
+// Block = kKlRows rows of one L_k, or (the last block) the q_mu term; the body is shared with
+// the two-layer launches of mgp_qsqrt_images_kl_f16_batch (qsqrt_jobs.hpp).
 __global__ __launch_bounds__(256) void kl_partials_kernel(const float* __restrict__ q_mu, int64_t ldq,
                                                           const float* __restrict__ q_sqrt,
                                                           int64_t ldqs, int64_t strideq, int64_t M,
                                                           int K, int nRowBlocks,
                                                           double* __restrict__ partials) {
-  // one block: kKlRows rows of one L_k; each thread owns 4 consecutive columns
-  // of every row (float4 loads of all the block's rows issued before any use:
-  // the rows were a serial chain of load latencies), masked to the lower triangle
   __shared__ double scratch[16];
   const int blk = blockIdx.x;
-  float tr = 0.f, ld = 0.f, mh = 0.f;
-  if (blk < K * nRowBlocks) {
-    const int k = blk / nRowBlocks;
-    const int64_t r0 = (int64_t)(blk % nRowBlocks) * kKlRows;
-    const float* L = q_sqrt + (int64_t)k * strideq;
-    const int64_t rmax = min<int64_t>(r0 + kKlRows, M) - 1;  // last row of the block
-    for (int64_t c0 = 4 * (int64_t)threadIdx.x; c0 <= rmax; c0 += 4 * (int64_t)blockDim.x) {
-      floatx4 v[kKlRows];
-#pragma unroll
-      for (int r = 0; r < kKlRows; ++r) {
-        const int64_t i = r0 + r;
-        v[r] = (i <= rmax && c0 <= i) ? *reinterpret_cast<const floatx4*>(L + i * ldqs + c0)
-                                      : floatx4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int r = 0; r < kKlRows; ++r) {
-        const int64_t i = r0 + r;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = (c0 + e <= i) ? v[r][e] : 0.f;
-          tr = fmaf(x, x, tr);
-          if (c0 + e == i && i <= rmax) ld += logf(x * x);
-        }
-      }
-    }
-  } else {  // the last block: Mahalanobis term sum q_mu^2
-    for (int64_t m = threadIdx.x; m < M; m += blockDim.x)
-      for (int k = 0; k < K; ++k) {
-        const float v = q_mu[m * ldq + k];
-        mh = fmaf(v, v, mh);
-      }
-  }
-  const double a = block_sum<double>((double)tr, scratch);
-  const double b = block_sum<double>((double)ld, scratch);
-  const double c = block_sum<double>((double)mh, scratch);
+  const KlPartial r = kl_partials_thread(q_mu, ldq, q_sqrt, ldqs, strideq, M, K, nRowBlocks, blk, threadIdx.x, 256);
+  const double a = block_sum<double>((double)r.tr, scratch);
+  const double b = block_sum<double>((double)r.ld, scratch);
+  const double c = block_sum<double>((double)r.mh, scratch);
   if (threadIdx.x == 0) {
     partials[3 * blk + 0] = a;
     partials[3 * blk + 1] = b;
@@ -567,12 +534,8 @@ __global__ __launch_bounds__(256) void kl_partials_kernel(const float* __restric
 __global__ __launch_bounds__(1024) void kl_final_kernel(const double* __restrict__ p, int nblk,
                                                         double MK, double* __restrict__ out) {
   __shared__ double scratch[16];
-  double tr = 0.0, ld = 0.0, mh = 0.0;
-  for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
-    tr += p[3 * i];
-    ld += p[3 * i + 1];
-    mh += p[3 * i + 2];
-  }
+  double tr, ld, mh;
+  kl_final_thread(p, nblk, threadIdx.x, blockDim.x, tr, ld, mh);
   tr = block_sum<double>(tr, scratch);
   ld = block_sum<double>(ld, scratch);
   mh = block_sum<double>(mh, scratch);

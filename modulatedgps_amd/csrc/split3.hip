@@ -44,6 +44,7 @@
 #include <type_traits>
 
 #include "mgp_common.hpp"
+#include "qsqrt_jobs.hpp"
 
 #ifndef MGP_K4_STORE_NT
 #define MGP_K4_STORE_NT 1   // K4's A-image stores non-temporal (0: plain, for A/B builds)
@@ -77,24 +78,74 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
                                                         const float* __restrict__ bound = nullptr) {
   const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= nfrag) return;
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int mk = (int)(f % nmk);
-  const int64_t kb = f / nmk;
-  const int mb = (int)(kb % nmb);
-  const int b = (int)(kb / nmb);
-  const int64_t mc = 32 * (int64_t)mb + r;
-  const float* S = src + (int64_t)b * stride;
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int64_t m = 16 * (int64_t)mk + kperm(h, j);
-    const bool keep = FULL || (LOWER ? (m >= mc) : (m <= mc));
-    v[j] = (m < M && mc < M && keep) ? S[TRANS ? mc * ld + m : m * ld + mc] : 0.f;
+  split_tri_frag<LOWER, TRANS, FULL>(src, ld, stride, M, nmb, nmk, f, threadIdx.x & 63, img, bound);
+}
+
+// ------------------------------------------------------------------ tril(q_sqrt) work of two layers
+// mgp_qsqrt_images_kl_f16_batch: the split-f16 images of tril(q_sqrt) and the whitened KL
+// terms of both SMGP layers in three launches (blockIdx.y / x = the layer) instead of five
+// per layer (bound memset, absmax, split, KL partials, KL final): the KL partial sums also
+// fold the images' scale bounds (the maxima of the lower triangles they read), the final
+// launch writes both KL terms and both bounds, the split launch follows.  Same sums in the
+// same order and the same bound as the per-layer launches: bit-identical results.
+struct QLayer {
+  const float* q_mu;
+  const float* q_sqrt;
+  bf16x8* Lfr;
+  float* bound;     // Lfr's trailer
+  double* kl_out;
+  double* part;     // [nblk][3] partial sums
+  float* bmax;      // [nblk] block maxima
+};
+
+__global__ __launch_bounds__(256) void kl_absmax2_kernel(QLayer l0, QLayer l1, int64_t ldq, int64_t ldqs,
+                                                         int64_t strideq, int64_t M, int K, int nrb) {
+  __shared__ double scratch[16];
+  __shared__ float smax[4];
+  const QLayer& l = blockIdx.y ? l1 : l0;
+  const int blk = blockIdx.x;
+  const KlPartial r = kl_partials_thread(l.q_mu, ldq, l.q_sqrt, ldqs, strideq, M, K, nrb, blk, threadIdx.x, 256);
+  const float m = wave_max_f32(r.amax);
+  if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = m;
+  const double a = block_sum<double>((double)r.tr, scratch);   // (its barriers publish smax)
+  const double b = block_sum<double>((double)r.ld, scratch);
+  const double c = block_sum<double>((double)r.mh, scratch);
+  if (threadIdx.x == 0) {
+    l.part[3 * blk + 0] = a;
+    l.part[3 * blk + 1] = b;
+    l.part[3 * blk + 2] = c;
+    l.bmax[blk] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
   }
-  if (bound)
-    store_split_f16<true>(img + f * 3 * 64 + lane, v, ldexpf(1.f, img_exp(*bound)));
-  else
-    store_split(img + f * 3 * 64 + lane, v);
+}
+
+// One 1024-thread block per layer: kl_final_kernel's sums, and the image bound.
+__global__ __launch_bounds__(1024) void kl_final2_kernel(QLayer l0, QLayer l1, int nblk, double MK) {
+  __shared__ double scratch[16];
+  __shared__ float smax[16];
+  const QLayer& l = blockIdx.x ? l1 : l0;
+  double tr, ld, mh;
+  kl_final_thread(l.part, nblk, threadIdx.x, 1024, tr, ld, mh);
+  float m = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += 1024) m = fmaxf(m, l.bmax[i]);
+  m = wave_max_f32(m);
+  if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = m;
+  tr = block_sum<double>(tr, scratch);   // (its barriers publish smax)
+  ld = block_sum<double>(ld, scratch);
+  mh = block_sum<double>(mh, scratch);
+  if (threadIdx.x == 0) {
+    *l.kl_out = 0.5 * (mh - MK - ld + tr);
+    float b = 0.f;
+    for (int i = 0; i < 16; ++i) b = fmaxf(b, smax[i]);
+    *l.bound = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void split_lower2_kernel(QLayer l0, QLayer l1, int64_t ldqs, int64_t strideq,
+                                                           int64_t M, int nmb, int nmk, int64_t nfrag) {
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= nfrag) return;
+  const QLayer& l = blockIdx.y ? l1 : l0;
+  split_tri_frag<true>(l.q_sqrt, ldqs, strideq, M, nmb, nmk, f, threadIdx.x & 63, l.Lfr, l.bound);
 }
 
 // split_tri_kernel<false> (the split-f16 L^-T images) for two matrices at src and
@@ -2430,6 +2481,65 @@ extern "C" int mgp_split_lower_f16(const float* q_sqrt, int64_t ldqs, int64_t st
   const int64_t nfrag = (int64_t)K * nmb * nmk;
   hipLaunchKernelGGL(split_tri_kernel<true>, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt, ldqs,
                      strideq, M, nmb, nmk, nfrag, (bf16x8*)Lfr, (const float*)bound);
+  return launch_status();
+}
+
+// Per layer: the KL partial sums [nblk][3] doubles, then the block maxima [nblk] floats.
+static int64_t qsqrt_nblk(int64_t M, int32_t K) { return (int64_t)K * ((M + kKlRows - 1) / kKlRows) + 1; }
+
+extern "C" size_t mgp_qsqrt_workspace_bytes(int64_t M, int32_t K) {
+  if (M <= 0 || K <= 0) return 0;
+  const int64_t n = qsqrt_nblk(M, K);
+  return (size_t)((n * 3 * 8 + n * 4 + 15) / 16 * 16);
+}
+
+extern "C" int mgp_qsqrt_images_kl_f16_batch(int32_t batch, const float* const* q_mu, int64_t ldq,
+                                             const float* const* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M,
+                                             int32_t K, void* const* Lfr, size_t lfr_bytes, double* const* kl_out,
+                                             void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  if (batch < 1 || batch > 2) return -1;
+  if (!q_mu) return -2;
+  if (ldq < K) return -3;
+  if (!q_sqrt) return -4;
+  if (ldqs < M) return -5;
+  if (K > 1 && strideq < ldqs * M) return -6;
+  if (M < 1) return -7;
+  if (K < 1) return -8;
+  if (!Lfr) return -9;
+  if (lfr_bytes < mgp_x6_lower_bytes(M, K)) return -10;
+  if (!kl_out) return -11;
+  if ((ldqs & 3) || (strideq & 3)) return MGP_ERR_ALIGN;   // the KL sums' float4 rows
+  const size_t wb = mgp_qsqrt_workspace_bytes(M, K);
+  if (!workspace || workspace_bytes < wb * (size_t)batch) return MGP_ERR_WORKSPACE;
+  if (!aligned16(workspace)) return MGP_ERR_ALIGN;
+  const int64_t nblk = qsqrt_nblk(M, K);
+  QLayer l[2];
+  for (int b = 0; b < 2; ++b) {
+    const int s = b < batch ? b : 0;
+    if (!q_mu[s]) return -2;
+    if (!q_sqrt[s]) return -4;
+    if (!Lfr[s]) return -9;
+    if (!kl_out[s]) return -11;
+    if (!aligned16(q_sqrt[s]) || !aligned16(Lfr[s])) return MGP_ERR_ALIGN;
+    char* w = (char*)workspace + wb * (size_t)s;
+    l[b] = QLayer{q_mu[s], q_sqrt[s], (bf16x8*)Lfr[s], trailer(Lfr[s], lower_planes(M, K)), kl_out[s],
+                  (double*)w, (float*)(w + nblk * 3 * 8)};
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int nrb = (int)((M + kKlRows - 1) / kKlRows);
+  hipLaunchKernelGGL(kl_absmax2_kernel, dim3((unsigned)nblk, (unsigned)batch), dim3(256), 0, st, l[0], l[1], ldq,
+                     ldqs, strideq, M, K, nrb);
+  int rc = launch_status();
+  if (rc) return rc;
+  hipLaunchKernelGGL(kl_final2_kernel, dim3((unsigned)batch), dim3(1024), 0, st, l[0], l[1], (int)nblk,
+                     (double)M * (double)K);
+  rc = launch_status();
+  if (rc) return rc;
+  const int64_t Mp = x6_mp(M);
+  const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
+  const int64_t nfrag = (int64_t)K * nmb * nmk;
+  hipLaunchKernelGGL(split_lower2_kernel, dim3((unsigned)((nfrag + 3) / 4), (unsigned)batch), dim3(256), 0, st, l[0],
+                     l[1], ldqs, strideq, M, nmb, nmk, nfrag);
   return launch_status();
 }
 

@@ -49,6 +49,9 @@ _K4_BATCHED = True
 # the training forward's colnorm_max (the C_k images' bound) on the side stream beside K3
 # (False: on the main stream right before K5; A/B probes only)
 _COLMAX_SIDE = True
+# split-f16: both layers' tril(q_sqrt) images and KL terms by mgp_qsqrt_images_kl_f16_batch
+# (False: mgp_split_lower_f16 + mgp_gauss_kl_white per layer; A/B probes only)
+_QS_BATCH = True
 
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
@@ -660,6 +663,11 @@ class SMGP(SGP):
         late = {"k1_in_k3": (), "overlap": (), "k1a_late": ("a",), "k1a_k5": ("a",), "k1_main": ("f", "a"),
                 "serial": ("f", "a")}[sched]
         if b["x6"]:
+            pf, pa = self.pred_layer, self.assign_layer
+            # split-f16: both layers' tril(q_sqrt) images and KL terms in three launches
+            # (mgp_qsqrt_images_kl_f16_batch) instead of five per layer, beside K3's chain
+            q_batch = _QS_BATCH and fmt == "f16" and pf.q_mu.shape == pa.q_mu.shape and "Lfr_f" in b
+
             def side_work():
                 for L, layer in layers:
                     X_ = layer.kernel._x(X)
@@ -668,11 +676,26 @@ class SMGP(SGP):
                             ops.rbf_kuf_x6(X_, layer.Z, layer.kernel.variance, layer.kernel.lengthscales,
                                            out=b["Kfr_" + L], fmt=fmt)
                     with _Stage(timing, "split_tri"):
-                        ops.split_lower_x6(layer.q_sqrt, out=b["Lfr_" + L], fmt=fmt)
+                        if not q_batch:
+                            ops.split_lower_x6(layer.q_sqrt, out=b["Lfr_" + L], fmt=fmt)
                         if _COLMAX_SIDE and "colmax_" + L in b:   # training: the C_k bound, off the K3 -> K5 path
                             ops.colnorm_max(layer.q_sqrt, out=b["colmax_" + L])
                     images[L] = (b["Kfr_" + L], b["Lfr_" + L])
-                if kl_out is not None:
+                if q_batch:
+                    if kl_out is not None:
+                        kls = [kl_out[0:1], kl_out[1:2]]
+                    else:   # prediction: the images are wanted, the KL values are not
+                        if "kl_scratch" not in b:
+                            b["kl_scratch"] = torch.empty(2, dtype=torch.float64, device=X.device)
+                        kls = [b["kl_scratch"][0:1], b["kl_scratch"][1:2]]
+                    if "qs_ws" not in b:
+                        M, K = pf.q_mu.shape
+                        b["qs_ws"] = torch.empty(2 * ops._lib.load().mgp_qsqrt_workspace_bytes(M, K),
+                                                 dtype=torch.uint8, device=X.device)
+                    with _Stage(timing, "split_tri"):
+                        ops.qsqrt_images_kl_f16_batch([pf.q_mu, pa.q_mu], [pf.q_sqrt, pa.q_sqrt],
+                                                      [b["Lfr_f"], b["Lfr_a"]], kls, workspace=b["qs_ws"])
+                elif kl_out is not None:
                     with _Stage(timing, "gauss_kl"):
                         self.pred_layer.prior_kl(out=kl_out[0:1])
                         self.assign_layer.prior_kl(out=kl_out[1:2])

@@ -399,6 +399,33 @@ def split_lower_x6(q_sqrt, out=None, fmt="x6"):
     return out
 
 
+def qsqrt_images_kl_f16_batch(q_mus, q_sqrts, Lfrs, kl_outs, workspace=None):
+    """Both layers' split-f16 tril(q_sqrt) images (split_lower_x6(q_sqrt, fmt="f16")) and
+    whitened KL terms (gauss_kl_white(q_mu, q_sqrt), float64 [1] each) in three launches
+    (mgp_qsqrt_images_kl_f16_batch; bit-identical).  Layers share q_mu / q_sqrt shapes."""
+    import ctypes
+    n = len(q_mus)
+    q_sqrts = [as_padded(t) for t in q_sqrts]   # float4 rows (no copy for the layers' storage)
+    M, K = q_mus[0].shape
+    for qm, qs, lf, kl in zip(q_mus, q_sqrts, Lfrs, kl_outs):
+        _check(qm, "q_mu", 2), _check(qs, "q_sqrt", 3)
+        if (tuple(qm.shape) != (M, K) or tuple(qs.shape) != (K, M, M) or _ld(qm) != _ld(q_mus[0])
+                or _ld(qs) != _ld(q_sqrts[0]) or qs.stride(0) != q_sqrts[0].stride(0)):
+            raise ValueError("every layer's q_mu [M, K] / q_sqrt [K, M, M] must share shape and strides")
+        if kl.dtype != torch.float64 or kl.numel() < 1:
+            raise ValueError("kl_out: float64 tensors of at least one element")
+    lib = _lib.load()
+    nbytes = lib.mgp_qsqrt_workspace_bytes(M, K) * n
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, q_mus[0].device)
+    P = ctypes.c_void_p * n
+    _lib.call("mgp_qsqrt_images_kl_f16_batch", n, P(*[t.data_ptr() for t in q_mus]), _ld(q_mus[0]),
+              P(*[t.data_ptr() for t in q_sqrts]), _ld(q_sqrts[0]), q_sqrts[0].stride(0), M, K,
+              P(*[t.data_ptr() for t in Lfrs]), min(t.numel() for t in Lfrs), P(*[t.data_ptr() for t in kl_outs]),
+              workspace.data_ptr(), workspace.numel(), _stream())
+    return Lfrs, kl_outs
+
+
 def split_cols_x6(A, out=None, fmt="x6"):
     """Fragment image (uint8 device tensor) of A [M, N] for the split-bf16 K5
     (fmt "f16": the split-f16 image, mgp_split_cols_f16)."""

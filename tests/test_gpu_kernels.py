@@ -420,3 +420,31 @@ def test_kuu_potrf_trtri_kuf_side_job(device, N, M, D, ard, fmt):
     for b in range(2):
         assert torch.equal(got[b], ref[b]), b
     assert torch.equal(L1, L0) and torch.equal(LinvT1, LinvT0) and torch.equal(info1, info0)
+
+
+@pytest.mark.parametrize("M,K,batch", [(1024, 8, 2), (130, 5, 2), (40, 2, 2), (300, 3, 1), (1, 1, 2)])
+def test_qsqrt_images_kl_batch_bit_identical(device, M, K, batch):
+    """mgp_qsqrt_images_kl_f16_batch: both layers' split-f16 tril(q_sqrt) images (fragments and
+    the trailer's bound) byte-identical to mgp_split_lower_f16's, KL terms equal to
+    mgp_gauss_kl_white's; q_sqrt carries garbage above the diagonal."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(M + 11 * K)
+    q_mu = [_t(0.5 * rng.standard_normal((M, K)), device) for _ in range(batch)]
+    q_sqrt = []
+    for b in range(batch):
+        q = ops.padded(M, M, device, batch=K)
+        q.copy_(_t(np.eye(M) * (0.5 + b) + 0.1 * rng.standard_normal((K, M, M)), device))
+        q_sqrt.append(q)
+    lb = ops.x6_lower_bytes(M, K)
+    ref = [ops.split_lower_x6(q_sqrt[b], fmt="f16") for b in range(batch)]
+    kl_ref = [ops.gauss_kl_white(q_mu[b], q_sqrt[b]) for b in range(batch)]
+    got = [torch.full((lb,), 7, dtype=torch.uint8, device=device) for _ in range(batch)]
+    kl = [torch.full((1,), float("nan"), dtype=torch.float64, device=device) for _ in range(batch)]
+    ops.qsqrt_images_kl_f16_batch(q_mu, q_sqrt, got, kl)
+    torch.cuda.synchronize()
+    Mp = (M + 127) // 128 * 128
+    nfb = K * (Mp // 32) * (Mp // 16) * 3 * 1024   # the fragments' bytes (the trailer's bound after them)
+    for b in range(batch):
+        assert torch.equal(got[b][:nfb], ref[b][:nfb]), b
+        assert torch.equal(got[b][lb - 256:lb - 252], ref[b][lb - 256:lb - 252]), b
+        assert torch.equal(kl[b], kl_ref[b]), (b, kl[b].item(), kl_ref[b].item())

@@ -89,3 +89,8 @@ def test_batch_entries_reject_out_of_range_batch():
     assert lib.mgp_split_upper_f16_bounded_batch(3, ctypes.c_void_p(8), 64, 4096, 64, p, 1 << 20, None) == -9
     assert lib.mgp_split_upper_f16_bounded_batch(0, ctypes.c_void_p(8), 64, 4096, 64, p, 1 << 20, None) == -9
     assert lib.mgp_split_upper_f16_bounded_batch(1, None, 64, 4096, 64, p, 1 << 20, None) == -2
+    for bad in (0, 3):
+        assert lib.mgp_qsqrt_images_kl_f16_batch(bad, p, 8, p, 64, 4096, 64, 8, p, 1 << 24, p, p, 1 << 20,
+                                                 None) == -1
+    assert lib.mgp_qsqrt_images_kl_f16_batch(2, None, 8, p, 64, 4096, 64, 8, p, 1 << 24, p, p, 1 << 20, None) == -2
+    assert lib.mgp_qsqrt_images_kl_f16_batch(2, p, 8, p, 64, 4096, 64, 8, p, 16, p, p, 1 << 20, None) == -10

@@ -19,6 +19,9 @@ def main():
     if "k4single" in sys.argv[4:]:   # one K4 launch per layer (the round-4 default before the batch)
         from modulatedgps_amd import models
         models._K4_BATCHED = False
+    if "qsper" in sys.argv[4:]:   # the tril(q_sqrt) images and KL per layer (before round 5's batch)
+        from modulatedgps_amd import models
+        models._QS_BATCH = False
     dev = torch.device("cuda", 0)
     cfg = bench.CONFIGS["c3"]
     X_np, Y_np, layers = bench.synthetic(cfg, 0, dev)
