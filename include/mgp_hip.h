@@ -457,6 +457,13 @@ size_t mgp_chol_backward_workspace_bytes(int64_t M);
 int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT, int64_t ldli, const float* gL,
                       int64_t ldg, int64_t M, float* gKuu, int64_t ldo, void* workspace,
                       size_t workspace_bytes, mgp_stream_t stream);
+/* mgp_chol_backward for both SMGP layers (batch 1 .. 8 layers of one M, shared
+ * leading dimensions) in five launches instead of eight per layer; bit-identical to
+ * batch calls of mgp_chol_backward.  Workspace: batch * mgp_chol_backward_workspace_bytes(M).
+ * -1 .. -10: batch, L, ldl, LinvT, ldli, gL, ldg, M, gKuu, ldo. */
+int mgp_chol_backward_batch(int32_t batch, const float* const* L, int64_t ldl, const float* const* LinvT,
+                            int64_t ldli, const float* const* gL, int64_t ldg, int64_t M, float* const* gKuu,
+                            int64_t ldo, void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 
 /* Reverse mode of K(Z, X) (models.py:135,139) for a cotangent gK [M][ldg]:
  * gZ [M][ldgz] (float), g_var and g_ls[n_ls] (double, device).  symmetric = 1
@@ -469,6 +476,22 @@ int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int64_t ldz, i
                      const float* gK, int64_t ldg, int32_t symmetric, int32_t accumulate, float* gZ,
                      int64_t ldgz, double* g_var, double* g_ls, void* workspace, size_t workspace_bytes,
                      mgp_stream_t stream);
+/* Both kernel cotangents of up to 8 layers (models.py:135,139; the layers share X,
+ * M, D, n_ls and the leading dimensions) in three launches instead of five per layer:
+ * per layer b the Kuf contribution (gKuf[b] [M][ldgf], over X [N][ldx]; accumulate
+ * as in mgp_rbf_backward) and then the Kuu one (gKuu[b] [M][ldgu], symmetric) added
+ * to it -- bit-identical to mgp_rbf_backward(Kuf, accumulate) followed by
+ * mgp_rbf_backward(Kuu, symmetric = 1, accumulate = 1).
+ * Workspace: batch * mgp_rbf_backward_batch_workspace_bytes(N, M, D).
+ * -1 .. -19: batch, X, ldx, N, Z, ldz, M, D, variance, lengthscales, n_ls, gKuf, ldgf,
+ * gKuu, ldgu, gZ, ldgz, g_var, g_ls. */
+size_t mgp_rbf_backward_batch_workspace_bytes(int64_t N, int64_t M, int32_t D);
+int mgp_rbf_backward_batch(int32_t batch, const float* X, int64_t ldx, int64_t N, const float* const* Z,
+                           int64_t ldz, int64_t M, int32_t D, const float* const* variance,
+                           const float* const* lengthscales, int32_t n_ls, const float* const* gKuf,
+                           int64_t ldgf, const float* const* gKuu, int64_t ldgu, int32_t accumulate,
+                           float* const* gZ, int64_t ldgz, double* const* g_var, double* const* g_ls,
+                           void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K7
  * Whitened Gaussian KL (GPflow gauss_kl(q_mu, q_sqrt, K=None), reached through
@@ -644,6 +667,14 @@ int mgp_kl_grad(const float* q_mu, int64_t ldq, const float* q_sqrt, int64_t ldq
 int mgp_adam_step(float* theta, float* u, const void* g, int32_t grad_is_double, int64_t ldg, float* m1,
                   float* m2, int64_t rows, int64_t cols, int64_t ld, float lr, float beta1, float beta2,
                   float eps, int64_t t, float grad_sign, mgp_stream_t stream);
+/* mgp_adam_step on n (1 .. 16) parameter blocks in one launch (per-block arrays of
+ * the arguments above; u[j] may be NULL; a block may be empty, its pointers unused), bit-identical to n
+ * mgp_adam_step calls.  -1 .. -11: n, theta, u, g, grad_is_double, ldg, m1, m2, rows,
+ * cols, ld (NULL array or a bad entry); -16: t. */
+int mgp_adam_step_set(int32_t n, float* const* theta, float* const* u, const void* const* g,
+                      const int32_t* grad_is_double, const int64_t* ldg, float* const* m1, float* const* m2,
+                      const int64_t* rows, const int64_t* cols, const int64_t* ld, float lr, float beta1,
+                      float beta2, float eps, int64_t t, float grad_sign, mgp_stream_t stream);
 
 #ifdef __cplusplus
 }

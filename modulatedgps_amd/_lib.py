@@ -75,10 +75,19 @@ SIGNATURES = {
     "mgp_adam_step": (ctypes.c_int, [c_ptr, c_ptr, c_ptr, c_i32, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_i64,
                                      ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, c_i64,
                                      ctypes.c_float, c_ptr]),
+    "mgp_adam_step_set": (ctypes.c_int, [c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                                         c_ptr, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                         c_i64, ctypes.c_float, c_ptr]),
     "mgp_rbf_backward_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
     "mgp_rbf_backward": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i32,
                                         c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size,
                                         c_ptr]),
+    "mgp_rbf_backward_batch_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
+    "mgp_rbf_backward_batch": (ctypes.c_int, [c_i32, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_ptr,
+                                              c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_ptr,
+                                              c_ptr, c_size, c_ptr]),
+    "mgp_chol_backward_batch": (ctypes.c_int, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr,
+                                               c_i64, c_ptr, c_size, c_ptr]),
     "mgp_chol_backward_workspace_bytes": (c_size, [c_i64]),
     "mgp_chol_backward": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr,
                                          c_size, c_ptr]),

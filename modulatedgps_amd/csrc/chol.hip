@@ -1227,12 +1227,18 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
 //   kTriUpperK: k over [max(i0, j0), M)  (op(A) upper, op(B) lower: L^T gL, Linv^T G);
 //   kTriBand: k over [j0, i0 + 64)       (A lower, B lower: P Linv);
 //   | kTriLowerOut: tiles wholly above the diagonal are not computed (their
-//     consumer reads only the lower triangle / never reaches them).
-constexpr int kTriNone = 0, kTriUpperK = 1, kTriBand = 2, kTriLowerOut = 4;
+//     consumer reads only the lower triangle / never reaches them);
+//   | kPhiOut: C = Phi(op(A) op(B)) (lower triangle, diagonal halved, zeros above).
+// blockIdx.z: the layer; A, B and C advance by zs doubles per layer.
+constexpr int kTriNone = 0, kTriUpperK = 1, kTriBand = 2, kTriLowerOut = 4, kPhiOut = 8;
 template <bool TA, bool TB, int BN = 64, int KC = 16>
 __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A, int64_t lda,
                                                     const double* __restrict__ B, int64_t ldb,
-                                                    double* __restrict__ C, int64_t ldc, int64_t M, int tri) {
+                                                    double* __restrict__ C, int64_t ldc, int64_t M, int tri,
+                                                    int64_t zs) {
+  A += blockIdx.z * zs;
+  B += blockIdx.z * zs;
+  C += blockIdx.z * zs;
   // 64 x BN tile; wave w: rows wi .. wi + 31, columns wj .. wj + BN / 2 - 1 (NB 16-wide blocks);
   // KC-deep chunks (KC / 4 MFMA k-steps per barrier pair)
   constexpr int NB = BN / 32, LA = 64 * KC / 256, LB = KC * BN / 256;  // loads per thread
@@ -1305,22 +1311,37 @@ __global__ __launch_bounds__(256) void dgemm_kernel(const double* __restrict__ A
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t i = i0 + wi + 16 * a + (lane >> 4) + 4 * r, j = j0 + wj + 16 * b + (lane & 15);
-        if (i < M && j < M) C[i * ldc + j] = acc[a][b][r];
+        const double v = acc[a][b][r];
+        if (i < M && j < M) C[i * ldc + j] = !(tri & kPhiOut) ? v : (j < i ? v : (j == i ? 0.5 * v : 0.0));
       }
 }
 
-// mode 0: dst = f64(src) (src f32);  1: dst = f64(src^T);  2: Phi (tril, diag / 2) in place on f64;
-// 3: out32 = (S + S^T) / 2 -> f32 and out64 (optional)
-__global__ __launch_bounds__(256) void chol_bwd_elem_kernel(int mode, const float* __restrict__ src32,
-                                                            int64_t lds, double* __restrict__ d, int64_t M,
-                                                            float* __restrict__ out32, int64_t ldo) {
+// The float32 operands and outputs of up to kMaxBatch layers; the float64 workspace
+// holds per layer b, at b * 4 M^2 doubles: Ld = L, Li = Linv = LinvT^T, G = gL, T.
+struct CholBwdIO {
+  const float* L[kMaxBatch]; const float* LinvT[kMaxBatch]; const float* gL[kMaxBatch]; float* gKuu[kMaxBatch];
+  int64_t ldl, ldli, ldg, ldo;
+};
+
+// grid (ceil(M^2 / 256), 3, batch): y = 0 Ld = f64(L), 1 Li = f64(LinvT^T), 2 G = f64(gL)
+__global__ __launch_bounds__(256) void chol_bwd_convert_kernel(CholBwdIO io, double* __restrict__ ws, int64_t M) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= M * M) return;
   const int64_t i = idx / M, j = idx % M;
-  if (mode == 0) d[idx] = (double)src32[i * lds + j];
-  else if (mode == 1) d[idx] = (double)src32[j * lds + i];
-  else if (mode == 2) d[idx] = (j < i) ? d[idx] : (j == i ? 0.5 * d[idx] : 0.0);
-  else out32[i * ldo + j] = (float)(0.5 * (d[i * M + j] + d[j * M + i]));
+  const int b = blockIdx.z, y = blockIdx.y;
+  double* d = ws + (int64_t)b * 4 * M * M + (int64_t)y * M * M;
+  if (y == 0) d[idx] = (double)io.L[b][i * io.ldl + j];
+  else if (y == 1) d[idx] = (double)io.LinvT[b][j * io.ldli + i];
+  else d[idx] = (double)io.gL[b][i * io.ldg + j];
+}
+
+// gKuu = (S + S^T) / 2 -> f32, S = T of layer blockIdx.y
+__global__ __launch_bounds__(256) void chol_bwd_sym_kernel(CholBwdIO io, const double* __restrict__ ws, int64_t M) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= M * M) return;
+  const int64_t i = idx / M, j = idx % M;
+  const double* T = ws + (int64_t)blockIdx.y * 4 * M * M + 3 * M * M;
+  io.gKuu[blockIdx.y][i * io.ldo + j] = (float)(0.5 * (T[i * M + j] + T[j * M + i]));
 }
 
 }  // namespace mgp
@@ -1555,6 +1576,31 @@ extern "C" size_t mgp_chol_backward_workspace_bytes(int64_t M) {
   return (size_t)(M > 0 ? M : 1) * (size_t)(M > 0 ? M : 1) * 4 * sizeof(double);
 }
 
+// both layers' Cholesky backward in five launches: the conversions, the three
+// products (blockIdx.z = layer, Phi folded into the first one's store) and the
+// symmetrisation -- the same float64 operations in the same order as per layer
+static int chol_backward_impl(const CholBwdIO& io, int batch, int64_t M, void* workspace, hipStream_t s) {
+  constexpr int KCB = 32;  // chunk depth of the products (32: half the barriers of 16)
+  double* Ld = (double*)workspace;
+  double* Li = Ld + M * M;  // Linv = LinvT^T
+  double* G = Li + M * M;
+  double* T = G + M * M;
+  const int64_t zs = 4 * M * M;
+  const unsigned ne = (unsigned)((M * M + 255) / 256);
+  const dim3 gg((unsigned)((M + 31) / 32), (unsigned)((M + 63) / 64), (unsigned)batch);  // 64 x 32 tiles: 2 x the workgroups of 64 x 64 (measured faster at M = 1024)
+  hipLaunchKernelGGL(chol_bwd_convert_kernel, dim3(ne, 3, (unsigned)batch), dim3(256), 0, s, io, Ld, M);
+  // L, gL, Linv are lower triangular (exact zeros above), so are P and P Linv: the
+  // products skip the zero terms and the tiles Phi / the next product never read
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32, KCB>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M,
+                     kTriUpperK | kTriLowerOut | kPhiOut, zs);                                          // Phi(L^T gL)
+  hipLaunchKernelGGL((dgemm_kernel<false, false, 32, KCB>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M,
+                     kTriBand | kTriLowerOut, zs);                                                    // P Linv
+  hipLaunchKernelGGL((dgemm_kernel<true, false, 32, KCB>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M,
+                     kTriUpperK, zs);                                                                 // Linv^T (.)
+  hipLaunchKernelGGL(chol_bwd_sym_kernel, dim3(ne, (unsigned)batch), dim3(256), 0, s, io, Ld, M);
+  return launch_status();
+}
+
 extern "C" int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT, int64_t ldli, const float* gL,
                                  int64_t ldg, int64_t M, float* gKuu, int64_t ldo, void* workspace,
                                  size_t workspace_bytes, mgp_stream_t stream) {
@@ -1569,25 +1615,36 @@ extern "C" int mgp_chol_backward(const float* L, int64_t ldl, const float* LinvT
   if (ldo < M) return -9;
   if (M == 0) return MGP_OK;
   if (!workspace || workspace_bytes < mgp_chol_backward_workspace_bytes(M)) return MGP_ERR_WORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
-  constexpr int KCB = 32;  // chunk depth of the products (32: half the barriers of 16)
-  double* Ld = (double*)workspace;
-  double* Li = Ld + M * M;   // Linv = LinvT^T
-  double* G = Li + M * M;
-  double* T = G + M * M;
-  const dim3 eg((unsigned)((M * M + 255) / 256)), gg((unsigned)((M + 31) / 32), (unsigned)((M + 63) / 64));  // 64 x 32 tiles: 2 x the workgroups of 64 x 64 (measured faster at M = 1024)
-  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, L, ldl, Ld, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 1, LinvT, ldli, Li, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 0, gL, ldg, G, M, nullptr, (int64_t)0);
-  // L, gL, Linv are lower triangular (exact zeros above), so are P and P Linv: the
-  // products skip the zero terms and the tiles Phi / the next product never read
-  hipLaunchKernelGGL((dgemm_kernel<true, false, 32, KCB>), gg, dim3(256), 0, s, Ld, M, G, M, T, M, M,
-                     kTriUpperK | kTriLowerOut);                                                      // L^T gL
-  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 2, nullptr, (int64_t)0, T, M, nullptr, (int64_t)0);
-  hipLaunchKernelGGL((dgemm_kernel<false, false, 32, KCB>), gg, dim3(256), 0, s, T, M, Li, M, G, M, M,
-                     kTriBand | kTriLowerOut);                                                        // P Linv
-  hipLaunchKernelGGL((dgemm_kernel<true, false, 32, KCB>), gg, dim3(256), 0, s, Li, M, G, M, T, M, M,
-                     kTriUpperK);                                                                     // Linv^T (.)
-  hipLaunchKernelGGL(chol_bwd_elem_kernel, eg, dim3(256), 0, s, 3, nullptr, (int64_t)0, T, M, gKuu, ldo);
-  return launch_status();
+  CholBwdIO io = {};
+  io.L[0] = L, io.LinvT[0] = LinvT, io.gL[0] = gL, io.gKuu[0] = gKuu;
+  io.ldl = ldl, io.ldli = ldli, io.ldg = ldg, io.ldo = ldo;
+  return chol_backward_impl(io, 1, M, workspace, (hipStream_t)stream);
+}
+
+extern "C" int mgp_chol_backward_batch(int32_t batch, const float* const* L, int64_t ldl, const float* const* LinvT,
+                                       int64_t ldli, const float* const* gL, int64_t ldg, int64_t M,
+                                       float* const* gKuu, int64_t ldo, void* workspace, size_t workspace_bytes,
+                                       mgp_stream_t stream) {
+  if (batch < 1 || batch > kMaxBatch) return -1;
+  if (!L) return -2;
+  if (ldl < M) return -3;
+  if (!LinvT) return -4;
+  if (ldli < M) return -5;
+  if (!gL) return -6;
+  if (ldg < M) return -7;
+  if (M < 0) return -8;
+  if (!gKuu) return -9;
+  if (ldo < M) return -10;
+  CholBwdIO io = {};
+  for (int b = 0; b < batch; ++b) {
+    if (!L[b]) return -2;
+    if (!LinvT[b]) return -4;
+    if (!gL[b]) return -6;
+    if (!gKuu[b]) return -9;
+    io.L[b] = L[b], io.LinvT[b] = LinvT[b], io.gL[b] = gL[b], io.gKuu[b] = gKuu[b];
+  }
+  if (M == 0) return MGP_OK;
+  if (!workspace || workspace_bytes < (size_t)batch * mgp_chol_backward_workspace_bytes(M)) return MGP_ERR_WORKSPACE;
+  io.ldl = ldl, io.ldli = ldli, io.ldg = ldg, io.ldo = ldo;
+  return chol_backward_impl(io, batch, M, workspace, (hipStream_t)stream);
 }

@@ -134,18 +134,17 @@ static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, 
 // stride -- the strided dword loads cost the address unit 8x the cycles and
 // bounded this kernel.
 constexpr int kRbfRows = 2;  // rows of Z per wave
-template <int DMAX, bool VEC = false>
-__global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restrict__ X, int64_t ldx,
-                                                           const float* __restrict__ Z, int64_t ldz, int64_t N,
-                                                           int64_t M, int D, const float* __restrict__ variance,
-                                                           const float* __restrict__ ls, int n_ls,
-                                                           const float* __restrict__ gK, int64_t ldg,
-                                                           int64_t nchunk, double* __restrict__ part) {
+// one workgroup's rows (blockIdx.x) over the points [nb, ne); part: this chunk's [M][NS]
+template <int DMAX, bool VEC>
+__device__ __forceinline__ void rbf_bwd_rows_body(const float* __restrict__ X, int64_t ldx,
+                                                  const float* __restrict__ Z, int64_t ldz, int64_t nb, int64_t ne,
+                                                  int64_t M, int D, const float* __restrict__ variance,
+                                                  const float* __restrict__ ls, int n_ls,
+                                                  const float* __restrict__ gK, int64_t ldg,
+                                                  double* __restrict__ part) {
   constexpr int NS = 1 + 2 * DMAX, R = kRbfRows;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t m0 = (int64_t)blockIdx.x * 4 * R + R * w;
-  const int64_t nb = (int64_t)blockIdx.y * nchunk;
-  const int64_t ne = (nb + nchunk < N) ? nb + nchunk : N;
   float hc2[DMAX], z[R][DMAX];
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
@@ -210,14 +209,59 @@ __global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restri
       double v = (double)acc[r][j];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0 && m0 + r < M) part[((int64_t)blockIdx.y * M + m0 + r) * NS + j] = v;
+      if (lane == 0 && m0 + r < M) part[(m0 + r) * NS + j] = v;
     }
+}
+
+template <int DMAX, bool VEC = false>
+__global__ __launch_bounds__(256) void rbf_bwd_rows_kernel(const float* __restrict__ X, int64_t ldx,
+                                                           const float* __restrict__ Z, int64_t ldz, int64_t N,
+                                                           int64_t M, int D, const float* __restrict__ variance,
+                                                           const float* __restrict__ ls, int n_ls,
+                                                           const float* __restrict__ gK, int64_t ldg,
+                                                           int64_t nchunk, double* __restrict__ part) {
+  constexpr int NS = 1 + 2 * DMAX;
+  const int64_t nb = (int64_t)blockIdx.y * nchunk;
+  const int64_t ne = (nb + nchunk < N) ? nb + nchunk : N;
+  rbf_bwd_rows_body<DMAX, VEC>(X, ldx, Z, ldz, nb, ne, M, D, variance, ls, n_ls, gK, ldg,
+                               part + (int64_t)blockIdx.y * M * NS);
+}
+
+// The layers of mgp_rbf_backward_batch: per layer the Kuf cotangent's chunks
+// (blockIdx.y < nch, over X) and the Kuu cotangent's (blockIdx.y == nch, X = Z, all
+// M points in one chunk), each into its own part slab; blockIdx.z = layer.
+constexpr int kRbfMaxBatch = 8;
+struct RbfBwdLayers {
+  const float* Z[kRbfMaxBatch]; const float* var[kRbfMaxBatch]; const float* ls[kRbfMaxBatch];
+  const float* gKuf[kRbfMaxBatch]; const float* gKuu[kRbfMaxBatch];
+  float* gZ[kRbfMaxBatch]; double* g_var[kRbfMaxBatch]; double* g_ls[kRbfMaxBatch];
+};
+template <int DMAX, bool VEC>
+__global__ __launch_bounds__(256) void rbf_bwd_rows_batch_kernel(const float* __restrict__ X, int64_t ldx,
+                                                                 int64_t N, int64_t ldz, int64_t M, int D, int n_ls,
+                                                                 RbfBwdLayers lay, int64_t ldgf, int64_t ldgu,
+                                                                 int64_t nchunk, int nch, int64_t slab,
+                                                                 double* __restrict__ ws) {
+  constexpr int NS = 1 + 2 * DMAX;
+  const int b = blockIdx.z, y = blockIdx.y;
+  double* part = ws + (int64_t)b * slab + (int64_t)y * M * NS;
+  if (y < nch) {
+    const int64_t nb = (int64_t)y * nchunk, ne = (nb + nchunk < N) ? nb + nchunk : N;
+    rbf_bwd_rows_body<DMAX, VEC>(X, ldx, lay.Z[b], ldz, nb, ne, M, D, lay.var[b], lay.ls[b], n_ls, lay.gKuf[b],
+                                 ldgf, part);
+  } else {
+    rbf_bwd_rows_body<DMAX, VEC>(lay.Z[b], ldz, lay.Z[b], ldz, 0, M, M, D, lay.var[b], lay.ls[b], n_ls,
+                                 lay.gKuu[b], ldgu, part);
+  }
 }
 
 // part[0][m][j] = sum over the chunks of part[ch][m][j] (in place: each thread
 // reads only its own (m, j) of every chunk), one thread per (m, j), fixed order.
-__global__ __launch_bounds__(256) void rbf_bwd_fold_kernel(double* __restrict__ part, int nchunks, int64_t total) {
+// blockIdx.y: the layer (part advances by slab doubles)
+__global__ __launch_bounds__(256) void rbf_bwd_fold_kernel(double* __restrict__ part, int nchunks, int64_t total,
+                                                           int64_t slab = 0) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  part += blockIdx.y * slab;
   if (idx >= total) return;
   double v = part[idx];
   for (int ch = 1; ch < nchunks; ++ch) v += part[(int64_t)ch * total + idx];
@@ -225,14 +269,12 @@ __global__ __launch_bounds__(256) void rbf_bwd_fold_kernel(double* __restrict__ 
 }
 
 template <int DMAX>
-__global__ __launch_bounds__(256) void rbf_bwd_finish_kernel(const double* __restrict__ part, int nchunks, int64_t M,
-                                                             int D, const float* __restrict__ Z, int64_t ldz,
-                                                             const float* __restrict__ variance,
-                                                             const float* __restrict__ ls, int n_ls, float zfactor,
-                                                             int accumulate, float* __restrict__ gZ, int64_t ldgz,
-                                                             double* __restrict__ g_var, double* __restrict__ g_ls) {
+__device__ __forceinline__ void rbf_bwd_finish_body(const double* __restrict__ part, int nchunks, int64_t M, int D,
+                                                    const float* __restrict__ variance, const float* __restrict__ ls,
+                                                    int n_ls, float zfactor, int accumulate, float* __restrict__ gZ,
+                                                    int64_t ldgz, double* __restrict__ g_var,
+                                                    double* __restrict__ g_ls, double* scratch) {
   constexpr int NS = 1 + 2 * DMAX;
-  __shared__ double scratch[16];
   double gl[DMAX], s0tot = 0.0;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) gl[d] = 0.0;
@@ -270,6 +312,34 @@ __global__ __launch_bounds__(256) void rbf_bwd_finish_kernel(const double* __res
     }
   }
   if (threadIdx.x == 0 && n_ls == 1) g_ls[0] = accumulate ? g_ls[0] + giso : giso;
+}
+
+template <int DMAX>
+__global__ __launch_bounds__(256) void rbf_bwd_finish_kernel(const double* __restrict__ part, int nchunks, int64_t M,
+                                                             int D, const float* __restrict__ variance,
+                                                             const float* __restrict__ ls, int n_ls, float zfactor,
+                                                             int accumulate, float* __restrict__ gZ, int64_t ldgz,
+                                                             double* __restrict__ g_var, double* __restrict__ g_ls) {
+  __shared__ double scratch[16];
+  rbf_bwd_finish_body<DMAX>(part, nchunks, M, D, variance, ls, n_ls, zfactor, accumulate, gZ, ldgz, g_var, g_ls,
+                            scratch);
+}
+
+// layer blockIdx.x: the Kuf contribution (folded slab 0; accumulate as given), then
+// the Kuu one (slab nch, symmetric) added to it -- the two finishes of the per-call path
+template <int DMAX>
+__global__ __launch_bounds__(256) void rbf_bwd_finish_batch_kernel(const double* __restrict__ ws, int64_t slab,
+                                                                   int nch, int64_t M, int D, int n_ls,
+                                                                   RbfBwdLayers lay, int accumulate, int64_t ldgz) {
+  constexpr int NS = 1 + 2 * DMAX;
+  __shared__ double scratch[16];
+  const int b = blockIdx.x;
+  const double* part = ws + (int64_t)b * slab;
+  rbf_bwd_finish_body<DMAX>(part, 1, M, D, lay.var[b], lay.ls[b], n_ls, 1.f, accumulate, lay.gZ[b], ldgz,
+                            lay.g_var[b], lay.g_ls[b], scratch);
+  __syncthreads();
+  rbf_bwd_finish_body<DMAX>(part + (int64_t)nch * M * NS, 1, M, D, lay.var[b], lay.ls[b], n_ls, 2.f, 1, lay.gZ[b],
+                            ldgz, lay.g_var[b], lay.g_ls[b], scratch);
 }
 
 }  // namespace mgp
@@ -425,7 +495,7 @@ extern "C" int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int
     if (nch > 1)                                                                                              \
       hipLaunchKernelGGL(rbf_bwd_fold_kernel, dim3((unsigned)((M * (1 + 2 * DM) + 255) / 256)), dim3(256), 0, s, \
                          part, nch, M * (1 + 2 * DM));                                                        \
-    hipLaunchKernelGGL(rbf_bwd_finish_kernel<DM>, dim3(1), dim3(256), 0, s, part, 1, M, D, Z, ldz, variance,   \
+    hipLaunchKernelGGL(rbf_bwd_finish_kernel<DM>, dim3(1), dim3(256), 0, s, part, 1, M, D, variance,           \
                        lengthscales, n_ls, zf, accumulate, gZ, ldgz, g_var, g_ls);                            \
     return launch_status();                                                                                   \
   }
@@ -436,5 +506,92 @@ extern "C" int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int
   MGP_RBF_BWD_CASE(16)
   MGP_RBF_BWD_CASE(32)
 #undef MGP_RBF_BWD_CASE
+  return MGP_ERR_UNSUPPORTED;
+}
+
+static int64_t rbf_bwd_batch_nch(int64_t N) {
+  const int64_t c = rbf_bwd_chunk(N), n = (N + c - 1) / c;
+  return n > 0 ? n : 1;
+}
+
+extern "C" size_t mgp_rbf_backward_batch_workspace_bytes(int64_t N, int64_t M, int32_t D) {
+  int dm = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16 : 32;
+  return (size_t)((rbf_bwd_batch_nch(N) + 1) * (M > 0 ? M : 1) * (1 + 2 * dm)) * sizeof(double);
+}
+
+extern "C" int mgp_rbf_backward_batch(int32_t batch, const float* X, int64_t ldx, int64_t N,
+                                      const float* const* Z, int64_t ldz, int64_t M, int32_t D,
+                                      const float* const* variance, const float* const* lengthscales, int32_t n_ls,
+                                      const float* const* gKuf, int64_t ldgf, const float* const* gKuu, int64_t ldgu,
+                                      int32_t accumulate, float* const* gZ, int64_t ldgz, double* const* g_var,
+                                      double* const* g_ls, void* workspace, size_t workspace_bytes,
+                                      mgp_stream_t stream) {
+  if (batch < 1 || batch > kRbfMaxBatch) return -1;
+  if (!X) return -2;
+  if (ldx < D) return -3;
+  if (N < 0) return -4;
+  if (!Z) return -5;
+  if (ldz < D) return -6;
+  if (M < 0) return -7;
+  if (D < 1) return -8;
+  if (D > 32) return MGP_ERR_UNSUPPORTED;
+  if (!variance) return -9;
+  if (!lengthscales) return -10;
+  if (n_ls != 1 && n_ls != D) return -11;
+  if (!gKuf) return -12;
+  if (ldgf < N) return -13;
+  if (!gKuu) return -14;
+  if (ldgu < M) return -15;
+  if (!gZ) return -16;
+  if (ldgz < D) return -17;
+  if (!g_var) return -18;
+  if (!g_ls) return -19;
+  RbfBwdLayers lay = {};
+  for (int b = 0; b < batch; ++b) {
+    if (!Z[b]) return -5;
+    if (!variance[b]) return -9;
+    if (!lengthscales[b]) return -10;
+    if (!gKuf[b]) return -12;
+    if (!gKuu[b]) return -14;
+    if (!gZ[b]) return -16;
+    if (!g_var[b]) return -18;
+    if (!g_ls[b]) return -19;
+    lay.Z[b] = Z[b], lay.var[b] = variance[b], lay.ls[b] = lengthscales[b], lay.gKuf[b] = gKuf[b];
+    lay.gKuu[b] = gKuu[b], lay.gZ[b] = gZ[b], lay.g_var[b] = g_var[b], lay.g_ls[b] = g_ls[b];
+  }
+  if (M == 0) return MGP_OK;
+  const size_t per = mgp_rbf_backward_batch_workspace_bytes(N, M, D);
+  if (!workspace || workspace_bytes < (size_t)batch * per) return MGP_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t chunk = rbf_bwd_chunk(N), slab = (int64_t)(per / sizeof(double));
+  const int nch = (int)rbf_bwd_batch_nch(N);
+  double* ws = (double*)workspace;
+  bool zvec = ldz % 4 == 0;
+  for (int b = 0; b < batch; ++b) zvec = zvec && aligned16(Z[b]);
+  const dim3 grid((unsigned)((M + 4 * kRbfRows - 1) / (4 * kRbfRows)), (unsigned)(nch + 1), (unsigned)batch);
+  // the point loads' form only (dwordx4 or dword): the same values either way
+#define MGP_RBF_BWDB_CASE(DM)                                                                                   \
+  if (D <= DM) {                                                                                                \
+    const bool vec = DM >= 4 && ldx % 4 == 0 && ldx >= DM && aligned16(X) && ldz >= DM && zvec;                  \
+    if (vec)                                                                                                    \
+      hipLaunchKernelGGL((rbf_bwd_rows_batch_kernel<DM, true>), grid, dim3(256), 0, s, X, ldx, N, ldz, M, D,      \
+                         n_ls, lay, ldgf, ldgu, chunk, nch, slab, ws);                                          \
+    else                                                                                                        \
+      hipLaunchKernelGGL((rbf_bwd_rows_batch_kernel<DM, false>), grid, dim3(256), 0, s, X, ldx, N, ldz, M, D,     \
+                         n_ls, lay, ldgf, ldgu, chunk, nch, slab, ws);                                          \
+    if (nch > 1)                                                                                                \
+      hipLaunchKernelGGL(rbf_bwd_fold_kernel, dim3((unsigned)((M * (1 + 2 * DM) + 255) / 256), (unsigned)batch),   \
+                         dim3(256), 0, s, ws, nch, M * (1 + 2 * DM), slab);                                     \
+    hipLaunchKernelGGL(rbf_bwd_finish_batch_kernel<DM>, dim3((unsigned)batch), dim3(256), 0, s, ws, slab, nch, M, \
+                       D, n_ls, lay, accumulate, ldgz);                                                         \
+    return launch_status();                                                                                     \
+  }
+  MGP_RBF_BWDB_CASE(1)
+  MGP_RBF_BWDB_CASE(2)
+  MGP_RBF_BWDB_CASE(4)
+  MGP_RBF_BWDB_CASE(8)
+  MGP_RBF_BWDB_CASE(16)
+  MGP_RBF_BWDB_CASE(32)
+#undef MGP_RBF_BWDB_CASE
   return MGP_ERR_UNSUPPORTED;
 }

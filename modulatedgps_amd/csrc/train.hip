@@ -48,6 +48,12 @@ __device__ __forceinline__ float sigmoid_f(float u) { return 1.f / (1.f + __expf
 // g: gradient of the ELBO w.r.t. theta (constrained), scaled by gsign (-1:
 // minimise -ELBO).  SOFTPLUS: u holds the unconstrained values, theta = softplus(u).
 template <typename GT, bool SOFTPLUS>
+__device__ __forceinline__ void adam_elem(float* __restrict__ theta, float* __restrict__ u,
+                                          const GT* __restrict__ g, int64_t ldg, float* __restrict__ m1,
+                                          float* __restrict__ m2, int64_t idx, int64_t cols, int64_t ld, float lr_t,
+                                          float b1, float b2, float eps, float gsign);
+
+template <typename GT, bool SOFTPLUS>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ theta, float* __restrict__ u,
                                                    const GT* __restrict__ g, int64_t ldg,
                                                    float* __restrict__ m1, float* __restrict__ m2, int64_t rows,
@@ -55,6 +61,27 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ theta, fl
                                                    float eps, float gsign) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= rows * cols) return;
+  adam_elem<GT, SOFTPLUS>(theta, u, g, ldg, m1, m2, idx, cols, ld, lr_t, b1, b2, eps, gsign);
+}
+
+// Up to kAdamMaxSet parameter blocks in one launch: workgroup blockIdx.x belongs to
+// block j with blk0[j] <= blockIdx.x < blk0[j + 1] and runs adam_kernel's element
+// update on it (the same float operations, so the same bits as one launch per block).
+constexpr int kAdamMaxSet = 16;
+struct AdamSet {
+  float* theta[kAdamMaxSet]; float* u[kAdamMaxSet]; const void* g[kAdamMaxSet];
+  float* m1[kAdamMaxSet]; float* m2[kAdamMaxSet];
+  int64_t rows[kAdamMaxSet], cols[kAdamMaxSet], ld[kAdamMaxSet], ldg[kAdamMaxSet];
+  int64_t blk0[kAdamMaxSet + 1];
+  int32_t dbl[kAdamMaxSet];
+  int32_t n;
+};
+
+template <typename GT, bool SOFTPLUS>
+__device__ __forceinline__ void adam_elem(float* __restrict__ theta, float* __restrict__ u,
+                                          const GT* __restrict__ g, int64_t ldg, float* __restrict__ m1,
+                                          float* __restrict__ m2, int64_t idx, int64_t cols, int64_t ld, float lr_t,
+                                          float b1, float b2, float eps, float gsign) {
   const int64_t r = idx / cols, c = idx % cols;
   const int64_t p = r * ld + c;
   float gr = gsign * (float)g[r * ldg + c];
@@ -70,6 +97,25 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ theta, fl
     theta[p] = softplus_f(x);
   } else {
     theta[p] = x;
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_set_kernel(AdamSet a, float lr_t, float b1, float b2, float eps,
+                                                       float gsign) {
+  int j = 0;
+  while (j + 1 < a.n && (int64_t)blockIdx.x >= a.blk0[j + 1]) ++j;
+  const int64_t idx = ((int64_t)blockIdx.x - a.blk0[j]) * 256 + threadIdx.x;
+  if (idx >= a.rows[j] * a.cols[j]) return;
+  if (a.dbl[j]) {
+    if (a.u[j]) adam_elem<double, true>(a.theta[j], a.u[j], (const double*)a.g[j], a.ldg[j], a.m1[j], a.m2[j], idx,
+                                        a.cols[j], a.ld[j], lr_t, b1, b2, eps, gsign);
+    else adam_elem<double, false>(a.theta[j], a.u[j], (const double*)a.g[j], a.ldg[j], a.m1[j], a.m2[j], idx,
+                                  a.cols[j], a.ld[j], lr_t, b1, b2, eps, gsign);
+  } else {
+    if (a.u[j]) adam_elem<float, true>(a.theta[j], a.u[j], (const float*)a.g[j], a.ldg[j], a.m1[j], a.m2[j], idx,
+                                       a.cols[j], a.ld[j], lr_t, b1, b2, eps, gsign);
+    else adam_elem<float, false>(a.theta[j], a.u[j], (const float*)a.g[j], a.ldg[j], a.m1[j], a.m2[j], idx,
+                                 a.cols[j], a.ld[j], lr_t, b1, b2, eps, gsign);
   }
 }
 
@@ -122,5 +168,48 @@ extern "C" int mgp_adam_step(float* theta, float* u, const void* g, int32_t grad
     else hipLaunchKernelGGL((adam_kernel<float, false>), grid, dim3(256), 0, s, theta, u, (const float*)g, ldg, m1,
                             m2, rows, cols, ld, (float)lr_t, beta1, beta2, eps, grad_sign);
   }
+  return launch_status();
+}
+
+extern "C" int mgp_adam_step_set(int32_t n, float* const* theta, float* const* u, const void* const* g,
+                                 const int32_t* grad_is_double, const int64_t* ldg, float* const* m1,
+                                 float* const* m2, const int64_t* rows, const int64_t* cols, const int64_t* ld,
+                                 float lr, float beta1, float beta2, float eps, int64_t t, float grad_sign,
+                                 mgp_stream_t stream) {
+  if (n < 1 || n > kAdamMaxSet) return -1;
+  if (!theta) return -2;
+  if (!u) return -3;
+  if (!g) return -4;
+  if (!grad_is_double) return -5;
+  if (!ldg) return -6;
+  if (!m1) return -7;
+  if (!m2) return -8;
+  if (!rows) return -9;
+  if (!cols) return -10;
+  if (!ld) return -11;
+  if (t < 1) return -16;
+  AdamSet a = {};
+  a.n = n;
+  int64_t blk = 0;
+  for (int j = 0; j < n; ++j) {
+    if (rows[j] < 0) return -9;
+    if (cols[j] < 0) return -10;
+    if (ld[j] < cols[j]) return -11;
+    if (rows[j] * cols[j] > 0) {   // an empty block's pointers are not used (torch: NULL)
+      if (!theta[j]) return -2;
+      if (!g[j]) return -4;
+      if (!m1[j]) return -7;
+      if (!m2[j]) return -8;
+    }
+    a.theta[j] = theta[j], a.u[j] = u[j], a.g[j] = g[j], a.m1[j] = m1[j], a.m2[j] = m2[j];
+    a.rows[j] = rows[j], a.cols[j] = cols[j], a.ld[j] = ld[j], a.ldg[j] = ldg[j], a.dbl[j] = grad_is_double[j];
+    a.blk0[j] = blk;
+    blk += (rows[j] * cols[j] + 255) / 256;
+  }
+  a.blk0[n] = blk;
+  if (blk == 0) return MGP_OK;
+  const double lr_t = (double)lr * sqrt(1.0 - pow((double)beta2, (double)t)) / (1.0 - pow((double)beta1, (double)t));
+  hipLaunchKernelGGL(adam_set_kernel, dim3((unsigned)blk), dim3(256), 0, (hipStream_t)stream, a, (float)lr_t, beta1,
+                     beta2, eps, grad_sign);
   return launch_status();
 }

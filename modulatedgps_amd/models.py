@@ -52,6 +52,7 @@ _COLMAX_SIDE = True
 # split-f16: both layers' tril(q_sqrt) images and KL terms by mgp_qsqrt_images_kl_f16_batch
 # (False: mgp_split_lower_f16 + mgp_gauss_kl_white per layer; A/B probes only)
 _QS_BATCH = True
+_TAIL_BATCH = True   # both layers' Cholesky / RBF backward in one batch each (elbo_and_grad)
 
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
@@ -919,6 +920,13 @@ class SMGP(SGP):
             v = values[name].to(device=t.device, dtype=torch.float32).reshape(t.shape)
             t.copy_(torch.nn.functional.softplus(v.double()).float() if kind == "positive" else v)
 
+    def _tail_batchable(self):
+        """Both layers' Cholesky / RBF backward can share launches: same M, D and
+        lengthscale count (mgp_chol_backward_batch, mgp_rbf_backward_batch)."""
+        f, a = self.pred_layer, self.assign_layer
+        return (f.Z.shape == a.Z.shape and f.kernel.lengthscales.numel() == a.kernel.lengthscales.numel()
+                and f.Z.stride() == a.Z.stride())
+
     def elbo_and_grad(self, X, Y, noise=None, seed=None, n_offset=0, n_total=None, process_group=None,
                       timing=None, unconstrained=False):
         """ELBO (0-d float32) and its gradient w.r.t. every constrained parameter of
@@ -981,6 +989,22 @@ class SMGP(SGP):
             return {name + ".Z": gZ, name + ".variance": gvar, name + ".lengthscales": gls,
                     name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]}
 
+        def tail_backward_batch(order, gs):
+            with _Stage(timing, "chol_bwd"):
+                gKuus = ops.chol_backward_batch([b["L_" + L] for L, *_ in order], [b["LinvT_" + L] for L, *_ in order],
+                                                [g["g_Lm"] for g in gs])
+            with _Stage(timing, "rbf_bwd"):
+                layers = [layer for _, _, layer, _ in order]
+                gZs = [torch.zeros_like(layer.Z) for layer in layers]
+                glss = [torch.zeros(layer.kernel.lengthscales.numel(), dtype=torch.float64, device=self.device)
+                        for layer in layers]
+                ops.rbf_backward_batch(X, [layer.Z for layer in layers], [layer.kernel.variance for layer in layers],
+                                       [layer.kernel.lengthscales for layer in layers], [g["g_Kuf"] for g in gs],
+                                       gKuus, gZs, [g["g_var"] for g in gs], glss, accumulate=True)
+            return [{name + ".Z": gZ, name + ".variance": g["g_var"], name + ".lengthscales": gls,
+                     name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]}
+                    for (_, name, _, _), g, gZ, gls in zip(order, gs, gZs, glss)]
+
         pending = []
 
         def reduce_bucket(layer_grads):
@@ -996,11 +1020,19 @@ class SMGP(SGP):
 
         # the two layers in order on this stream (a side stream for one layer's Cholesky /
         # RBF backward beside the other's conditional backward measured slower: the
-        # matrix-core kernel starves the small ones, DESIGN.md round-4 results)
-        for L, name, layer, gi in (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2)):
-            layer_grads = tail_backward(L, name, layer, cond_backward(L, layer, gi, b["ws_cbwd"]))
-            reduce_bucket(layer_grads)
-            grads.update(layer_grads)
+        # matrix-core kernel starves the small ones, DESIGN.md round-4 results); with
+        # matching shapes both layers' Cholesky and RBF backward run as one batch each
+        order = (("f", "pred", self.pred_layer, 0), ("a", "assign", self.assign_layer, 2))
+        if _TAIL_BATCH and self._tail_batchable():
+            gs = [cond_backward(L, layer, gi, b["ws_cbwd"]) for L, _, layer, gi in order]
+            for layer_grads in tail_backward_batch(order, gs):
+                reduce_bucket(layer_grads)
+                grads.update(layer_grads)
+        else:
+            for L, name, layer, gi in order:
+                layer_grads = tail_backward(L, name, layer, cond_backward(L, layer, gi, b["ws_cbwd"]))
+                reduce_bucket(layer_grads)
+                grads.update(layer_grads)
         if process_group is not None:
             with _Stage(timing, "allreduce"):
                 for pb in pending:

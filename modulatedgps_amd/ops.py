@@ -580,6 +580,66 @@ def rbf_backward(X, Z, variance, lengthscales, gK, symmetric=False, accumulate=F
     return gZ, g_var, g_ls
 
 
+def _same_ld(ts, what):
+    if any(_ld(t) != _ld(ts[0]) for t in ts):
+        raise ValueError(f"every layer's {what} must share its leading dimension")
+    return _ld(ts[0])
+
+
+def rbf_backward_batch(X, Zs, variances, lengthscales, gKufs, gKuus, gZs, g_vars, g_lss, accumulate=True,
+                       workspace=None):
+    """Per layer b: rbf_backward(X, Z[b], .., gKuf[b], accumulate) then
+    rbf_backward(Z[b], Z[b], .., gKuu[b], symmetric=True, accumulate=True) into
+    gZ[b], g_var[b], g_ls[b], for all layers in three launches (mgp_rbf_backward_batch;
+    bit-identical)."""
+    import ctypes
+    _check(X, "X", 2)
+    N, D = X.shape
+    n = len(Zs)
+    M = Zs[0].shape[0]
+    n_ls = lengthscales[0].numel()
+    for z, gf, gu in zip(Zs, gKufs, gKuus):
+        _check(z, "Z", 2), _check(gf, "gKuf", 2), _check(gu, "gKuu", 2)
+        if tuple(z.shape) != (M, D):
+            raise ValueError("every layer's Z must be [M, D]")
+    if any(t.numel() != n_ls for t in lengthscales):
+        raise ValueError("every layer's lengthscales must have the same size")
+    lib = _lib.load()
+    nbytes = lib.mgp_rbf_backward_batch_workspace_bytes(N, M, D) * n
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, X.device)
+    P = ctypes.c_void_p * n
+    ptrs = lambda ts: P(*[t.data_ptr() for t in ts])
+    _lib.call("mgp_rbf_backward_batch", n, X.data_ptr(), _ld(X), N, ptrs(Zs), _same_ld(Zs, "Z"), M, D,
+              ptrs(variances), ptrs(lengthscales), n_ls, ptrs(gKufs), _same_ld(gKufs, "gKuf"), ptrs(gKuus),
+              _same_ld(gKuus, "gKuu"), int(accumulate), ptrs(gZs), _same_ld(gZs, "gZ"), ptrs(g_vars), ptrs(g_lss),
+              workspace.data_ptr(), workspace.numel(), _stream())
+    return gZs, g_vars, g_lss
+
+
+def chol_backward_batch(Ls, LinvTs, gLs, outs=None, workspace=None):
+    """chol_backward for every layer (same M) in five launches (mgp_chol_backward_batch;
+    bit-identical): list of gKuu [M, M]."""
+    import ctypes
+    n = len(Ls)
+    M = Ls[0].shape[0]
+    for t in list(Ls) + list(LinvTs) + list(gLs):
+        _check(t, "L / LinvT / gL", 2)
+        if tuple(t.shape) != (M, M):
+            raise ValueError("every layer's L, LinvT and gL must be [M, M]")
+    if outs is None:
+        outs = [padded(M, M, Ls[0].device) for _ in range(n)]
+    nbytes = _lib.load().mgp_chol_backward_workspace_bytes(M) * n
+    if workspace is None or workspace.numel() < nbytes:
+        workspace = _ws(nbytes, Ls[0].device)
+    P = ctypes.c_void_p * n
+    ptrs = lambda ts: P(*[t.data_ptr() for t in ts])
+    _lib.call("mgp_chol_backward_batch", n, ptrs(Ls), _same_ld(Ls, "L"), ptrs(LinvTs), _same_ld(LinvTs, "LinvT"),
+              ptrs(gLs), _same_ld(gLs, "gL"), M, ptrs(outs), _same_ld(outs, "gKuu"), workspace.data_ptr(),
+              workspace.numel(), _stream())
+    return outs
+
+
 def chol_backward(L, LinvT, gL, out=None, workspace=None):
     """gKuu [M, M] (float32, symmetric) from the gradient w.r.t. Lm = chol(Kuu)."""
     _check(L, "L", 2), _check(LinvT, "LinvT", 2), _check(gL, "gL", 2)
@@ -611,6 +671,40 @@ def adam_step(theta, grad, m1, m2, t, lr, u=None, beta1=0.9, beta2=0.999, eps=1e
     _lib.call("mgp_adam_step", theta.data_ptr(), u.data_ptr() if u is not None else None, grad.data_ptr(),
               int(grad.dtype == torch.float64), _ld(grad), m1.data_ptr(), m2.data_ptr(), rows, cols, _ld(theta),
               float(lr), float(beta1), float(beta2), float(eps), int(t), float(grad_sign), _stream())
+
+
+class AdamSet:
+    """adam_step over a fixed list of parameter blocks in one launch (mgp_adam_step_set;
+    bit-identical to one adam_step per block).  blocks: (theta 2-D view, m1, m2, u or
+    None); the pointer arrays of the fixed state are built once."""
+
+    def __init__(self, blocks):
+        import ctypes
+        n = len(blocks)
+        if not 1 <= n <= 16:
+            raise ValueError("AdamSet takes 1 .. 16 parameter blocks")
+        P, I64 = ctypes.c_void_p * n, ctypes.c_int64 * n
+        self.n = n
+        self.shapes = [tuple(th.shape) for th, *_ in blocks]
+        self.theta = P(*[th.data_ptr() for th, *_ in blocks])
+        self.u = P(*[(u.data_ptr() if u is not None else None) for *_, u in blocks])
+        self.m1 = P(*[m1.data_ptr() for _, m1, _, _ in blocks])
+        self.m2 = P(*[m2.data_ptr() for _, _, m2, _ in blocks])
+        self.rows = I64(*[s[0] for s in self.shapes])
+        self.cols = I64(*[s[1] for s in self.shapes])
+        self.ld = I64(*[_ld(th) for th, *_ in blocks])
+        self._keep = blocks
+        self._P, self._I64, self._I32 = P, I64, ctypes.c_int32 * n
+
+    def step(self, grads, t, lr, beta1=0.9, beta2=0.999, eps=1e-7, grad_sign=-1.0):
+        """grads: one 2-D gradient per block, in order (float32 or float64)."""
+        for gr, s in zip(grads, self.shapes):
+            if gr.shape[-1] != s[1]:
+                raise ValueError("gradient / parameter shape mismatch")
+        _lib.call("mgp_adam_step_set", self.n, self.theta, self.u, self._P(*[gr.data_ptr() for gr in grads]),
+                  self._I32(*[int(gr.dtype == torch.float64) for gr in grads]), self._I64(*[_ld(gr) for gr in grads]),
+                  self.m1, self.m2, self.rows, self.cols, self.ld, float(lr), float(beta1), float(beta2), float(eps),
+                  int(t), float(grad_sign), _stream())
 
 
 def gram(X, Y, N=None, alpha=1.0, tri=False, out=None, workspace=None):

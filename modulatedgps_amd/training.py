@@ -1,6 +1,7 @@
 """Optimiser of the training step: TF 2.10 Keras-legacy Adam on the unconstrained
 variables (utils/training_utils.py:6,10), one HIP kernel
-launch per parameter block (csrc/train.hip).
+launch for all parameter blocks (mgp_adam_step_set, csrc/train.hip; one launch per
+block when there are more than 16).
 
 Positive parameters (GPflow positive() = softplus) keep an unconstrained shadow
 u = softplus^-1(theta) on the device; Adam updates u and the kernel refreshes
@@ -11,6 +12,8 @@ packed FillTriangular vector, since Adam is elementwise)."""
 import torch
 
 from . import ops
+
+_ADAM_SET = True   # False: one mgp_adam_step launch per block (A/B probes only)
 
 
 def _as2d(t):
@@ -42,6 +45,13 @@ class AdamTF:
     def step(self, grads):
         """Apply one step from the ELBO gradients (dict name -> tensor)."""
         self.t += 1
+        if _ADAM_SET and len(self.params) <= 16:
+            if getattr(self, "_set", None) is None:
+                self._set = ops.AdamSet([(_as2d(theta), self.state[name]["m1"], self.state[name]["m2"],
+                                          self.state[name]["u"]) for name, theta, _ in self.params])
+            self._set.step([_as2d(grads[name]) for name, _, _ in self.params], self.t, self.lr, beta1=self.beta1,
+                           beta2=self.beta2, eps=self.eps, grad_sign=-1.0)
+            return
         for name, theta, kind in self.params:
             st = self.state[name]
             ops.adam_step(_as2d(theta), _as2d(grads[name]), st["m1"], st["m2"], self.t, self.lr, u=st["u"],

@@ -198,6 +198,74 @@ def test_chol_backward(device, M, D, ls):
     assert normwise(to_np(g), ref) < 1e-4
 
 
+@pytest.mark.parametrize("M,batch", [(64, 2), (200, 2), (1024, 2), (1024, 1), (33, 3)])
+def test_chol_backward_batch_bit_identical(device, M, batch):
+    """mgp_chol_backward_batch (conversions, three products with Phi folded into the
+    first one's store, symmetrisation; blockIdx.z = layer) equals mgp_chol_backward
+    per layer bit for bit."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(M + batch)
+    Ls, LinvTs, gLs = [], [], []
+    for b in range(batch):
+        Z = torch.as_tensor(rng.standard_normal((M, 3)).astype(np.float32), device=device)
+        L, LinvT, _ = ops.kuu_potrf_trtri([Z], [torch.tensor([0.7 + 0.1 * b], device=device)],
+                                          [torch.tensor([1.1], device=device)], 1e-6, want_L=True)
+        gL = ops.padded(M, M, device)
+        gL.copy_(torch.as_tensor(np.tril(rng.standard_normal((M, M))).astype(np.float32)))
+        Ls.append(L[0]), LinvTs.append(LinvT[0]), gLs.append(gL)
+    ref = [ops.chol_backward(Ls[b], LinvTs[b], gLs[b]) for b in range(batch)]
+    outs = [ops.padded(M, M, device) for _ in range(batch)]
+    for o in outs:
+        o.fill_(float("nan"))
+    got = ops.chol_backward_batch(Ls, LinvTs, gLs, outs=outs)
+    torch.cuda.synchronize()
+    for b in range(batch):
+        assert torch.equal(got[b], ref[b]), b
+
+
+@pytest.mark.parametrize("N,M,D,ard,ldx,batch", [(65536, 1024, 8, False, 0, 2), (5000, 200, 3, True, 0, 2),
+                                                  (3001, 64, 16, True, 0, 2), (2500, 80, 5, True, 8, 2),
+                                                  (300, 96, 4, False, 0, 1), (100, 130, 1, False, 0, 3)])
+def test_rbf_backward_batch_bit_identical(device, N, M, D, ard, ldx, batch):
+    """mgp_rbf_backward_batch equals, per layer, mgp_rbf_backward on the Kuf cotangent
+    (accumulating onto prior values) followed by the symmetric Kuu one, bit for bit."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(N + M + D)
+    dev = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=device)
+    X = rng.standard_normal((N, D))
+    Xd = dev(X)
+    if ldx:
+        Xd = torch.full((N, ldx), 7.0, device=device)
+        Xd[:, :D] = dev(X)
+        Xd = Xd[:, :D]
+    nls = D if ard else 1
+    Zs = [dev(rng.standard_normal((M, D))) for _ in range(batch)]
+    var = [dev([0.6 + 0.2 * b]) for b in range(batch)]
+    ls = [dev(np.linspace(0.7, 1.3, nls) + 0.1 * b) for b in range(batch)]
+    gKuf = [ops.as_padded(dev(rng.standard_normal((M, N)))) for _ in range(batch)]
+    gKuu = []
+    for _ in range(batch):
+        g = rng.standard_normal((M, M))
+        gKuu.append(ops.as_padded(dev(0.5 * (g + g.T))))
+    init_Z = [dev(rng.standard_normal((M, D))) for _ in range(batch)]
+    init_v = [torch.tensor([0.25 * b - 0.3], dtype=torch.float64, device=device) for b in range(batch)]
+    init_l = [torch.as_tensor(rng.standard_normal(nls), dtype=torch.float64, device=device) for _ in range(batch)]
+    ref = []
+    for b in range(batch):
+        gZ, gv, gl = init_Z[b].clone(), init_v[b].clone(), init_l[b].clone()
+        ops.rbf_backward(Xd, Zs[b], var[b], ls[b], gKuf[b], accumulate=True, gZ=gZ, g_var=gv, g_ls=gl)
+        ops.rbf_backward(Zs[b], Zs[b], var[b], ls[b], gKuu[b], symmetric=True, accumulate=True, gZ=gZ, g_var=gv,
+                         g_ls=gl)
+        ref.append((gZ, gv, gl))
+    gZs, gvs, gls = [t.clone() for t in init_Z], [t.clone() for t in init_v], [t.clone() for t in init_l]
+    ops.rbf_backward_batch(Xd, Zs, var, ls, gKuf, gKuu, gZs, gvs, gls, accumulate=True)
+    torch.cuda.synchronize()
+    for b in range(batch):
+        assert torch.equal(gZs[b], ref[b][0]), b
+        assert torch.equal(gvs[b], ref[b][1]), b
+        assert torch.equal(gls[b], ref[b][2]), b
+
+
 @pytest.mark.parametrize("N,M,D,ard,sym,ldx", [(3000, 64, 2, False, False, 0), (5000, 200, 3, True, False, 0),
                                                 (200, 200, 3, True, True, 0), (1024, 1024, 8, False, True, 0),
                                                 (4000, 96, 4, True, False, 0), (3001, 64, 16, True, False, 0),

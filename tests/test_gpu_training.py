@@ -161,6 +161,45 @@ def test_adam_step(device):
         assert np.all(to_np(buf[:, cols:]) == 0)
 
 
+def test_adam_step_set_bit_identical(device):
+    """mgp_adam_step_set (one launch over every block) equals one mgp_adam_step per
+    block bit for bit: free and positive blocks, float and double gradients, padded
+    rows, an empty block and a 1 x 1 block, three steps."""
+    from modulatedgps_amd import ops
+    rng = np.random.default_rng(5)
+    shapes = [(37, 5, 8, False, False), (1, 1, 1, True, True), (0, 3, 4, False, False), (1024, 8, 8, False, False),
+              (3, 1024, 1028, True, False), (2, 7, 7, True, True), (513, 257, 260, False, False)]
+
+    def make():
+        r = np.random.default_rng(9)
+        blocks = []
+        for rows, cols, ld, pos, _ in shapes:
+            buf = torch.zeros(rows, ld, dtype=torch.float32, device=device)
+            th = buf[:, :cols]
+            th.copy_(torch.as_tensor(r.uniform(0.2, 2.0, (rows, cols)), dtype=torch.float32))
+            u = (torch.log(torch.expm1(th.double())).float().contiguous() if pos else None)
+            blocks.append((th, torch.zeros(rows, cols, device=device), torch.zeros(rows, cols, device=device), u))
+        return blocks
+
+    ref, got = make(), make()
+    aset = ops.AdamSet(got)
+    for t in (1, 2, 3):
+        grads = []
+        for rows, cols, ld, pos, dbl in shapes:
+            g = torch.empty(rows, cols, device=device, dtype=torch.float64 if dbl else torch.float32)
+            g.copy_(torch.as_tensor(rng.standard_normal((rows, cols))))
+            grads.append(g)
+        for (th, m1, m2, u), g in zip(ref, grads):
+            if th.numel():   # (mgp_adam_step takes no NULL pointers, an empty tensor's)
+                ops.adam_step(th, g, m1, m2, t, 0.01, u=u)
+        aset.step(grads, t, 0.01)
+    torch.cuda.synchronize()
+    for j, (a, b) in enumerate(zip(ref, got)):
+        for x, y in zip(a, b):
+            if x is not None:
+                assert torch.equal(x, y), j
+
+
 def test_run_adam_improves_elbo(device):
     """utils.training_utils.run_adam drop-in: same signature / return value; the ELBO
     rises over a short run on the c1-shaped problem (minibatches of 250)."""

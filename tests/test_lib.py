@@ -94,3 +94,54 @@ def test_batch_entries_reject_out_of_range_batch():
                                                  None) == -1
     assert lib.mgp_qsqrt_images_kl_f16_batch(2, None, 8, p, 64, 4096, 64, 8, p, 1 << 24, p, p, 1 << 20, None) == -2
     assert lib.mgp_qsqrt_images_kl_f16_batch(2, p, 8, p, 64, 4096, 64, 8, p, 16, p, p, 1 << 20, None) == -10
+
+
+def test_tail_backward_batch_entries_check_arguments():
+    """mgp_chol_backward_batch / mgp_rbf_backward_batch: batch in [1, 8], per-layer NULL
+    pointers and sizes rejected with the codes documented in mgp_hip.h, a short
+    workspace with MGP_ERR_WORKSPACE -- all before any HIP call."""
+    lib = _lib.load()
+    c = ctypes.c_void_p(8)
+    p = (ctypes.c_void_p * 2)(8, 8)
+    z = (ctypes.c_void_p * 2)(8, None)
+    for bad in (0, 9):
+        assert lib.mgp_chol_backward_batch(bad, p, 64, p, 64, p, 64, 64, p, 64, c, 1 << 30, None) == -1
+        assert lib.mgp_rbf_backward_batch(bad, c, 8, 100, p, 8, 64, 8, p, p, 1, p, 100, p, 64, 1, p, 8, p, p,
+                                          c, 1 << 30, None) == -1
+    assert lib.mgp_chol_backward_batch(2, z, 64, p, 64, p, 64, 64, p, 64, c, 1 << 30, None) == -2
+    assert lib.mgp_chol_backward_batch(2, p, 64, p, 64, z, 64, 64, p, 64, c, 1 << 30, None) == -6
+    assert lib.mgp_chol_backward_batch(2, p, 64, p, 64, p, 64, -1, p, 64, c, 1 << 30, None) == -8
+    assert lib.mgp_chol_backward_batch(2, p, 64, p, 64, p, 64, 64, p, 32, c, 1 << 30, None) == -10
+    ws = lib.mgp_chol_backward_workspace_bytes(64)
+    assert lib.mgp_chol_backward_batch(2, p, 64, p, 64, p, 64, 64, p, 64, c, 2 * ws - 1, None) == 1
+    args = lambda **kw: [kw.get(k, v) for k, v in (
+        ("batch", 2), ("X", c), ("ldx", 8), ("N", 100), ("Z", p), ("ldz", 8), ("M", 64), ("D", 8), ("var", p),
+        ("ls", p), ("n_ls", 1), ("gKuf", p), ("ldgf", 100), ("gKuu", p), ("ldgu", 64), ("acc", 1), ("gZ", p),
+        ("ldgz", 8), ("g_var", p), ("g_ls", p), ("ws", c), ("wsb", 1 << 30), ("s", None))]
+    assert lib.mgp_rbf_backward_batch(*args(X=None)) == -2
+    assert lib.mgp_rbf_backward_batch(*args(D=33, ldx=64, ldz=64, ldgz=64)) == 3
+    assert lib.mgp_rbf_backward_batch(*args(n_ls=3)) == -11
+    assert lib.mgp_rbf_backward_batch(*args(gKuu=z)) == -14
+    assert lib.mgp_rbf_backward_batch(*args(g_ls=z)) == -19
+    wb = lib.mgp_rbf_backward_batch_workspace_bytes(100, 64, 8)
+    assert lib.mgp_rbf_backward_batch(*args(wsb=2 * wb - 1)) == 1
+
+
+def test_adam_step_set_checks_arguments():
+    """mgp_adam_step_set: n in [1, 16], NULL arrays / entries and bad sizes rejected
+    with the codes of mgp_hip.h before any HIP call; all-empty blocks are a no-op."""
+    lib = _lib.load()
+    P, I64, I32 = ctypes.c_void_p * 2, ctypes.c_int64 * 2, ctypes.c_int32 * 2
+    p, z = P(8, 8), P(8, None)
+    one, i32 = I64(4, 4), I32(0, 1)
+    call = lambda n=2, theta=p, u=p, g=p, m1=p, rows=one, cols=one, ld=one, t=1: lib.mgp_adam_step_set(
+        n, theta, u, g, i32, one, m1, p, rows, cols, ld, 1e-3, 0.9, 0.999, 1e-7, t, -1.0, None)
+    assert call(n=0) == -1 and call(n=17) == -1
+    assert call(theta=z) == -2
+    assert call(theta=z, rows=I64(0, 0)) == 0   # an empty block's pointers are not used
+    assert call(g=z) == -4
+    assert call(m1=z) == -7
+    assert call(rows=I64(4, -1)) == -9
+    assert call(ld=I64(4, 3)) == -11
+    assert call(t=0) == -16
+    assert call(rows=I64(0, 0)) == 0   # nothing to update: no launch

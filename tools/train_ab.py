@@ -22,6 +22,12 @@ def main():
     if "k4single" in sys.argv[4:]:   # one K4 launch per layer (the round-4 default before the batch)
         from modulatedgps_amd import models
         models._K4_BATCHED = False
+    if "tailper" in sys.argv[4:]:   # Cholesky / RBF backward per layer (before round 5's batch)
+        from modulatedgps_amd import models
+        models._TAIL_BATCH = False
+    if "adamper" in sys.argv[4:]:   # one Adam launch per parameter block (before round 5's set)
+        from modulatedgps_amd import training
+        training._ADAM_SET = False
     dev = torch.device("cuda", 0)
     cfg = bench.CONFIGS["c3"]
     X_np, Y_np, layers = bench.synthetic(cfg, 0, dev)
