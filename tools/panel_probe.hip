@@ -1,8 +1,11 @@
 // K3 panel-sweep probe: cycles of one 64 x 16 panel factorisation (wave 0 of a
 // 64-thread workgroup) for variants of the sweep, stamped with sched-barrier
 // fenced s_memtime.  Build and run on the GPU box:
-//   hipcc -O3 --offload-arch=gfx950 -I include -I modulatedgps_amd/csrc -o tools/panel_probe tools/panel_probe.hip
+//   hipcc -O3 --offload-arch=gfx950 -I include -I modulatedgps_amd/csrc -o tools/panel_probe tools/panel_probe.hip \
+//     -Lmodulatedgps_amd -lmgp_hip -Wl,-rpath,'$ORIGIN/../modulatedgps_amd'
 //   tools/panel_probe
+#include <cstring>
+
 #include "../modulatedgps_amd/csrc/chol.hip"
 
 namespace probe {
@@ -325,6 +328,103 @@ __device__ void dpp_sweep(double* sF, double* col, int r, int& bad) {
   for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
 }
 
+// V13: the kernel's numerics (rsq + two Newton steps, t = a rs^2) with the column
+// broadcasts through LDS, one column ahead: right after column c's first FMA makes
+// a[c + 1] final, every lane stores it and reads rows c + 2 .. 15 back (uniform
+// addresses: LDS broadcasts), consumed after column c + 1's pivot chain; the
+// pivot check deferred.  VEC: the reads as 16-B pairs.
+template <bool VEC>
+__device__ void lds_rsq(double* sF, double* col, double* sb, int r, int& bad) {
+  double a[16], rs[16], pv[16], vcur[16], vnext[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  int zb;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zb));
+  double* sbz = sb + zb;
+  sbz[r] = a[0];
+#pragma unroll
+  for (int s2 = 1; s2 < 16; ++s2) vcur[s2] = sbz[s2];
+  pv[0] = read_lane_f64(a[0], 0);
+  rs[0] = rsqrt_f64(pv[0]);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double t = a[c] * (rs[c] * rs[c]);
+    if (c + 1 < 16) {
+      a[c + 1] = fma(-t, vcur[c + 1], a[c + 1]);
+      if (c + 2 < 16) {
+        double* buf = sbz + ((c + 1) & 1) * CB;
+        buf[r] = a[c + 1];
+        if (VEC) {
+          const int s0 = (c + 2) & ~1;
+#pragma unroll
+          for (int s2 = s0; s2 < 16; s2 += 2) {
+            const double2 v2 = *reinterpret_cast<const double2*>(buf + s2);
+            vnext[s2] = v2.x;
+            vnext[s2 + 1] = v2.y;
+          }
+        } else {
+#pragma unroll
+          for (int s2 = c + 2; s2 < 16; ++s2) vnext[s2] = buf[s2];
+        }
+      }
+      pv[c + 1] = read_lane_f64(a[c + 1], c + 1);
+      rs[c + 1] = rsqrt_f64(pv[c + 1]);
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, vcur[s2], a[s2]);
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) vcur[s2] = vnext[s2];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) if (!(pv[c] > 0.0) && bad == 0) bad = c + 1;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+  if (r == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) col[c] = rs[c];
+  }
+}
+
+// V15: as V13 with the broadcasts by ds_bpermute (two per value, no LDS storage)
+__device__ __forceinline__ double bperm_f64(double v, int lane) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * lane, (int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * lane, (int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ void bperm_rsq(double* sF, double* col, int r, int& bad) {
+  double a[16], rs[16], pv[16], vcur[16], vnext[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+#pragma unroll
+  for (int s2 = 1; s2 < 16; ++s2) vcur[s2] = bperm_f64(a[0], s2);
+  pv[0] = read_lane_f64(a[0], 0);
+  rs[0] = rsqrt_f64(pv[0]);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double t = a[c] * (rs[c] * rs[c]);
+    if (c + 1 < 16) {
+      a[c + 1] = fma(-t, vcur[c + 1], a[c + 1]);
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) vnext[s2] = bperm_f64(a[c + 1], s2);
+      pv[c + 1] = read_lane_f64(a[c + 1], c + 1);
+      rs[c + 1] = rsqrt_f64(pv[c + 1]);
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, vcur[s2], a[s2]);
+#pragma unroll
+      for (int s2 = c + 2; s2 < 16; ++s2) vcur[s2] = vnext[s2];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) if (!(pv[c] > 0.0) && bad == 0) bad = c + 1;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+  if (r == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) col[c] = rs[c];
+  }
+}
+
 __global__ void run(const double* src, double* dst, unsigned long long* t, int variant) {
   __shared__ double sF[CB * LDT], col[3 * CB];
   const int r = threadIdx.x;
@@ -344,6 +444,9 @@ __global__ void run(const double* src, double* dst, unsigned long long* t, int v
   else if (variant == 11) dpp_sweep(sF, col, r, bad);
   else if (variant == 12) panel_factor<0>(sF, col, r, bad);
   else if (variant == 9) rl_mode<1>(sF, col, r, bad);
+  else if (variant == 13) lds_rsq<false>(sF, col, col + CB, r, bad);
+  else if (variant == 14) lds_rsq<true>(sF, col, col + CB, r, bad);
+  else if (variant == 15) bperm_rsq(sF, col, r, bad);
   else rl_mode<2>(sF, col, r, bad);
   unsigned long long t1 = stamp();
   if (r == 0) t[variant] = t1 - t0;
@@ -361,24 +464,31 @@ int main() {
   (void)hipMalloc(&src, sizeof(h));
   (void)hipMalloc(&dst, sizeof(h));
   (void)hipMalloc(&t, 16 * sizeof(unsigned long long));
+  constexpr int NV = 16;
   (void)hipMemcpy(src, h, sizeof(h), hipMemcpyHostToDevice);
   unsigned long long ht[16] = {0};
-  const char* names[13] = {"panel_factor (LDS broadcast, rcp chain)", "readlane sweep (kernel)", "chain only",
-                          "trailing updates only", "readlane + rcp chain", "pipelined, pinned", "pipelined", "rsq1 chain", "readlane, rsq f64 + 1 Newton", "readlane, rsq f32 + 2 Newton", "readlane, rsq f32 + 1 Newton", "DPP row_newbcast + row copies", "panel_factor<0> (kernel)"};
+  const char* names[NV] = {"panel_factor (LDS broadcast, rcp chain)", "readlane sweep (kernel)", "chain only",
+                          "trailing updates only", "readlane + rcp chain", "pipelined, pinned", "pipelined", "rsq1 chain", "readlane, rsq f64 + 1 Newton", "readlane, rsq f32 + 2 Newton", "readlane, rsq f32 + 1 Newton", "DPP row_newbcast + row copies", "panel_factor<0> (kernel)",
+                          "LDS column broadcast, kernel chain", "LDS column broadcast (16-B pairs)", "ds_bpermute broadcast, kernel chain"};
   for (int rep = 0; rep < 3; ++rep)
-    for (int v = 0; v < 13; ++v) hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
+    for (int v = 0; v < NV; ++v) hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
   (void)hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
   // agreement of the variants' L panels
-  double ref[64 * 64], out[64 * 64];
-  for (int v = 0; v < 13; ++v) {
+  double ref[64 * 64], out[64 * 64], ref1[64 * 64];
+  for (int v = 0; v < NV; ++v) {
     if (v == 2 || v == 3) continue;
     hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
     (void)hipMemcpy(v == 0 ? ref : out, dst, sizeof(ref), hipMemcpyDeviceToHost);
     if (v == 0) continue;
-    double e = 0;
-    for (int i = 0; i < 64; ++i) for (int j = 0; j < 16; ++j) e = fmax(e, fabs(out[i * 64 + j] - ref[i * 64 + j]));
-    printf("variant %d max |diff| vs 0: %.3e\n", v, e);
+    if (v == 1) memcpy(ref1, out, sizeof(ref1));
+    double e = 0, e1 = 0;
+    for (int i = 0; i < 64; ++i)
+      for (int j = 0; j < 16; ++j) {
+        e = fmax(e, fabs(out[i * 64 + j] - ref[i * 64 + j]));
+        e1 = fmax(e1, fabs(out[i * 64 + j] - ref1[i * 64 + j]));
+      }
+    printf("variant %d max |diff| vs 0: %.3e, vs 1 (the kernel's numerics): %.3e\n", v, e, e1);
   }
-  for (int v = 0; v < 13; ++v) printf("%-42s %6llu cycles (%.0f per column)\n", names[v], ht[v], ht[v] / 16.0);
+  for (int v = 0; v < NV; ++v) printf("%-42s %6llu cycles (%.0f per column)\n", names[v], ht[v], ht[v] / 16.0);
   return 0;
 }
