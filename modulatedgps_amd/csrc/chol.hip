@@ -533,9 +533,12 @@ __device__ __forceinline__ void sub_outer_blk(double* __restrict__ s, int R0, in
 // rsq + two Newton steps (1/piv = rs^2, no second reciprocal chain) and one
 // multiply before the next column's FMA; the remaining FMAs of column c overlap
 // the next pivot's chain.  Writes L's panel (zeros above the diagonal) and
-// col[16P + c] = 1 / L[16P + c][16P + c].
+// col[16P + c] = 1 / L[16P + c][16P + c].  No pivot check in the sweep (each
+// check is a VALU compare feeding scalar selects, 0.7 K cycles per panel,
+// r05z_panel_probe.log): a non-positive (or NaN) pivot leaves a NaN or zero L
+// diagonal, which factor_diag_tile's check_pivots finds after the last panel.
 template <int P>
-__device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __restrict__ col, int r, int& bad) {
+__device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __restrict__ col, int r) {
   constexpr int C0 = 16 * P;
   double a[16];
 #pragma unroll
@@ -544,7 +547,6 @@ __device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __
   // software pipeline: column c's pivot chain is issued before column c - 1's
   // remaining FMAs (only a[c] had to be updated first)
   double piv = read_lane_f64(a[0], C0);
-  if (!(piv > 0.0) && bad == 0) bad = C0 + 1;
   rs[0] = rsqrt_f64(piv);
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
@@ -555,7 +557,6 @@ __device__ __forceinline__ void panel_factor(double* __restrict__ sF, double* __
     if (c + 1 < 16) {
       a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
       piv = read_lane_f64(a[c + 1], C0 + c + 1);
-      if (!(piv > 0.0) && bad == 0) bad = C0 + c + 2;
       rs[c + 1] = rsqrt_f64(piv);
     }
 #pragma unroll
@@ -673,10 +674,9 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
   // active = false: the caller's idle waves take part in every barrier and do no work
   // (w = 4 matches no role), so the barrier sequence is the same for all waves
   const int w = active ? (ctid() >> 6) : 4, lane = ctid() & 63;
-  int bad = 0;
   const int js = (int)(gcol0 / CB) - 1;
   if (w == 0) {
-    panel_factor<0>(sF, col, lane, bad);
+    panel_factor<0>(sF, col, lane);
   } else if (w < 4 && sPend) {  // blocks (1,1), (2,1) | (3,1), (2,2) | (3,2), (3,3)
     const int bi0 = (w == 1) ? 1 : 3, bj0 = (w == 3) ? 2 : 1;
     const int bi1 = (w == 3) ? 3 : 2, bj1 = (w == 1) ? 1 : (w == 2 ? 2 : 3);
@@ -697,7 +697,7 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
   __syncthreads();
   STAMP(js, 9);
   if (w == 0) {
-    panel_factor<1>(sF, col, lane, bad);
+    panel_factor<1>(sF, col, lane);
   } else if (w == 1) {
     inv_diag_block(sF, sX, col, 0, lane);
   } else if (w == 2) {
@@ -711,7 +711,7 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
   if (w < 2) sub_outer_blk<1>(sF, 32 + 16 * w, 32, sF + 16, sF + 16);  // update 1 of (2,2), (3,2)
   __syncthreads();
   STAMP(js, 11);
-  if (w == 0) panel_factor<2>(sF, col, lane, bad);
+  if (w == 0) panel_factor<2>(sF, col, lane);
   else if (w == 1) inv_diag_block(sF, sX, col, 1, lane);
   else if (w == 2) sub_outer_blk<1>(sF, 48, 48, sF + 16, sF + 16);  // update 1 of (3,3)
   STAMP(js, 12);
@@ -728,8 +728,7 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
   };
   const doublex4 zero4 = {0.0, 0.0, 0.0, 0.0};
   if (w == 0) {
-    panel_factor<3>(sF, col, lane, bad);
-    if (bad && lane == 0) atomicCAS(info, 0, (int32_t)(gcol0 + bad));
+    panel_factor<3>(sF, col, lane);
   } else if (w == 1) {
     inv_diag_block(sF, sX, col, 2, lane);
     inv_offdiag_block(sF, sX, 2, 1, lane);
@@ -779,6 +778,13 @@ __device__ __forceinline__ void factor_diag_tile(double* __restrict__ sF, double
     blk_store(S_(3, 0), zero4);
     blk_mma<false>(y, L_(3, 2), X_(2, 0), 1.0);
     blk_store(X_(3, 0), neg_x_times(X_(3, 3), y, lane));
+  } else if (w == 3) {
+    // pivot check (LAPACK info: the first column, 1-based, + gcol0): pivot c is
+    // positive iff L_cc = piv * rsq(piv) is (NaN for a negative or NaN pivot, 0 * inf
+    // for a zero one; an infinite pivot is reported too)
+    const double d = sF[lane * LDT + lane];
+    const unsigned long long nonpos = __ballot(!(d > 0.0));
+    if (nonpos && lane == 0) atomicCAS(info, 0, (int32_t)(gcol0 + __ffsll(nonpos)));
   }
   __syncthreads();
 }

@@ -425,6 +425,76 @@ __device__ void bperm_rsq(double* sF, double* col, int r, int& bad) {
   }
 }
 
+// V16: panel_factor<0> with the pivot check after the sweep (pv[] kept)
+__device__ void pf_deferred(double* __restrict__ sF, double* __restrict__ col, int r, int& bad) {
+  double a[16], rs[16], pv[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  pv[0] = read_lane_f64(a[0], 0);
+  rs[0] = rsqrt_f64(pv[0]);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    double v[16];
+#pragma unroll
+    for (int s2 = c + 1; s2 < 16; ++s2) v[s2] = read_lane_f64(a[c], s2);
+    const double t = a[c] * (rs[c] * rs[c]);
+    if (c + 1 < 16) {
+      a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+      pv[c + 1] = read_lane_f64(a[c + 1], c + 1);
+      rs[c + 1] = rsqrt_f64(pv[c + 1]);
+    }
+#pragma unroll
+    for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) if (!(pv[c] > 0.0) && bad == 0) bad = c + 1;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+  if (r == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) col[c] = rs[c];
+  }
+}
+
+// V17: the bare readlane sweep plus the col[] writes of rs (no pivot check)
+// V18: the same plus a lane-wise pivot check: lane c keeps its own pivot (a cndmask pair
+// per column, no VALU -> SALU round trip in the sweep), one compare and ballot after it
+template <bool CHECK>
+__device__ void rl_col(double* __restrict__ sF, double* __restrict__ col, int r, int& bad) {
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  double rs[16];
+  double piv = read_lane_f64(a[0], 0);
+  double mine = a[0];   // lane c: the pivot of column c (lane 0's is a[0] now)
+  rs[0] = rsqrt_f64(piv);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    double v[16];
+#pragma unroll
+    for (int s2 = c + 1; s2 < 16; ++s2) v[s2] = read_lane_f64(a[c], s2);
+    const double t = a[c] * (rs[c] * rs[c]);
+    if (c + 1 < 16) {
+      a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+      if (CHECK) mine = (r == c + 1) ? a[c + 1] : mine;
+      piv = read_lane_f64(a[c + 1], c + 1);
+      rs[c + 1] = rsqrt_f64(piv);
+    }
+#pragma unroll
+    for (int s2 = c + 2; s2 < 16; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+  if (r == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) col[c] = rs[c];
+  }
+  if (CHECK) {
+    const unsigned long long nonpos = __ballot(r < 16 && !(mine > 0.0));
+    if (nonpos && bad == 0) bad = __ffsll(nonpos);   // 1-based column of the first
+  }
+}
+
 __global__ void run(const double* src, double* dst, unsigned long long* t, int variant) {
   __shared__ double sF[CB * LDT], col[3 * CB];
   const int r = threadIdx.x;
@@ -442,11 +512,14 @@ __global__ void run(const double* src, double* dst, unsigned long long* t, int v
   else if (variant == 7) rs1<false>(sF, col, r, bad);
   else if (variant == 8) rl_mode<0>(sF, col, r, bad);
   else if (variant == 11) dpp_sweep(sF, col, r, bad);
-  else if (variant == 12) panel_factor<0>(sF, col, r, bad);
+  else if (variant == 12) panel_factor<0>(sF, col, r);
   else if (variant == 9) rl_mode<1>(sF, col, r, bad);
   else if (variant == 13) lds_rsq<false>(sF, col, col + CB, r, bad);
   else if (variant == 14) lds_rsq<true>(sF, col, col + CB, r, bad);
   else if (variant == 15) bperm_rsq(sF, col, r, bad);
+  else if (variant == 16) pf_deferred(sF, col, r, bad);
+  else if (variant == 17) rl_col<false>(sF, col, r, bad);
+  else if (variant == 18) rl_col<true>(sF, col, r, bad);
   else rl_mode<2>(sF, col, r, bad);
   unsigned long long t1 = stamp();
   if (r == 0) t[variant] = t1 - t0;
@@ -463,13 +536,15 @@ int main() {
   unsigned long long* t;
   (void)hipMalloc(&src, sizeof(h));
   (void)hipMalloc(&dst, sizeof(h));
-  (void)hipMalloc(&t, 16 * sizeof(unsigned long long));
-  constexpr int NV = 16;
+  (void)hipMalloc(&t, 32 * sizeof(unsigned long long));
+  constexpr int NV = 19;
   (void)hipMemcpy(src, h, sizeof(h), hipMemcpyHostToDevice);
-  unsigned long long ht[16] = {0};
+  unsigned long long ht[32] = {0};
   const char* names[NV] = {"panel_factor (LDS broadcast, rcp chain)", "readlane sweep (kernel)", "chain only",
                           "trailing updates only", "readlane + rcp chain", "pipelined, pinned", "pipelined", "rsq1 chain", "readlane, rsq f64 + 1 Newton", "readlane, rsq f32 + 2 Newton", "readlane, rsq f32 + 1 Newton", "DPP row_newbcast + row copies", "panel_factor<0> (kernel)",
-                          "LDS column broadcast, kernel chain", "LDS column broadcast (16-B pairs)", "ds_bpermute broadcast, kernel chain"};
+                          "LDS column broadcast, kernel chain", "LDS column broadcast (16-B pairs)", "ds_bpermute broadcast, kernel chain",
+                          "panel_factor, pivot check after the sweep", "readlane sweep + col writes",
+                          "col writes + lane-wise pivot check"};
   for (int rep = 0; rep < 3; ++rep)
     for (int v = 0; v < NV; ++v) hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
   (void)hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
