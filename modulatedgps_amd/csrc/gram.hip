@@ -469,12 +469,21 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
 // fragments and Y's chunk are loaded once per chunk and Y is weighted and split
 // per entry (half the L2 -> CU traffic and a third less split work than one
 // entry per workgroup on gram_x6_kernel).  768 threads: consumer waves 0-7
-// (entry e = w / 4, 64 x 64 of the tile each, two per SIMD), producer waves 8-11.
+// (entry e = w / 4, 64 x 64 of the tile each, two per SIMD), producer waves 8-15
+// (kRows2PW; 8-11 with 4).
 // Chunks of 32 n, double-buffered, one barrier each.
+#ifndef MGP_ROWS2_PW
+#define MGP_ROWS2_PW 8
+#endif
+constexpr int kRows2PW = MGP_ROWS2_PW;
 constexpr int kXG2 = 2176;  // LDS bytes per (32-row block, k-step) group: 2 planes x 1 KiB + 128 B pad
 
-template <bool TRI>
-__global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restrict__ Ximg, int64_t nns, int64_t MI,
+// PW: producer waves (4: 768 threads; 8, the default: 1024 threads, each producer
+// thread taking half the row groups and image units of a chunk, 118 VGPRs, four
+// waves per SIMD -- the P_k gram 2.06 -> 1.92 ms in the training step,
+// profiles/r05zd_rows2_pw8_train_ab.log)
+template <bool TRI, int PW = 4>
+__global__ __launch_bounds__(512 + 64 * PW, 1) void gram_rows2_kernel(const char* __restrict__ Ximg, int64_t nns, int64_t MI,
                                                             const float* __restrict__ Y, int64_t ldy, int64_t MJ,
                                                            const float* __restrict__ W, int64_t sw, int64_t N,
                                                            int64_t nper, int nbj, int tiles, int pairs, int batch,
@@ -528,8 +537,9 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
   // (lane / 2) % 8, cg = 2 (lane / 16) + lane % 2 (gram_x6_kernel's lane pattern).
   // X: 16-B image units u = pt + 256 s of the chunk's 8 blocks (row block u / 256,
   // k-step (u / 128) % 2) -> LDS group u / 128, byte (u % 128) 16.
-  const int pt = tid - 512, pw = pt >> 6;
-  const int rr = 8 * pw + ((lane >> 1) & 7), cg = 2 * (lane >> 4) + (lane & 1);
+  constexpr int QN = 16 / PW;   // row groups of Y (and 16-B X units) per producer thread per chunk
+  const int pt = tid - 512, pw = pt >> 6, ph = pw >> 2;
+  const int rr = 8 * (pw & 3) + ((lane >> 1) & 7), cg = 2 * (lane >> 4) + (lane & 1);
   const int soff = (cg >> 2) * kXG2 + (rr + 32 * ((cg >> 1) & 1)) * 16 + (cg & 1) * 8;
   const int64_t rows_x = MI - i0 < kGT ? MI - i0 : kGT, rows_y = MJ - j0 < kGT ? MJ - j0 : kGT;
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
@@ -542,15 +552,15 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
   const __amdgpu_buffer_rsrc_t rW1 = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(W + (two ? b0 + 1 : b0) * sw), (short)0, (int)(uint32_t)(N * 4), 0x00020000);
   const uint32_t vy = (uint32_t)(rr * ldy + 4 * cg) * 4u, qy = (uint32_t)(32 * ldy * 4);
-  uint32_t vxi[4];
-  int dxi[4];
+  uint32_t vxi[QN];
+  int dxi[QN];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int u = pt + 256 * s, g = u >> 7;
+  for (int s = 0; s < QN; ++s) {
+    const int u = (pt & 255) + 256 * (s + QN * ph), g = u >> 7;
     vxi[s] = (uint32_t)(((g >> 1) * nns + (g & 1)) * 2048 + (u & 127) * 16);
     dxi[s] = g * kXG2 + (u & 127) * 16;
   }
-  struct Regs { u32x4v x[4]; floatx4 y[4], w0, w1; };
+  struct Regs { u32x4v x[QN]; floatx4 y[QN], w0, w1; };
   Regs ra, rb;
   // loads are unconditional (past the data the resources read zeros or unused
   // bytes): every path issues the same count, so the wait counts stay tight
@@ -558,10 +568,11 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
     const int64_t n0 = nb + c * kXC;
     const uint32_t so = (uint32_t)(n0 * 4), xso = (uint32_t)(n0 / 16 * 2048);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) r.x[s] = __builtin_amdgcn_raw_buffer_load_b128(rX, vxi[s], xso, 0);
+    for (int s = 0; s < QN; ++s) r.x[s] = __builtin_amdgcn_raw_buffer_load_b128(rX, vxi[s], xso, 0);
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
-      r.y[qq] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rY, vy + qq * qy, so, 0));
+    for (int qi = 0; qi < QN; ++qi)
+      r.y[qi] = __builtin_bit_cast(floatx4,
+                                   __builtin_amdgcn_raw_buffer_load_b128(rY, vy + (qi + QN * ph) * qy, so, 0));
     r.w0 = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rW0, 16u * cg, so, 0));
     r.w1 = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rW1, 16u * cg, so, 0));
   };
@@ -572,13 +583,14 @@ __global__ __launch_bounds__(768, 1) void gram_rows2_kernel(const char* __restri
 #pragma unroll
     for (int e2 = 0; e2 < 4; ++e2)
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) r.y[qq][e2] = e2 < lim ? r.y[qq][e2] : 0.f;
+      for (int qi = 0; qi < QN; ++qi) r.y[qi][e2] = e2 < lim ? r.y[qi][e2] : 0.f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) *reinterpret_cast<u32x4v*>(sX[buf] + dxi[s]) = r.x[s];
+    for (int s = 0; s < QN; ++s) *reinterpret_cast<u32x4v*>(sX[buf] + dxi[s]) = r.x[s];
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      stash4h(sY[buf][0] + 2 * qq * kXG2 + soff, r.y[qq] * r.w0, ys);
-      stash4h(sY[buf][1] + 2 * qq * kXG2 + soff, r.y[qq] * r.w1, ys);
+    for (int qi = 0; qi < QN; ++qi) {
+      const int qq = qi + QN * ph;
+      stash4h(sY[buf][0] + 2 * qq * kXG2 + soff, r.y[qi] * r.w0, ys);
+      stash4h(sY[buf][1] + 2 * qq * kXG2 + soff, r.y[qi] * r.w1, ys);
     }
   };
 
@@ -1041,15 +1053,15 @@ extern "C" int mgp_gram_f16_rows(const void* ximg, size_t ximg_bytes, int64_t MI
   nper = (nper + kXC - 1) / kXC * kXC;
   float* ws = (float*)workspace;
   const int64_t bstride = MI * MJ, zstride = (int64_t)batch * MI * MJ;
-  const dim3 grid((unsigned)(tiles * pairs * nsplit));
+  const dim3 grid((unsigned)(tiles * pairs * nsplit)), block(512 + 64 * kRows2PW);
   if (mode != 0)
-    hipLaunchKernelGGL(gram_rows2_kernel<true>, grid, dim3(768), 0, s, (const char*)ximg, nns, MI, Y, ldy, MJ, W, sw,
-                       N, nper, nbj, tiles, pairs, (int)batch, nsplit, ws, bstride, zstride, x_bound, y_bound,
+    hipLaunchKernelGGL((gram_rows2_kernel<true, kRows2PW>), grid, block, 0, s, (const char*)ximg, nns, MI, Y, ldy, MJ,
+                       W, sw, N, nper, nbj, tiles, pairs, (int)batch, nsplit, ws, bstride, zstride, x_bound, y_bound,
                        w_bound);
   else
-    hipLaunchKernelGGL(gram_rows2_kernel<false>, grid, dim3(768), 0, s, (const char*)ximg, nns, MI, Y, ldy, MJ, W, sw,
-                       N, nper, nbj, tiles, pairs, (int)batch, nsplit, ws, bstride, zstride, x_bound, y_bound,
-                       w_bound);
+    hipLaunchKernelGGL((gram_rows2_kernel<false, kRows2PW>), grid, block, 0, s, (const char*)ximg, nns, MI, Y, ldy,
+                       MJ, W, sw, N, nper, nbj, tiles, pairs, (int)batch, nsplit, ws, bstride, zstride, x_bound,
+                       y_bound, w_bound);
   int st = launch_status();
   if (st) return st;
   hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((MJ + 31) / 32), (unsigned)((MI + 31) / 32), (unsigned)batch),
