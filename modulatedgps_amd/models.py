@@ -873,11 +873,12 @@ class SMGP(SGP):
                 dist.all_reduce(b["data_sum"], op=dist.ReduceOp.SUM, group=process_group)
         n_batch = n_total if n_total is not None else N
         num_data = self.num_data if self.num_data is not None else n_batch
-        ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"],
-                         out64=b["elbo64"])
-        # a fresh tensor per call (the reference returns a new value each time); the
-        # buffers are reused by the next evaluation
-        return (b["elbo64"] if return64 else b["elbo"]).clone()
+        # a fresh tensor per call (the reference returns a new value each time), written
+        # by the combine kernel itself (no copy launch behind it)
+        e32 = torch.empty((), dtype=torch.float32, device=self.device)
+        e64 = torch.empty((), dtype=torch.float64, device=self.device)
+        ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=e32, out64=e64)
+        return e64 if return64 else e32
 
     # ------------------------------------------------------------------ training
     def trainable_parameters(self):
@@ -1040,12 +1041,13 @@ class SMGP(SGP):
         num_data = self.num_data if self.num_data is not None else n_batch
         for name, layer in (("pred", self.pred_layer), ("assign", self.assign_layer)):
             ops.kl_grad(layer.q_mu, layer.q_sqrt, num_data, grads[name + ".q_mu"], grads[name + ".q_sqrt"])
-        ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=b["elbo"], out64=b["elbo64"])
+        e32 = torch.empty((), dtype=torch.float32, device=self.device)   # fresh per call, no copy launch
+        ops.elbo_combine(b["data_sum"], kl[0:1], kl[1:2], n_batch, num_data, out=e32, out64=b["elbo64"])
         if unconstrained:   # d/du = d/dtheta * softplus'(u) = d/dtheta * (1 - exp(-theta)) for positive ones
             for name, t, kind in self.trainable_parameters():
                 if kind == "positive":
                     grads[name] = grads[name] * (-torch.expm1(-t.double())).float()
-        return b["elbo"].clone(), grads
+        return e32, grads
 
     def training_loss_closure(self, data_iter, compile=True):
         """GPflow ExternalDataTrainingLossMixin.training_loss_closure: () -> -ELBO on the next batch."""
