@@ -478,13 +478,15 @@ int mgp_rbf_backward(const float* X, int64_t ldx, const float* Z, int64_t ldz, i
                      mgp_stream_t stream);
 /* Both kernel cotangents of up to 8 layers (models.py:135,139; the layers share X,
  * M, D, n_ls and the leading dimensions) in three launches instead of five per layer:
- * per layer b the Kuf contribution (gKuf[b] [M][ldgf], over X [N][ldx]; accumulate
- * as in mgp_rbf_backward) and then the Kuu one (gKuu[b] [M][ldgu], symmetric) added
- * to it -- bit-identical to mgp_rbf_backward(Kuf, accumulate) followed by
- * mgp_rbf_backward(Kuu, symmetric = 1, accumulate = 1).
+ * per layer b the Kuf contribution (gKuf[b] [M][ldgf], over X [N][ldx]) and then the
+ * Kuu one (gKuu[b] [M][ldgu], symmetric) added to it -- bit-identical to
+ * mgp_rbf_backward(Kuf, accumulate) followed by mgp_rbf_backward(Kuu, symmetric = 1,
+ * accumulate = 1).  accumulate: 0 the Kuf contribution overwrites gZ, g_var and g_ls,
+ * 1 it adds to them, 2 it overwrites gZ and g_ls and adds to g_var (the training
+ * step: g_var carries the conditional's part; no zero fills of gZ / g_ls needed).
  * Workspace: batch * mgp_rbf_backward_batch_workspace_bytes(N, M, D).
- * -1 .. -19: batch, X, ldx, N, Z, ldz, M, D, variance, lengthscales, n_ls, gKuf, ldgf,
- * gKuu, ldgu, gZ, ldgz, g_var, g_ls. */
+ * -1 .. -20: batch, X, ldx, N, Z, ldz, M, D, variance, lengthscales, n_ls, gKuf, ldgf,
+ * gKuu, ldgu, gZ, ldgz, g_var, g_ls, accumulate. */
 size_t mgp_rbf_backward_batch_workspace_bytes(int64_t N, int64_t M, int32_t D);
 int mgp_rbf_backward_batch(int32_t batch, const float* X, int64_t ldx, int64_t N, const float* const* Z,
                            int64_t ldz, int64_t M, int32_t D, const float* const* variance,

@@ -273,7 +273,7 @@ __device__ __forceinline__ void rbf_bwd_finish_body(const double* __restrict__ p
                                                     const float* __restrict__ variance, const float* __restrict__ ls,
                                                     int n_ls, float zfactor, int accumulate, float* __restrict__ gZ,
                                                     int64_t ldgz, double* __restrict__ g_var,
-                                                    double* __restrict__ g_ls, double* scratch) {
+                                                    double* __restrict__ g_ls, double* scratch, int acc_var) {
   constexpr int NS = 1 + 2 * DMAX;
   double gl[DMAX], s0tot = 0.0;
 #pragma unroll
@@ -299,7 +299,7 @@ __device__ __forceinline__ void rbf_bwd_finish_body(const double* __restrict__ p
   }
   const double var = (double)variance[0];
   const double gv = block_sum<double>(s0tot, scratch) / var;
-  if (threadIdx.x == 0) *g_var = accumulate ? *g_var + gv : gv;
+  if (threadIdx.x == 0) *g_var = acc_var ? *g_var + gv : gv;
   double giso = 0.0;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void rbf_bwd_finish_kernel(const double* __res
                                                              double* __restrict__ g_var, double* __restrict__ g_ls) {
   __shared__ double scratch[16];
   rbf_bwd_finish_body<DMAX>(part, nchunks, M, D, variance, ls, n_ls, zfactor, accumulate, gZ, ldgz, g_var, g_ls,
-                            scratch);
+                            scratch, accumulate);
 }
 
 // layer blockIdx.x: the Kuf contribution (folded slab 0; accumulate as given), then
@@ -335,11 +335,11 @@ __global__ __launch_bounds__(256) void rbf_bwd_finish_batch_kernel(const double*
   __shared__ double scratch[16];
   const int b = blockIdx.x;
   const double* part = ws + (int64_t)b * slab;
-  rbf_bwd_finish_body<DMAX>(part, 1, M, D, lay.var[b], lay.ls[b], n_ls, 1.f, accumulate, lay.gZ[b], ldgz,
-                            lay.g_var[b], lay.g_ls[b], scratch);
+  rbf_bwd_finish_body<DMAX>(part, 1, M, D, lay.var[b], lay.ls[b], n_ls, 1.f, accumulate & 1, lay.gZ[b], ldgz,
+                            lay.g_var[b], lay.g_ls[b], scratch, accumulate != 0);
   __syncthreads();
   rbf_bwd_finish_body<DMAX>(part + (int64_t)nch * M * NS, 1, M, D, lay.var[b], lay.ls[b], n_ls, 2.f, 1, lay.gZ[b],
-                            ldgz, lay.g_var[b], lay.g_ls[b], scratch);
+                            ldgz, lay.g_var[b], lay.g_ls[b], scratch, 1);
 }
 
 }  // namespace mgp
@@ -546,6 +546,7 @@ extern "C" int mgp_rbf_backward_batch(int32_t batch, const float* X, int64_t ldx
   if (ldgz < D) return -17;
   if (!g_var) return -18;
   if (!g_ls) return -19;
+  if (accumulate < 0 || accumulate > 2) return -20;
   RbfBwdLayers lay = {};
   for (int b = 0; b < batch; ++b) {
     if (!Z[b]) return -5;

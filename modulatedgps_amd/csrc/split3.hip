@@ -2848,10 +2848,20 @@ __global__ __launch_bounds__(256) void row_sums_kernel(const float* __restrict__
   if (threadIdx.x == 0) part[blockIdx.x * kRowSumChunks + blockIdx.y] = v;
 }
 
-__global__ void sum_parts_kernel(const double* __restrict__ part, int rows, double* __restrict__ out) {
-  double v = 0.0;
-  for (int k = 0; k < rows; ++k) v += part[k];
-  *out = v;
+// out = sum of part[0 .. rows) in index order (one wave stages the partials in LDS,
+// lane 0 adds them: the single-thread loop over global memory took 16 us)
+constexpr int kSumPartsMax = 16 * kRowSumChunks;
+__global__ __launch_bounds__(64) void sum_parts_kernel(const double* __restrict__ part, int rows,
+                                                       double* __restrict__ out) {
+  __shared__ double sp[kSumPartsMax];
+  for (int i = threadIdx.x; i < rows; i += 64) sp[i] = part[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double v = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < rows; ++k) v += sp[k];
+    *out = v;
+  }
 }
 
 // T[k][i][j] = L_k[i][j] for j <= i, else 0 (the lower triangle of q_sqrt).
@@ -3078,7 +3088,7 @@ static int conditional_backward(
     if (st) return st;
   }
   hipLaunchKernelGGL(row_sums_kernel, dim3((unsigned)K, kRowSumChunks), dim3(256), 0, s, Gv, N, ldg, part);
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1), 0, s, part, (int)K * kRowSumChunks, g_var);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, s, part, (int)K * kRowSumChunks, g_var);
   return launch_status();
 }
 

@@ -53,6 +53,7 @@ _COLMAX_SIDE = True
 # (False: mgp_split_lower_f16 + mgp_gauss_kl_white per layer; A/B probes only)
 _QS_BATCH = True
 _TAIL_BATCH = True   # both layers' Cholesky / RBF backward in one batch each (elbo_and_grad)
+_RBF_NO_FILL = True  # the batched RBF backward overwrites gZ / g_ls (False: zero fills + accumulate; A/B only)
 
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
@@ -996,12 +997,16 @@ class SMGP(SGP):
                                                 [g["g_Lm"] for g in gs])
             with _Stage(timing, "rbf_bwd"):
                 layers = [layer for _, _, layer, _ in order]
-                gZs = [torch.zeros_like(layer.Z) for layer in layers]
-                glss = [torch.zeros(layer.kernel.lengthscales.numel(), dtype=torch.float64, device=self.device)
+                # gZ / g_ls written by the finish (accumulate 2: no zero fills), g_var added
+                # to the conditional backward's part
+                alloc = torch.empty if _RBF_NO_FILL else torch.zeros
+                gZs = [alloc(layer.Z.shape, dtype=layer.Z.dtype, device=self.device) for layer in layers]
+                glss = [alloc(layer.kernel.lengthscales.numel(), dtype=torch.float64, device=self.device)
                         for layer in layers]
                 ops.rbf_backward_batch(X, [layer.Z for layer in layers], [layer.kernel.variance for layer in layers],
                                        [layer.kernel.lengthscales for layer in layers], [g["g_Kuf"] for g in gs],
-                                       gKuus, gZs, [g["g_var"] for g in gs], glss, accumulate=True)
+                                       gKuus, gZs, [g["g_var"] for g in gs], glss,
+                                       accumulate=2 if _RBF_NO_FILL else 1)
             return [{name + ".Z": gZ, name + ".variance": g["g_var"], name + ".lengthscales": gls,
                      name + ".q_mu": g["g_q_mu"], name + ".q_sqrt": g["g_q_sqrt"]}
                     for (_, name, _, _), g, gZ, gls in zip(order, gs, gZs, glss)]

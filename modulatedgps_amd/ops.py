@@ -591,7 +591,7 @@ def rbf_backward_batch(X, Zs, variances, lengthscales, gKufs, gKuus, gZs, g_vars
     """Per layer b: rbf_backward(X, Z[b], .., gKuf[b], accumulate) then
     rbf_backward(Z[b], Z[b], .., gKuu[b], symmetric=True, accumulate=True) into
     gZ[b], g_var[b], g_ls[b], for all layers in three launches (mgp_rbf_backward_batch;
-    bit-identical)."""
+    bit-identical).  accumulate 2: gZ / g_ls overwritten, g_var added to."""
     import ctypes
     _check(X, "X", 2)
     N, D = X.shape

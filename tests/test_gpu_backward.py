@@ -264,6 +264,24 @@ def test_rbf_backward_batch_bit_identical(device, N, M, D, ard, ldx, batch):
         assert torch.equal(gZs[b], ref[b][0]), b
         assert torch.equal(gvs[b], ref[b][1]), b
         assert torch.equal(gls[b], ref[b][2]), b
+    # accumulate 2 (the training step): gZ / g_ls overwritten (garbage before), g_var
+    # added to -- equal to the per-call path from zero gZ / g_ls
+    ref2 = []
+    for b in range(batch):
+        gZ, gv, gl = torch.zeros_like(init_Z[b]), init_v[b].clone(), torch.zeros_like(init_l[b])
+        ops.rbf_backward(Xd, Zs[b], var[b], ls[b], gKuf[b], accumulate=True, gZ=gZ, g_var=gv, g_ls=gl)
+        ops.rbf_backward(Zs[b], Zs[b], var[b], ls[b], gKuu[b], symmetric=True, accumulate=True, gZ=gZ, g_var=gv,
+                         g_ls=gl)
+        ref2.append((gZ, gv, gl))
+    gZs = [torch.full_like(t, float("nan")) for t in init_Z]
+    gls = [torch.full_like(t, float("nan")) for t in init_l]
+    gvs = [t.clone() for t in init_v]
+    ops.rbf_backward_batch(Xd, Zs, var, ls, gKuf, gKuu, gZs, gvs, gls, accumulate=2)
+    torch.cuda.synchronize()
+    for b in range(batch):
+        assert torch.equal(gZs[b], ref2[b][0]), b
+        assert torch.equal(gvs[b], ref2[b][1]), b
+        assert torch.equal(gls[b], ref2[b][2]), b
 
 
 @pytest.mark.parametrize("N,M,D,ard,sym,ldx", [(3000, 64, 2, False, False, 0), (5000, 200, 3, True, False, 0),

@@ -123,6 +123,7 @@ def test_tail_backward_batch_entries_check_arguments():
     assert lib.mgp_rbf_backward_batch(*args(n_ls=3)) == -11
     assert lib.mgp_rbf_backward_batch(*args(gKuu=z)) == -14
     assert lib.mgp_rbf_backward_batch(*args(g_ls=z)) == -19
+    assert lib.mgp_rbf_backward_batch(*args(acc=3)) == -20 and lib.mgp_rbf_backward_batch(*args(acc=-1)) == -20
     wb = lib.mgp_rbf_backward_batch_workspace_bytes(100, 64, 8)
     assert lib.mgp_rbf_backward_batch(*args(wsb=2 * wb - 1)) == 1
 

@@ -25,6 +25,9 @@ def main():
     if "tailper" in sys.argv[4:]:   # Cholesky / RBF backward per layer (before round 5's batch)
         from modulatedgps_amd import models
         models._TAIL_BATCH = False
+    if "fill" in sys.argv[4:]:   # zero-filled gZ / g_ls + accumulate (before the overwrite mode)
+        from modulatedgps_amd import models
+        models._RBF_NO_FILL = False
     if "adamper" in sys.argv[4:]:   # one Adam launch per parameter block (before round 5's set)
         from modulatedgps_amd import training
         training._ADAM_SET = False
