@@ -52,6 +52,11 @@ _COLMAX_SIDE = True
 # split-f16: both layers' tril(q_sqrt) images and KL terms by mgp_qsqrt_images_kl_f16_batch
 # (False: mgp_split_lower_f16 + mgp_gauss_kl_white per layer; A/B probes only)
 _QS_BATCH = True
+# k1_in_k3 carries K1's image blocks on the step launches' idle CUs at one 512-thread
+# workgroup per CU; past this image size (N * M) the blocks outlast the chain's steps
+# (BASELINE c5, N * M = 2^29: K3 2.15 -> 5.78 ms) and K1 runs on the side stream instead
+# (schedule overlap, bit-identical)
+_K1_IN_K3_MAX_NM = 1 << 27
 _TAIL_BATCH = True   # both layers' Cholesky / RBF backward in one batch each (elbo_and_grad)
 _RBF_NO_FILL = True  # the batched RBF backward overwrites gZ / g_ls (False: zero fills + accumulate; A/B only)
 
@@ -647,7 +652,8 @@ class SMGP(SGP):
         sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
         # schedule k1_in_k3: both layers' K1 as a side job of K3's step launches (batched K3)
         k1_in_k3 = (sched == "k1_in_k3" and "LinvT2" in b and self.pred_layer.kernel._x(X) is X
-                    and self.assign_layer.kernel._x(X) is X)
+                    and self.assign_layer.kernel._x(X) is X
+                    and N * self.pred_layer.num_inducing <= _K1_IN_K3_MAX_NM)
         if sched == "k1_in_k3" and not k1_in_k3:
             sched = "overlap"
         with _Stage(timing, "kuu_chol"):
