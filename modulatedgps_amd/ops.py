@@ -527,6 +527,14 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
         _check(lik_var, "lik_var")
     if G is None:
         G = padded(4 * K, N, dev).unflatten(0, (4, K))
+    # the kernel addresses G's 4K rows as one [4K][ldg] block: the row stride from
+    # G's outer dimension (a K = 1 view's stride(1) is torch's contiguous placeholder,
+    # N, not the padded row length)
+    if G.dim() != 3 or tuple(G.shape) != (4, K, N) or G.stride(2) != 1 or G.stride(0) % K:
+        raise ValueError("G must be a [4, K, N] view of [4K][ldg] rows")
+    ldg = G.stride(0) // K
+    if K > 1 and G.stride(1) != ldg:
+        raise ValueError("G must be a [4, K, N] view of [4K][ldg] rows")
     glv = torch.empty(K, dtype=torch.float64, device=dev) if multiclass_eps is None else None
     glva = torch.empty(K, dtype=torch.float64, device=dev) if assign_lik_var is not None else None
     nbytes = _lib.load().mgp_elbo_backward_workspace_bytes(N, K)
@@ -542,7 +550,7 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
                   var_a.data_ptr(), ldf, Y.data_ptr(), float(multiclass_eps),
                   assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau),
                   float(jitter), zp, up,
-                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), G.stride(1),
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), ldg,
                   glva.data_ptr() if glva is not None else None, workspace.data_ptr(), workspace.numel(),
                   _stream())
         return G, glv, glva
@@ -550,7 +558,7 @@ def elbo_terms_backward(mu_f, var_f, mu_a, var_a, Y, lik_var, S, tau=1e-2, noise
               var_a.data_ptr(), ldf, Y.data_ptr(), lik_var.data_ptr(),
               assign_lik_var.data_ptr() if assign_lik_var is not None else None, N, K, S, float(tau),
               float(jitter), zp, up,
-              int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), G.stride(1),
+              int(seed) & 0xFFFFFFFFFFFFFFFF, int(n_offset), float(scale), G.data_ptr(), ldg,
               glv.data_ptr(), glva.data_ptr() if glva is not None else None, workspace.data_ptr(),
               workspace.numel(), _stream())
     return G, glv, glva

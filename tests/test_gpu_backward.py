@@ -30,6 +30,8 @@ def _oracle_grads(X, Y, p, z, u, a_var=None):  # end-to-end (used by the paramet
 
 @pytest.mark.parametrize("N,M,K,D,ls,S,modified", [(1000, 25, 3, 1, 0.5, 25, False),
                                                     (777, 33, 5, 2, 0.8, 7, False),
+                                                    (1001, 25, 1, 1, 0.5, 3, False),    # K = 1, N % 4 != 0
+                                                    (3, 1, 1, 1, 0.5, 1, True),
                                                     (1000, 25, 3, 1, 0.5, 25, True),
                                                     (513, 16, 8, 3, 0.9, 4, True)])
 def test_elbo_terms_backward(device, N, M, K, D, ls, S, modified):

@@ -26,10 +26,10 @@ _SETTINGS = settings(max_examples=30, deadline=None, derandomize=True, database=
 
 
 @st.composite
-def shapes(draw):
+def shapes(draw, n_min=2):
     D = draw(st.sampled_from([1, 2, 8, 16]))
     K = draw(st.sampled_from([1, 3, 8, 16]))
-    N = draw(st.integers(min_value=2, max_value=3001))
+    N = draw(st.integers(min_value=n_min, max_value=3001))
     m_max = min(N, 24 if D == 1 else (96 if D == 2 else 300))
     M = draw(st.integers(min_value=1, max_value=m_max))
     S = draw(st.integers(min_value=1, max_value=9))
@@ -81,3 +81,24 @@ def test_layer_batched_launches_match_per_layer(device, shape):
         models._K4_BATCHED, models._QS_BATCH = flags
     for a, b in zip(batched, per_layer):
         assert torch.equal(a, b), shape
+
+
+@settings(max_examples=16, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(shape=shapes(n_min=32), modified=st.booleans())
+def test_elbo_and_grad_random_shapes(device, shape, modified):
+    """The whole training gradient (SMGP / SMGPModified elbo_and_grad: K6 backward,
+    conditional backward, the batched Cholesky / RBF backward, KL) at drawn shapes
+    against float64 autograd of oracle/grad_ref.py: every block within max(3e-4,
+    4 x float32 autograd's error).  test_elbo_and_grad holds the configured shapes to
+    1.5 x; drawn shapes reach degenerate ones (M = 1, S = 1, a few points per expert)
+    where the kernel-variance gradients -- near-cancelling sums (1 - |A|^2 + |L^T A|^2
+    terms) -- are 1e-3 off float64 in float32 itself, and there the default format's
+    22-bit operands (unit roundoff 2^-22, 4 x float32's) show: e.g. (N, M, K, D, S) =
+    (130, 1, 3, 1, 1), assign.variance 5.0e-3 against float32's 2.3e-3.  N >= 32 for
+    the same reason (N = 2, K = 8: float32 8.6e-4 off).  (This test found the K = 1
+    row-stride bug of the K6 backward's G, fixed in ops.elbo_terms_backward.)"""
+    from tests.test_gpu_training import _check_elbo_and_grad
+    N, M, K, D, S, ls = shape
+    print("grad shape (N, M, K, D, S, ls), modified:", shape, modified, flush=True)
+    _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, factor=4.0)
