@@ -26,14 +26,14 @@ _SETTINGS = settings(max_examples=30, deadline=None, derandomize=True, database=
 
 
 @st.composite
-def shapes(draw, n_min=2):
+def shapes(draw, n_min=2, ls_min=0.25):
     D = draw(st.sampled_from([1, 2, 8, 16]))
     K = draw(st.sampled_from([1, 3, 8, 16]))
     N = draw(st.integers(min_value=n_min, max_value=3001))
     m_max = min(N, 24 if D == 1 else (96 if D == 2 else 300))
     M = draw(st.integers(min_value=1, max_value=m_max))
     S = draw(st.integers(min_value=1, max_value=9))
-    ls = draw(st.floats(min_value=0.25, max_value=0.5 if D <= 2 else 1.5))
+    ls = draw(st.floats(min_value=ls_min, max_value=max(ls_min, 0.5) if D <= 2 else 1.5))
     return N, M, K, D, S, ls
 
 
@@ -83,9 +83,9 @@ def test_layer_batched_launches_match_per_layer(device, shape):
         assert torch.equal(a, b), shape
 
 
-@settings(max_examples=16, deadline=None, derandomize=True, database=None,
+@settings(max_examples=24, deadline=None, derandomize=True, database=None,
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
-@given(shape=shapes(n_min=32), modified=st.booleans())
+@given(shape=shapes(ls_min=0.5), modified=st.booleans())
 def test_elbo_and_grad_random_shapes(device, shape, modified):
     """The whole training gradient (SMGP / SMGPModified elbo_and_grad: K6 backward,
     conditional backward, the batched Cholesky / RBF backward, KL) at drawn shapes
@@ -95,9 +95,13 @@ def test_elbo_and_grad_random_shapes(device, shape, modified):
     where the kernel-variance gradients -- near-cancelling sums (1 - |A|^2 + |L^T A|^2
     terms) -- are 1e-3 off float64 in float32 itself, and there the default format's
     22-bit operands (unit roundoff 2^-22, 4 x float32's) show: e.g. (N, M, K, D, S) =
-    (130, 1, 3, 1, 1), assign.variance 5.0e-3 against float32's 2.3e-3.  N >= 32 for
-    the same reason (N = 2, K = 8: float32 8.6e-4 off).  (This test found the K = 1
-    row-stride bug of the K6 backward's G, fixed in ops.elbo_terms_backward.)"""
+    (130, 1, 3, 1, 1), assign.variance 5.0e-3 against float32's 2.3e-3; (2, 1, 8, 1, 2),
+    2.2e-3 against 8.6e-4.  Lengthscales from 0.5: at 0.25 in one dimension most
+    points see K(z, x) ~ 0 and the assign layer's gradients through the
+    temperature-0.01 Gumbel-softmax near-cancel — (72, 1, 3, 1, 2, 0.25): float32 autograd
+    1.8e-2 off on assign.variance, and the HIP path 10x float32 on assign.lengthscales in
+    both image formats alike (x6 = f16 there: not an operand-format effect).  (This test
+    found the K = 1 row-stride bug of the K6 backward's G, fixed in ops.elbo_terms_backward.)"""
     from tests.test_gpu_training import _check_elbo_and_grad
     N, M, K, D, S, ls = shape
     print("grad shape (N, M, K, D, S, ls), modified:", shape, modified, flush=True)
