@@ -1,8 +1,8 @@
 """Shape/size property tests, driven by hypothesis: odd N, M not
 a multiple of any tile size, D in {1, 2, 8, 16}, K in {1, 3, 8, 16}, S in 1..9.
 
-For every drawn shape the drop-in SMGP ELBO (models.py:69-79) and the per-layer
-conditionals (models.py:126-144) match the float64 oracle at the north_star
+For every drawn shape the drop-in SMGP ELBO (models.py:69-79), the per-layer
+conditionals (models.py:126-144) and predict_y / predict_assign match the float64 oracle at the north_star
 tolerance (ELBO 1e-4 relative, fmean / fvar 1e-4 normwise), and the per-layer
 launches agree with the layer-batched ones bit for bit.  The examples are
 derandomized (a fixed sequence, no example database), so a failure reproduces.
@@ -59,6 +59,20 @@ def test_elbo_and_conditionals_random_shapes(device, shape):
             assert np.abs(to_np(got)).max() < 1e-6, (shape, name)
         else:
             assert normwise(to_np(got).T, want) < tol, (shape, name, cond)
+    # predict_y / predict_assign (models.py:38-41, 85-89) on held-out points
+    cond = max(np.linalg.cond(R.rbf_Kuu(L["Z"], L["variance"], L["lengthscales"])) for L in (p.pred, p.assign))
+    tol = max(1e-4, 10 * np.sqrt(cond) * 1.2e-7)
+    Xt = np.random.default_rng(N + M).standard_normal((min(N, 97), D))
+    ym, yv = model.predict_y(torch.as_tensor(Xt, dtype=torch.float32, device=device))
+    rm, rv = R.predict_y(Xt.astype(np.float32).astype(np.float64), p)
+    # normwise, with an absolute floor where the reference itself is negligible (held-out
+    # points far from every Z at a short lengthscale: means ~1e-17 in float64)
+    close = lambda got, ref: np.linalg.norm(np.asarray(got, np.float64) - ref) <= tol * max(
+        np.linalg.norm(ref), 1e-3 * np.sqrt(ref.size))
+    assert close(ym, rm), (shape, "predict_y mean")
+    assert close(yv, rv), (shape, "predict_y var")
+    pa = model.predict_assign(torch.as_tensor(Xt, dtype=torch.float32, device=device))
+    assert close(pa, R.predict_assign(Xt.astype(np.float32).astype(np.float64), p)), (shape, "predict_assign")
 
 
 @_SETTINGS
