@@ -120,3 +120,40 @@ def test_elbo_and_grad_random_shapes(device, shape, modified):
     N, M, K, D, S, ls = shape
     print("grad shape (N, M, K, D, S, ls), modified:", shape, modified, flush=True)
     _check_elbo_and_grad(device, N, M, K, D, ls, S, modified, factor=4.0)
+
+
+@_SETTINGS
+@given(shape=shapes(), modified=st.booleans(), cut=st.floats(min_value=0.0, max_value=1.0))
+def test_multiclass_and_shard_random_shapes(device, shape, modified, cut):
+    """At drawn shapes: the MultiClass / RobustMax pred likelihood (SMGP and
+    SMGPModified, K classes from the draw, at least 2) against the float64 oracle
+    (ELBO 1e-4 relative), and the data-parallel property the multi-GPU path rests on --
+    the Gaussian data term of two N-shards (split at a drawn point, Philox keyed by the
+    global row via n_offset) sums to the unsharded one (1e-6 relative)."""
+    from modulatedgps_amd import ops
+    from tests.test_gpu_multiclass import _model, _problem
+    N, M, K, D, S, ls = shape
+    K = max(K, 2)
+    print("mc/shard shape (N, M, K, D, S, ls), modified, cut:", shape, modified, round(cut, 3), flush=True)
+    X, Y, p = _problem(N, M, K, D, ls, S)
+    a_var = np.linspace(0.3, 0.9, K)[None, :]
+    z, u = R.explicit_noise(S, N, K, seed=5)
+    ref = R.smgp_modified_elbo(X, Y, p, a_var, z, u) if modified else R.smgp_elbo(X, Y, p, z, u)
+    model = _model(p, device, modified, a_var)
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=device)
+    e = float(model._build_likelihood(Xd, Y, noise=dev_noise(z, u, device)).cpu())
+    assert e == pytest.approx(ref, rel=1e-4), (shape, e, ref)
+    # N-shard invariance of the Gaussian data term (tests/test_gpu_model.py's property at drawn sizes)
+    Xg, Yg, pg = R.synthetic_problem(N, M, K, D, ls, state="perturbed", S=S)
+    gm = build_model(pg, device)
+    Xgd = torch.as_tensor(Xg, dtype=torch.float32, device=device)
+    Ygd = torch.as_tensor(Yg[:, 0], dtype=torch.float32, device=device)
+    lv = gm.likelihood.likelihood.variance.reshape(-1)
+    full = [t.clone() for t in gm.conditionals(Xgd)]
+    tot = float(ops.elbo_terms(*full, Ygd, lv, S, seed=23).cpu())
+    c = min(max(int(round(cut * N)), 1), N - 1)
+    parts = 0.0
+    for lo, hi in ((0, c), (c, N)):
+        cs = [t.clone() for t in gm.conditionals(Xgd[lo:hi])]
+        parts += float(ops.elbo_terms(*cs, Ygd[lo:hi].contiguous(), lv, S, seed=23, n_offset=lo).cpu())
+    assert parts == pytest.approx(tot, rel=1e-6, abs=1e-9), (shape, c, parts, tot)
