@@ -5,6 +5,7 @@
 //     -Lmodulatedgps_amd -lmgp_hip -Wl,-rpath,'$ORIGIN/../modulatedgps_amd'
 //   tools/panel_probe
 #include <cstring>
+#include <type_traits>
 
 #include "../modulatedgps_amd/csrc/chol.hip"
 
@@ -495,6 +496,64 @@ __device__ void rl_col(double* __restrict__ sF, double* __restrict__ col, int r,
   }
 }
 
+// V19: two-level panel, the kernel's numerics: the left 8 columns swept (updating
+// columns <= 7 only), the right half's updates from them applied afterwards as one
+// batch with the column values broadcast through LDS (each a[s] gets the same FMAs
+// in the same c order as in the one-level sweep: bit-identical), then the right 8
+// columns swept.  sb: 64 doubles of LDS.
+__device__ void two_level(double* __restrict__ sF, double* __restrict__ col, double* __restrict__ sb, int r,
+                          int& bad) {
+  double a[16], rs[16], tl[8];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = sF[r * LDT + j];
+  auto sweep = [&](auto C0c) {
+    constexpr int C0 = decltype(C0c)::value;   // 0: left half, 8: right half
+    double piv = read_lane_f64(a[C0], C0);
+    rs[C0] = rsqrt_f64(piv);
+#pragma unroll
+    for (int c = C0; c < C0 + 8; ++c) {
+      double v[16];
+#pragma unroll
+      for (int s2 = c + 1; s2 < C0 + 8; ++s2) v[s2] = read_lane_f64(a[c], s2);
+      const double t = a[c] * (rs[c] * rs[c]);
+      if (C0 == 0) tl[c] = t;
+      if (c + 1 < C0 + 8) {
+        a[c + 1] = fma(-t, v[c + 1], a[c + 1]);
+        piv = read_lane_f64(a[c + 1], c + 1);
+        rs[c + 1] = rsqrt_f64(piv);
+      }
+#pragma unroll
+      for (int s2 = c + 2; s2 < C0 + 8; ++s2) a[s2] = fma(-t, v[s2], a[s2]);
+    }
+  };
+  sweep(std::integral_constant<int, 0>());
+  // right half from the left columns: rows 8..15 publish a[s][c] (c < 8), c-major
+  if (r >= 8 && r < 16) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) sb[c * 8 + (r - 8)] = a[c];
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's own LDS writes land first
+  __builtin_amdgcn_wave_barrier();
+  // column 8's first update must precede its pivot: a[8] gets all 8 FMAs first
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const double2 p0 = *reinterpret_cast<const double2*>(sb + c * 8 + 0);
+    const double2 p1 = *reinterpret_cast<const double2*>(sb + c * 8 + 2);
+    const double2 p2 = *reinterpret_cast<const double2*>(sb + c * 8 + 4);
+    const double2 p3 = *reinterpret_cast<const double2*>(sb + c * 8 + 6);
+    const double vv[8] = {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) a[8 + s] = fma(-tl[c], vv[s], a[8 + s]);
+  }
+  sweep(std::integral_constant<int, 8>());
+#pragma unroll
+  for (int c = 0; c < 16; ++c) sF[r * LDT + c] = (r >= c) ? a[c] * rs[c] : 0.0;
+  if (r == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) col[c] = rs[c];
+  }
+}
+
 __global__ void run(const double* src, double* dst, unsigned long long* t, int variant) {
   __shared__ double sF[CB * LDT], col[3 * CB];
   const int r = threadIdx.x;
@@ -520,6 +579,7 @@ __global__ void run(const double* src, double* dst, unsigned long long* t, int v
   else if (variant == 16) pf_deferred(sF, col, r, bad);
   else if (variant == 17) rl_col<false>(sF, col, r, bad);
   else if (variant == 18) rl_col<true>(sF, col, r, bad);
+  else if (variant == 19) two_level(sF, col, col + CB, r, bad);
   else rl_mode<2>(sF, col, r, bad);
   unsigned long long t1 = stamp();
   if (r == 0) t[variant] = t1 - t0;
@@ -537,14 +597,14 @@ int main() {
   (void)hipMalloc(&src, sizeof(h));
   (void)hipMalloc(&dst, sizeof(h));
   (void)hipMalloc(&t, 32 * sizeof(unsigned long long));
-  constexpr int NV = 19;
+  constexpr int NV = 20;
   (void)hipMemcpy(src, h, sizeof(h), hipMemcpyHostToDevice);
   unsigned long long ht[32] = {0};
   const char* names[NV] = {"panel_factor (LDS broadcast, rcp chain)", "readlane sweep (kernel)", "chain only",
                           "trailing updates only", "readlane + rcp chain", "pipelined, pinned", "pipelined", "rsq1 chain", "readlane, rsq f64 + 1 Newton", "readlane, rsq f32 + 2 Newton", "readlane, rsq f32 + 1 Newton", "DPP row_newbcast + row copies", "panel_factor<0> (kernel)",
                           "LDS column broadcast, kernel chain", "LDS column broadcast (16-B pairs)", "ds_bpermute broadcast, kernel chain",
                           "panel_factor, pivot check after the sweep", "readlane sweep + col writes",
-                          "col writes + lane-wise pivot check"};
+                          "col writes + lane-wise pivot check", "two-level (8 + LDS batch + 8)"};
   for (int rep = 0; rep < 3; ++rep)
     for (int v = 0; v < NV; ++v) hipLaunchKernelGGL(probe::run, dim3(1), dim3(64), 0, 0, src, dst, t, v);
   (void)hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
