@@ -124,6 +124,14 @@ SIGNATURES = {
                                                     c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64,
                                                     c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr,
                                                     c_size, c_ptr, c_ptr, c_ptr]),
+    "mgp_conditional_backward_prep_bytes": (c_size, [c_i64, c_i32]),
+    "mgp_conditional_backward_prep_f16c": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_size,
+                                                         c_ptr]),
+    "mgp_conditional_backward_f16c_prepped": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,
+                                                            c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                                            c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64,
+                                                            c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr,
+                                                            c_size, c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
     "mgp_c_images_bytes": (c_size, [c_i64, c_i64, c_i32]),
     "mgp_colnorm_max": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr]),
     "mgp_expert_conditional_f16c": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,

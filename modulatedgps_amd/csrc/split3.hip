@@ -2905,7 +2905,7 @@ static int conditional_backward(
     float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
     float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream,
     bool f16, bool x8 = false, const void* Cfr = nullptr, size_t cfr_bytes = 0, const float* colmax = nullptr,
-    const float* l_bound = nullptr) {
+    const float* l_bound = nullptr, const void* qprep = nullptr) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!A) return -3;
@@ -2939,10 +2939,12 @@ static int conditional_backward(
   char* ws = (char*)workspace;
   const int64_t ldn = (N + 3) / 4 * 4;
   float* P = (float*)(ws + L.P);
-  float* LT = (float*)(ws + L.LT);
+  float* LT = qprep ? (float*)((char*)const_cast<void*>(qprep) + al256(mgp_x6_lower_bytes(M, K))) : (float*)(ws + L.LT);
   double* part = (double*)(ws + L.part);
   const int64_t ldm = (M + 3) / 4 * 4;
-  bf16x8* Sfr = (bf16x8*)(ws + L.sfr);
+  // qprep (mgp_conditional_backward_prep_f16c, the C path only): L_k's image and the
+  // transposed triangles already formed from q_sqrt, e.g. beside the forward's K3
+  bf16x8* Sfr = qprep ? (bf16x8*)const_cast<void*>(qprep) : (bf16x8*)(ws + L.sfr);
   float* gA0 = (float*)(ws + L.ga0);
   bf16x8* gAfr = (bf16x8*)(ws + L.gafr);
   bf16x8* LIfr = (bf16x8*)(ws + L.lifr);
@@ -2960,8 +2962,9 @@ static int conditional_backward(
     if (!aligned16(Cfr)) return MGP_ERR_ALIGN;
     // L_k's image (rows m, k-steps over m' <= m) into the S image's space; Linv's image
     const int64_t nfrag = (int64_t)K * nmb * nmk, nf1 = (int64_t)nmb * nmk;
-    hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
-                       ldqs, strideq, M, nmb, nmk, nfrag, Sfr, l_bound);
+    if (!qprep)
+      hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
+                         ldqs, strideq, M, nmb, nmk, nfrag, Sfr, l_bound);
     hipLaunchKernelGGL((split_tri_kernel<true, true>), dim3((unsigned)((nf1 + 3) / 4)), dim3(256), 0, s, LinvT, ldl,
                        (int64_t)0, M, nmb, nmk, nf1, LIfr);
     if ((st = launch_status())) return st;
@@ -3067,9 +3070,11 @@ static int conditional_backward(
     st = mgp_gram_x6(A, lda, 0, M, A, lda, 0, M, Gv, ldg, N, K, 1.f, 2, P, ldm, M * ldm, gws, gwsb, stream);
   }
   if (st) return st;
-  hipLaunchKernelGGL(tril_transpose_kernel, dim3((unsigned)((M + 31) / 32), (unsigned)((M + 31) / 32), (unsigned)K),
-                     dim3(256), 0, s, q_sqrt, ldqs, strideq, M, LT, ldm, M * ldm);
-  if ((st = launch_status())) return st;
+  if (!(cpath && qprep)) {
+    hipLaunchKernelGGL(tril_transpose_kernel, dim3((unsigned)((M + 31) / 32), (unsigned)((M + 31) / 32), (unsigned)K),
+                       dim3(256), 0, s, q_sqrt, ldqs, strideq, M, LT, ldm, M * ldm);
+    if ((st = launch_status())) return st;
+  }
   st = mgp_gram_x6(P, ldm, M * ldm, M, LT, ldm, M * ldm, M, nullptr, 0, M, K, 2.f, 1, g_q_sqrt, ldgs, strideg, gws,
                    gwsb, stream);
   if (st) return st;
@@ -3130,6 +3135,61 @@ extern "C" int mgp_conditional_backward_f16c(
   return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
                               N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
                               workspace_bytes, stream, true, false, Cfr, cfr_bytes, colmax, l_bound);
+}
+
+// The q_sqrt-only part of mgp_conditional_backward_f16c -- L_k's image (the B-b operand,
+// scale l_bound: the bound of the forward's Lfr image) and the transposed triangles
+// L_k^T (B-d's operand) -- into prep, so that it can run off the backward's critical
+// path (the Python host: on the side stream beside the forward's K3).
+extern "C" size_t mgp_conditional_backward_prep_bytes(int64_t M, int32_t K) {
+  if (M <= 0 || K <= 0) return 256;
+  const int64_t ldm = (M + 3) / 4 * 4;
+  return al256(mgp_x6_lower_bytes(M, K)) + al256((size_t)K * M * ldm * 4);
+}
+
+extern "C" int mgp_conditional_backward_prep_f16c(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M,
+                                                  int32_t K, const float* l_bound, void* prep, size_t prep_bytes,
+                                                  mgp_stream_t stream) {
+  if (!q_sqrt) return -1;
+  if (ldqs < M) return -2;
+  if (K > 1 && strideq < ldqs * M) return -3;
+  if (M <= 0) return -4;
+  if (K < 1) return -5;
+  if (K > 16) return MGP_ERR_UNSUPPORTED;
+  if (!l_bound) return -6;
+  if (!prep) return -7;
+  if (prep_bytes < mgp_conditional_backward_prep_bytes(M, K)) return MGP_ERR_WORKSPACE;
+  if (!aligned16(prep)) return MGP_ERR_ALIGN;
+  if (lower_planes(M, K) >= ((size_t)1 << 32)) return MGP_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t Mp = x6_mp(M), ldm = (M + 3) / 4 * 4;
+  const int nmk = (int)(Mp / 16), nmb = (int)(Mp / 32);
+  const int64_t nfrag = (int64_t)K * nmb * nmk;
+  float* LT = (float*)((char*)prep + al256(mgp_x6_lower_bytes(M, K)));
+  hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
+                     ldqs, strideq, M, nmb, nmk, nfrag, (bf16x8*)prep, l_bound);
+  hipLaunchKernelGGL(tril_transpose_kernel, dim3((unsigned)((M + 31) / 32), (unsigned)((M + 31) / 32), (unsigned)K),
+                     dim3(256), 0, s, q_sqrt, ldqs, strideq, M, LT, ldm, M * ldm);
+  return launch_status();
+}
+
+// mgp_conditional_backward_f16c on a prep of the same q_sqrt and l_bound
+// (mgp_conditional_backward_prep_f16c): two launches fewer, the same results.
+extern "C" int mgp_conditional_backward_f16c_prepped(
+    const void* Afr, size_t afr_bytes, const float* A, int64_t lda,
+    const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* q_mu, int64_t ldq, const float* LinvT,
+    int64_t ldl, const float* Gmu, const float* Gv, int64_t ldg, int64_t M, int64_t N, int32_t K,
+    float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
+    float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, const void* Cfr,
+    size_t cfr_bytes, const float* colmax, const float* l_bound, const void* prep, size_t prep_bytes,
+    mgp_stream_t stream) {
+  if (!Cfr) return -30;
+  if (!prep) return -33;
+  if (prep_bytes < mgp_conditional_backward_prep_bytes(M, K)) return -34;
+  if (!aligned16(prep)) return MGP_ERR_ALIGN;
+  return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
+                              N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
+                              workspace_bytes, stream, true, false, Cfr, cfr_bytes, colmax, l_bound, prep);
 }
 
 // Afr from mgp_trsm_stats_f16x8 with the f32 A (all three planes): S_k A on f16 hi

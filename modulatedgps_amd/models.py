@@ -59,6 +59,9 @@ _QS_BATCH = True
 _K1_IN_K3_MAX_NM = 1 << 27
 _TAIL_BATCH = True   # both layers' Cholesky / RBF backward in one batch each (elbo_and_grad)
 _RBF_NO_FILL = True  # the batched RBF backward overwrites gZ / g_ls (False: zero fills + accumulate; A/B only)
+# training: the q_sqrt-only launches of the C-images backward (L_k's image, L_k^T) on the
+# side stream beside K3 (mgp_conditional_backward_prep_f16c; False: inside the backward)
+_COND_PREP = True
 
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
@@ -571,6 +574,8 @@ class SMGP(SGP):
                 for L in ("f", "a"):  # K5 writes C_k per expert; the backward reads them
                     b["Cfr_" + L] = torch.empty(cb, dtype=torch.uint8, device=dev)
                     b["colmax_" + L] = torch.empty(1, dtype=torch.float32, device=dev)
+                    b["cprep_" + L] = torch.empty(ops._lib.load().mgp_conditional_backward_prep_bytes(Mx, K),
+                                                  dtype=torch.uint8, device=dev)
             b["ws_cbwd"] = torch.empty(ops.conditional_backward_workspace_bytes(Mx, N, K), dtype=torch.uint8,
                                        device=dev)
         self._bufs[key] = b
@@ -707,6 +712,15 @@ class SMGP(SGP):
                     with _Stage(timing, "gauss_kl"):
                         self.pred_layer.prior_kl(out=kl_out[0:1])
                         self.assign_layer.prior_kl(out=kl_out[1:2])
+                b["cprep_done"] = False
+                if train and _COND_PREP and fmt == "f16" and "cprep_a" in b:
+                    # the backward's q_sqrt-only launches, on the forward's L_k image bounds
+                    with _Stage(timing, "split_tri"):
+                        for L, layer in layers:
+                            ops.conditional_backward_prep(
+                                layer.q_sqrt, ops.image_bound(b["Lfr_" + L], layer.num_inducing,
+                                                              K=layer.num_latent_gps), out=b["cprep_" + L])
+                    b["cprep_done"] = True
             if sched == "serial":
                 side_work()
             else:
@@ -977,10 +991,11 @@ class SMGP(SGP):
                 if "Cfr_" + L in b:  # the forward's C_k images (mgp_conditional_backward_f16c)
                     cimg = (b["Cfr_" + L], b["colmax_" + L],
                             ops.image_bound(b["Lfr_" + L], M, K=layer.num_latent_gps))
+                prep = b["cprep_" + L] if cimg is not None and b.get("cprep_done") else None
                 return ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], layer.q_sqrt,
                                                    layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
                                                    workspace=ws, fmt=forward_image_format(True),
-                                                   c_images=cimg)
+                                                   c_images=cimg, prep=prep)
 
         def tail_backward(L, name, layer, g):
             with _Stage(timing, "chol_bwd"):

@@ -790,8 +790,22 @@ def conditional_backward_workspace_bytes(M, N, K):
     return int(_lib.load().mgp_conditional_backward_workspace_bytes(M, N, K))
 
 
+def conditional_backward_prep(q_sqrt, l_bound, out=None):
+    """The q_sqrt-only part of the C-images backward (L_k's image at scale l_bound, the
+    transposed triangles) as a uint8 device buffer for conditional_backward_x6(...,
+    prep=...) (mgp_conditional_backward_prep_f16c)."""
+    _check(q_sqrt, "q_sqrt", 3)
+    K, M, _ = q_sqrt.shape
+    nbytes = _lib.load().mgp_conditional_backward_prep_bytes(M, K)
+    if out is None or out.numel() < nbytes:
+        out = _ws(nbytes, q_sqrt.device)
+    _lib.call("mgp_conditional_backward_prep_f16c", q_sqrt.data_ptr(), _ld(q_sqrt), q_sqrt.stride(0), M, K,
+              l_bound.data_ptr(), out.data_ptr(), out.numel(), _stream())
+    return out
+
+
 def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None, fmt="x6",
-                            cross=None, c_images=None):
+                            cross=None, c_images=None, prep=None):
     """Backward of one layer's conditional (see include/mgp_hip.h): returns dict of
     g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1]).
     fmt: format of A's image Afr ("f16": mgp_conditional_backward_f16; with cross "f8",
@@ -826,6 +840,11 @@ def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None
         Cfr, colmax, l_bound = c_images
         entry = "mgp_conditional_backward_f16c"
         args += [Cfr.data_ptr(), Cfr.numel(), colmax.data_ptr(), l_bound.data_ptr()]
+        if prep is not None:   # from conditional_backward_prep(q_sqrt, l_bound) of the same q_sqrt
+            entry += "_prepped"
+            args += [prep.data_ptr(), prep.numel()]
+    elif prep is not None:
+        raise ValueError("prep needs c_images (the C-images backward)")
     _lib.call(entry, *args, _stream())
     return out
 

@@ -177,6 +177,15 @@ def test_conditional_backward_c_images(device, N, M, K, D, ls, pattern):
     assert np.quantile(cols, 0.99) < 1e-3
     assert normwise(got, to_np(g_s["g_Kuf"])[:, :N]) < 1e-4
     assert normwise(to_np(g["g_Lm"]), to_np(g_s["g_Lm"])) < 1e-4
+    # the same backward on a prep of q_sqrt (mgp_conditional_backward_prep_f16c, as the
+    # training step runs it beside K3): every output bit-identical
+    lb = ops.image_bound(Lhr, M, K=K)
+    prep = ops.conditional_backward_prep(qs, lb)
+    g_p = ops.conditional_backward_x6(Ahr, A, qs, qmu, LinvT[0], Gmu, Gv, M, N, fmt="f16", cross="f16",
+                                      c_images=(Cfr, colmax, lb), prep=prep)
+    for key in g:
+        if torch.is_tensor(g[key]):
+            assert torch.equal(g[key], g_p[key]), key
 
 
 @pytest.mark.parametrize("M,D,ls", [(64, 2, 0.8), (200, 3, 1.0), (1024, 8, 1.0)])

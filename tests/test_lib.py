@@ -146,3 +146,24 @@ def test_adam_step_set_checks_arguments():
     assert call(ld=I64(4, 3)) == -11
     assert call(t=0) == -16
     assert call(rows=I64(0, 0)) == 0   # nothing to update: no launch
+
+
+def test_conditional_backward_prep_entries_check_arguments():
+    """mgp_conditional_backward_prep_f16c / _f16c_prepped: NULL pointers, bad sizes and a
+    short prep buffer rejected with the codes of mgp_hip.h before any HIP call."""
+    lib = _lib.load()
+    c = ctypes.c_void_p(256)
+    M, K, N = 64, 3, 100
+    pb = lib.mgp_conditional_backward_prep_bytes(M, K)
+    assert pb >= lib.mgp_x6_lower_bytes(M, K) + K * M * M * 4
+    prep = lambda q=c, ldqs=M, sq=M * M, m=M, k=K, lb=c, out=c, nb=pb: lib.mgp_conditional_backward_prep_f16c(
+        q, ldqs, sq, m, k, lb, out, nb, None)
+    assert prep(q=None) == -1 and prep(ldqs=M - 1) == -2 and prep(sq=M) == -3
+    assert prep(m=0) == -4 and prep(k=0) == -5 and prep(k=17) == 3
+    assert prep(lb=None) == -6 and prep(out=None) == -7 and prep(nb=pb - 1) == 1
+    assert prep(out=ctypes.c_void_p(264)) == 2
+    wsb = lib.mgp_conditional_backward_workspace_bytes(M, N, K)
+    cb = lambda cfr=c, pr=c, nb=pb: lib.mgp_conditional_backward_f16c_prepped(
+        c, 1 << 30, c, 128, c, M, M * M, c, K, c, M, c, c, 128, M, N, K, c, K, c, M, M * M, c, 128, c, M, c, c, wsb,
+        cfr, 1 << 30, c, c, pr, nb, None)
+    assert cb(cfr=None) == -30 and cb(pr=None) == -33 and cb(nb=pb - 1) == -34

@@ -28,6 +28,9 @@ def main():
     if "fill" in sys.argv[4:]:   # zero-filled gZ / g_ls + accumulate (before the overwrite mode)
         from modulatedgps_amd import models
         models._RBF_NO_FILL = False
+    if "noprep" in sys.argv[4:]:   # the C-images backward's q_sqrt launches inside it (before the prep)
+        from modulatedgps_amd import models
+        models._COND_PREP = False
     if "adamper" in sys.argv[4:]:   # one Adam launch per parameter block (before round 5's set)
         from modulatedgps_amd import training
         training._ADAM_SET = False
