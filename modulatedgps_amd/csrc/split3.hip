@@ -331,11 +331,22 @@ using ic = std::integral_constant<int, V>;
 // cross terms (mfma_f8x): 2 + 2 f16-product-equivalents instead of 6.
 // HOIST: all T fragment reads of a k-step issued before its MFMAs (trsm_bwd: 457 ->
 // 438 us; K4 +2.5 %, K5 unchanged -- so only there).
-template <int DIAG, int NC = 2, int NPL = 3, bool F16 = false, bool X8 = false, bool HOIST = false>
+// BH: called as bh(b, mk) on k-step mk's B fragments right before their MFMAs
+// (trsm_bwd16_kernel's per-column rescale of the gA image); NoBHook: nothing.
+#ifndef MGP_BH_EARLY
+#define MGP_BH_EARLY 0
+#endif
+constexpr bool kBhEarly = MGP_BH_EARLY;  // the hook on the next k-step's fragments, after this one's MFMAs
+struct NoBHook {
+  template <class B>
+  __device__ __forceinline__ void operator()(B&, int) const {}
+};
+template <int DIAG, int NC = 2, int NPL = 3, bool F16 = false, bool X8 = false, bool HOIST = false,
+          typename BH = NoBHook>
 __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)[4 * 3 * 64],
                                             __amdgpu_buffer_rsrc_t rT, uint32_t tbase,
                                             __amdgpu_buffer_rsrc_t rB, uint32_t sB0, int mk_begin,
-                                            int mk_end, int nmk, bool init = true) {
+                                            int mk_end, int nmk, bool init = true, BH bhook = BH{}) {
   static_assert(!X8 || (F16 && NPL == 2), "X8 reads split-f16 images");
   auto PL = [](int p) { return (X8 && p == 1) ? 2 : p; };  // LDS / register plane -> image plane
   const int tid = threadIdx.x, lane = tid & 63;
@@ -427,6 +438,7 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
   u32x4v st[NPL];
   load_t(st, mk_begin);
   load_b(b0, mk_begin);
+  if constexpr (kBhEarly) bhook(b0, mk_begin);
   store_t(0, st);
   __syncthreads();
   // two k-steps per iteration: LDS buffers and fragment sets alternate
@@ -436,10 +448,12 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     load_t(st, mk + 1);
     load_b(b1, mk + 1);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!kBhEarly) bhook(b0, mk);
     if constexpr (X8)
       compute_x8(0, b0, ilo, ihi, std::false_type{});
     else
       compute(0, b0, ilo, ihi);
+    if constexpr (kBhEarly) bhook(b1, mk + 1);   // beside k-step mk's MFMAs
     __builtin_amdgcn_sched_barrier(0);
     store_t(1, st);
     __syncthreads();
@@ -447,10 +461,12 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     load_t(st, m2);
     load_b(b0, m2);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!kBhEarly) bhook(b1, mk + 1);
     if constexpr (X8)
       compute_x8(1, b1, ilo, ihi, std::true_type{});
     else
       compute(1, b1, ilo, ihi);
+    if constexpr (kBhEarly) bhook(b0, m2);
     __builtin_amdgcn_sched_barrier(0);
     store_t(0, st);
     __syncthreads();
@@ -1310,10 +1326,16 @@ __global__ __launch_bounds__(256, 2) void grad_a_s_f16_kernel(const bf16x8* __re
 // C_k column strip is read from HBM about once and served to the other pairs
 // from L2 (one row tile per workgroup: the light tiles ran ahead through the
 // experts and every strip came from HBM/MALL ~4.5 times).
+// cexp != nullptr (MGP_TRSM_BWD16): the image is split-f16 instead of x6, each
+// column of the 128-row tile t scaled by 2^e, e = img_exp(max over the tile's rows of
+// |gA[., n]|) -- exact per (tile, column), so no bound can be loose -- and e goes to
+// cexp[t][n] (kCexpZero for an all-zero tile) for trsm_bwd16_kernel.
+constexpr float kCexpZero = 1000.f;
 template <int NC>
 __device__ __forceinline__ void grad_a_c_store(const floatx16 (&out)[4][NC], int c, int t, int tn, int w, int lane,
                                                int nmk, int64_t M, int64_t N, const float* __restrict__ gA0,
-                                               int64_t ld0, bf16x8* __restrict__ gAfr) {
+                                               int64_t ld0, bf16x8* __restrict__ gAfr, float* __restrict__ cexp,
+                                               int64_t ldc) {
   const int64_t nb = 4 * (int64_t)tn + w;
   const int64_t n = 32 * nb + (lane & 31);
   const int64_t i0 = 128 * (int64_t)t;
@@ -1322,6 +1344,36 @@ __device__ __forceinline__ void grad_a_c_store(const floatx16 (&out)[4][NC], int
   const uint32_t soff = (uint32_t)((i0 * ld0 + 128 * (int64_t)tn) * 4), ld32 = (uint32_t)ld0;
   const int nl = 32 * w + (lane & 31);
   const bool ok = n < N;
+  if (cexp) {
+    float v[4][16];
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const uint32_t rl = (uint32_t)(32 * i + acc_row(e, lane));
+        const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
+        v[i][e] = ok ? fmaf(2.f, out[i][c][e], b0) : 0.f;
+        mx = fmaxf(mx, fabsf(v[i][e]));
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the column's other 16 rows of each 32-row block
+    // 2^ex as two factors: a tile of tiny values (|gA| < 2^-114) needs ex > 127
+    const int ex = img_exp(mx), ex1 = ex / 2;
+    const float sc1 = ldexpf(1.f, ex1), scale = ldexpf(1.f, ex - ex1);
+    if (lane < 32 && ok) cexp[t * ldc + n] = mx > 0.f ? (float)ex : kCexpZero;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t mk = 8 * (int64_t)t + 2 * i;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float u[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[j] = v[i][8 * s2 + j] * sc1;
+        store_split_f16(gAfr + ((nb * nmk + mk + s2) * 3) * 64 + lane, u, scale);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float v[16];
@@ -1392,7 +1444,8 @@ __global__ __launch_bounds__(256, 2) void grad_a_c_kernel(const bf16x8* __restri
                                                          bf16x8* __restrict__ gAfr,
                                                          const float* __restrict__ l_bound,
                                                          const float* __restrict__ a_bound,
-                                                         const float* __restrict__ colmax) {
+                                                         const float* __restrict__ colmax,
+                                                         float* __restrict__ gexp, int64_t ldc) {
   constexpr int U = PD + 1;
   static_assert(8 % U == 0, "the ring cycles within an expert's 8 k-steps (and the LDS double buffer)");
   __shared__ bf16x8 sL[2][4 * 3 * 64];
@@ -1538,7 +1591,8 @@ __global__ __launch_bounds__(256, 2) void grad_a_c_kernel(const bf16x8* __restri
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][c][e] *= gl;
       // column block nb + c as (128-column tile, wave) of the one-block store
-      grad_a_c_store(acc, c, t, (int)((nb + c) / 4), (int)((nb + c) % 4), lane, nmk, M, N, gA0, ld0, gAfr);
+      grad_a_c_store(acc, c, t, (int)((nb + c) / 4), (int)((nb + c) % 4), lane, nmk, M, N, gA0, ld0, gAfr, gexp,
+                     ldc);
     }
   }
 }
@@ -1589,6 +1643,82 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd_kernel(const bf16x8* __restri
   floatx16 acc[4][2];
   x6_mainloop<1, 2, 3, false, false, true>(acc, sL, img_rsrc(LIfr, lifr_bytes), (uint32_t)((4 * t) * nmk) * 3u * kFragBytes,
                     img_rsrc(gAfr, gafr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk);
+  store_acc_f32(acc, gKuf, ldk, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
+}
+
+// B-d on split-f16 images (MGP_TRSM_BWD16): three f16 products per block instead of
+// six bf16 ones.  Linv's image at 2^img_exp(*li_bound); gA's image per (128-row tile
+// t', column n) at 2^cexp[t'][n] (grad_a_c_store).  Each lane owns one column of each
+// of its two sub-tiles: at the start it takes E = min over the tiles t' >= t it
+// contracts of cexp[t'][n] (the largest tile), and every B fragment of tile t' is
+// multiplied by 2^(E - cexp[t'][n]) <= 1 in f16 right before its MFMAs, so all
+// tiles meet in the accumulator at the common scale 2^E (exact powers of two: the
+// product is that of the exactly-scaled image; only parts below 2^-24 of the
+// column's largest tile are lost to f16 underflow).  Output unscaled by 2^-(E + eL).
+constexpr int kTrsmBwd16MaxT = 32;  // row tiles (M <= 4096); larger M: trsm_bwd_kernel
+#ifndef MGP_TRSM_BWD16
+#define MGP_TRSM_BWD16 1
+#endif
+constexpr bool kTrsmBwd16 = MGP_TRSM_BWD16;
+__global__ __launch_bounds__(256, 2) void trsm_bwd16_kernel(const bf16x8* __restrict__ gAfr,
+                                                           const bf16x8* __restrict__ LIfr, uint32_t gafr_bytes,
+                                                           uint32_t lifr_bytes, int nmk, int nmb, int nTn,
+                                                           int64_t M, int64_t N, float* __restrict__ gKuf,
+                                                           int64_t ldk, const float* __restrict__ cexp, int64_t ldc,
+                                                           const float* __restrict__ li_bound) {
+  __shared__ bf16x8 sL[2][4 * 3 * 64];
+  __shared__ float sF[kTrsmBwd16MaxT][kX6BN];  // per (tile t' - t, column): 2^(E - cexp)
+  int t, tn;
+  const int nT = nmk / 8;
+  col_major_item(blockIdx.x, nT, nTn, t, tn);
+  t = nT - 1 - t;  // lower T from the diagonal on: row tile 0 is the heaviest
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  {  // thread = one column of the item
+    const int64_t n = (int64_t)tn * kX6BN + threadIdx.x;
+    float E = kCexpZero;
+    if (n < N)
+      for (int tp = t; tp < nT; ++tp) E = fminf(E, cexp[tp * ldc + n]);
+    for (int tp = t; tp < nT; ++tp) sF[tp - t][threadIdx.x] = n < N ? exp2f(E - cexp[tp * ldc + n]) : 0.f;
+  }
+  float E2[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {  // this lane's columns (the accumulators' and the B fragments')
+    const int64_t n = (int64_t)tn * kX6BN + 64 * w + 32 * c + (lane & 31);
+    float E = kCexpZero;
+    if (n < N)
+      for (int tp = t; tp < nT; ++tp) E = fminf(E, cexp[tp * ldc + n]);
+    E2[c] = E;
+  }
+  int tcur = -1;
+  _Float16 f[2] = {(_Float16)1.f, (_Float16)1.f};
+  auto bh = [&](bf16x8 (&b)[2][3], int mk) {
+    const int tp = mk >> 3;
+    if (tp != tcur) {  // uniform: every 8 k-steps
+      tcur = tp;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) f[c] = (_Float16)sF[tp - t][64 * w + 32 * c + (lane & 31)];
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        b[c][p] = __builtin_bit_cast(bf16x8, __builtin_bit_cast(halfx8, b[c][p]) * f[c]);
+  };
+  floatx16 acc[4][2];
+  x6_mainloop<1, 2, 2, true, false, true>(acc, sL, img_rsrc(LIfr, lifr_bytes), (uint32_t)((4 * t) * nmk) * 3u * kFragBytes,
+                    img_rsrc(gAfr, gafr_bytes), (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes, 8 * t, nmk, nmk,
+                    true, bh);
+  const int eL = img_exp(*li_bound);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    // 2^-(E + eL) as two factors (E reaches ~160 for a column of tiny values)
+    const float x = E2[c] + (float)eL, x1 = floorf(0.5f * x);
+    const float u1 = E2[c] >= kCexpZero ? 0.f : exp2f(-x1), u2 = exp2f(x1 - x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][c][e] = acc[i][c][e] * u1 * u2;
+  }
   store_acc_f32(acc, gKuf, ldk, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
 }
 
@@ -2802,7 +2932,7 @@ constexpr int kRowSumChunks = 32;  // column chunks of row_sums_kernel
 
 namespace {
 struct CondBwdWs {  // workspace carve-up (256-B aligned pieces)
-  size_t sfr, ga0, rimg, qpart, gafr, lifr, P, LT, part, bnd, gram, total;
+  size_t sfr, ga0, rimg, qpart, gafr, lifr, P, LT, part, bnd, cexp, gram, total;
 };
 size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
@@ -2821,7 +2951,8 @@ CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
   w.P = o;    o += al256((size_t)K * M * ldm * 4);
   w.LT = o;   o += al256((size_t)K * M * ldm * 4);
   w.part = o; o += al256((size_t)K * kRowSumChunks * 8);  // row_sums partials
-  w.bnd = o;  o += 256;  // split-f16 bound: max |Gv|
+  w.bnd = o;  o += 256;  // split-f16 bounds: max |Gv|, max |LinvT| (MGP_TRSM_BWD16)
+  w.cexp = o; o += al256((size_t)((M + 127) / 128) * ldn * 4);  // gA image scales per (row tile, column)
   w.gram = o;
   size_t g = mgp_gram_x6_workspace_bytes(M, M, N, K, 2);
   g = g > mgp_gram_x6_workspace_bytes(M, M, M, K, 2) ? g : mgp_gram_x6_workspace_bytes(M, M, M, K, 2);
@@ -2955,6 +3086,10 @@ static int conditional_backward(
   const int nTn = (int)(x6_np(N) / kX6BN);
   int st;
   const bool cpath = f16 && !x8 && Cfr;  // B-b from the forward's C_k images
+  // B-d on split-f16 images (trsm_bwd16_kernel): the C path, M <= 4096
+  const bool bwd16 = kTrsmBwd16 && cpath && nT <= kTrsmBwd16MaxT;
+  float* li_bound = (float*)(ws + L.bnd) + 1;
+  float* cexp = (float*)(ws + L.cexp);
   if (cpath) {
     if (!colmax || !l_bound) return -32;
     if (cfr_bytes < mgp_c_images_bytes(M, N, K)) return -31;
@@ -2965,8 +3100,12 @@ static int conditional_backward(
     if (!qprep)
       hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
                          ldqs, strideq, M, nmb, nmk, nfrag, Sfr, l_bound);
+    if (bwd16) {  // Linv's split-f16 image at max |LinvT| (its upper triangle)
+      if ((st = hip_status(hipMemsetAsync(li_bound, 0, sizeof(float), s)))) return st;
+      launch_absmax<2>(LinvT, ldl, (int64_t)0, M, M, M, li_bound, s);
+    }
     hipLaunchKernelGGL((split_tri_kernel<true, true>), dim3((unsigned)((nf1 + 3) / 4)), dim3(256), 0, s, LinvT, ldl,
-                       (int64_t)0, M, nmb, nmk, nf1, LIfr);
+                       (int64_t)0, M, nmb, nmk, nf1, LIfr, bwd16 ? (const float*)li_bound : nullptr);
     if ((st = launch_status())) return st;
   } else {
   // 1. S_k = L_k L_k^T (x6 gram over M of tril(q_sqrt), into the LT buffer) and its
@@ -3033,7 +3172,8 @@ static int conditional_backward(
     hipLaunchKernelGGL((grad_a_c_kernel<kGacPD, kGacNC>), dim3((unsigned)((nT + 1) / 2 * (2 / kGacNC) * nTn)), dim3(256), 0, s,
                        (const bf16x8*)Sfr, (uint32_t)lower_planes(M, K), (const bf16x8*)Cfr,
                        (int64_t)(cols_planes(M, N) / 16), (uint32_t)cols_planes(M, N), nmk, (2 / kGacNC) * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, l_bound,
-                       (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)), colmax);
+                       (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)), colmax,
+                       bwd16 ? cexp : nullptr, ldn);
   else if (f16 && x8)
     hipLaunchKernelGGL((grad_a_s_kernel<true, true>), dim3((unsigned)(nT * 2 * nTn)), dim3(256), 0, s,
                        (const bf16x8*)Sfr, (uint32_t)mgp_x6_lower_bytes(M, 1), (const bf16x8*)Afr, (uint32_t)afr_bytes,
@@ -3050,6 +3190,11 @@ static int conditional_backward(
                        M, N, Gv, ldg, gA0, ldn, gAfr, nullptr, nullptr);
   if ((st = launch_status())) return st;
   // 4. gKuf = Linv^T gA
+  if (bwd16)
+    hipLaunchKernelGGL(trsm_bwd16_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)gAfr,
+                       (const bf16x8*)LIfr, (uint32_t)img, (uint32_t)mgp_x6_lower_bytes(M, 1), nmk, nmb, nTn, M, N,
+                       g_Kuf, ldk, (const float*)cexp, ldn, (const float*)li_bound);
+  else
   hipLaunchKernelGGL(trsm_bwd_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)gAfr,
                      (const bf16x8*)LIfr, (uint32_t)img, (uint32_t)mgp_x6_lower_bytes(M, 1), nmk, nmb, nTn, M, N, g_Kuf,
                      ldk);

@@ -118,7 +118,7 @@ def test_conditional_backward(device, N, M, K, D, ls):
 
 @pytest.mark.parametrize("N,M,K,D,ls", [(2000, 64, 3, 2, 1.0), (4097, 200, 4, 3, 1.2), (3000, 300, 5, 2, 1.0),
                                         (8192, 512, 8, 8, 2.0), (1500, 96, 1, 2, 1.0)])
-@pytest.mark.parametrize("pattern", ["normal", "adversarial"])
+@pytest.mark.parametrize("pattern", ["normal", "adversarial", "tiny"])
 def test_conditional_backward_c_images(device, N, M, K, D, ls, pattern):
     """The split-f16 training backward from the forward's C_k = L_k^T A images
     (grad_a_c_kernel: one pipeline over all experts, the accumulator kept in units
@@ -145,6 +145,11 @@ def test_conditional_backward_c_images(device, N, M, K, D, ls, pattern):
         gv[min(2, K - 1), 80:120] *= 1e6
         gv[0, 80:120] *= 1e-6
         gv[:, 120:130] = 1e-30
+    if pattern == "tiny":   # whole columns of gA ~1e-34 (per-tile image scales 2^125 .. 2^131: past f32's 2^127)
+        gv[:, 200:260] *= 1e-33
+        gmu[:, 200:260] *= 1e-33
+        gv[:, 300:310] = 0.0
+        gmu[:, 300:310] = 0.0
     Gmu, Gv = ops.padded(K, N, device), ops.padded(K, N, device)
     Gmu.copy_(torch.as_tensor(gmu))
     Gv.copy_(torch.as_tensor(gv))
@@ -175,6 +180,10 @@ def test_conditional_backward_c_images(device, N, M, K, D, ls, pattern):
     # column-wise too: the tiny and zero-weight columns must not pick up noise
     cols = np.linalg.norm(got - gKuf_ref, axis=0) / np.maximum(np.linalg.norm(gKuf_ref, axis=0), 1e-30)
     assert np.quantile(cols, 0.99) < 1e-3
+    if pattern == "tiny":   # the tiny columns relative to themselves, the zero ones exact
+        tiny = np.linalg.norm(got[:, 200:260] - gKuf_ref[:, 200:260], axis=0) / np.linalg.norm(gKuf_ref[:, 200:260], axis=0)
+        assert np.quantile(tiny, 0.9) < 1e-2, np.quantile(tiny, 0.9)
+        assert not got[:, 300:310].any()
     assert normwise(got, to_np(g_s["g_Kuf"])[:, :N]) < 1e-4
     assert normwise(to_np(g["g_Lm"]), to_np(g_s["g_Lm"])) < 1e-4
     # the same backward on a prep of q_sqrt (mgp_conditional_backward_prep_f16c, as the
