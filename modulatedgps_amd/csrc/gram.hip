@@ -246,7 +246,10 @@ __device__ __forceinline__ void stash4h(char* dst, floatx4 v, float scale) {
 // F16: the chunks are split into scaled fp16 hi / lo planes instead (xb, yb, wb:
 // device bounds of |X|, |Y| and |W|, the scales 2^img_exp(xb), 2^img_exp(yb wb)),
 // three f16 products per fragment pair; the accumulators are unscaled on store.
-template <bool TRI, bool WEIGHT, bool F16 = false>
+// RS (with F16): xb / yb are per-row bounds (xb[i] >= max_n |X[i][n]|, yb[j] likewise),
+// each row split at its own scale 2^min(img_exp, 120) and the output unscaled per row
+// and column -- rows of very different size (g_Kuf, A = L^-1 Kuf) keep their 22 bits.
+template <bool TRI, bool WEIGHT, bool F16 = false, bool RS = false>
 __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict__ X, int64_t ldx, int64_t sx,
                                                          int64_t MI, const float* __restrict__ Y, int64_t ldy,
                                                          int64_t sy, int64_t MJ, const float* __restrict__ W,
@@ -296,7 +299,7 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool producer = w >= 4;
   float xs = 1.f, ys = 1.f, unscale = 1.f;
-  if constexpr (F16) {
+  if constexpr (F16 && !RS) {
     const int ex = img_exp(*xb), ey = img_exp(*yb * (WEIGHT ? *wb : 1.f));
     xs = ldexpf(1.f, ex);
     ys = ldexpf(1.f, ey);
@@ -313,6 +316,17 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
   const int rr = 8 * (pw & 3) + ((lane >> 1) & 7), cg = 2 * (lane >> 4) + (lane & 1);
   const int q0 = 2 * ((pw >> 2) & 1);
   const int soff = (cg >> 2) * kXG + (rr + 32 * ((cg >> 1) & 1)) * 16 + (cg & 1) * 8;
+  float xsq[2] = {xs, xs}, ysq[2] = {ys, ys};  // this producer thread's two rows of each tile
+  if constexpr (RS) {
+    if (producer) {
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int64_t ri = i0 + 32 * (q0 + qq) + rr, rj = j0 + 32 * (q0 + qq) + rr;
+        xsq[qq] = ldexpf(1.f, ri < MI ? min(img_exp(xb[ri]), 120) : 0);
+        ysq[qq] = ldexpf(1.f, rj < MJ ? min(img_exp(yb[rj]), 120) : 0);
+      }
+    }
+  }
   // buffer loads: rows beyond the matrix fall outside the resource and read 0;
   // the one partial chunk at the end of n is masked when it is stashed
   const int64_t rows_x = MI - i0 < kGT ? MI - i0 : kGT, rows_y = MJ - j0 < kGT ? MJ - j0 : kGT;
@@ -352,8 +366,8 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
       if constexpr (F16) {
-        stash4h(sX[buf] + 2 * (q0 + qq) * kXG + soff, r.x[qq], xs);
-        stash4h(sY[buf] + 2 * (q0 + qq) * kXG + soff, WEIGHT ? r.y[qq] * r.w : r.y[qq], ys);
+        stash4h(sX[buf] + 2 * (q0 + qq) * kXG + soff, r.x[qq], xsq[qq]);
+        stash4h(sY[buf] + 2 * (q0 + qq) * kXG + soff, WEIGHT ? r.y[qq] * r.w : r.y[qq], ysq[qq]);
       } else {
         stash4(sX[buf] + 2 * (q0 + qq) * kXG + soff, r.x[qq]);
         stash4(sY[buf] + 2 * (q0 + qq) * kXG + soff, WEIGHT ? r.y[qq] * r.w : r.y[qq]);
@@ -454,10 +468,17 @@ __global__ __launch_bounds__(768, 1) void gram_x6_kernel(const float* __restrict
 #pragma unroll
     for (int tb = 0; tb < 2; ++tb) {
       const int64_t j = j0 + 32 * (vb + tb) + (lane & 31);
+      float uj = unscale;
+      if constexpr (RS) uj = ldexpf(1.f, j < MJ ? -min(img_exp(yb[j]), 120) : 0);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int64_t i = i0 + 32 * (wb_ + ta) + acc_row(e, lane);
-        if (i < MI && j < MJ) out[i * MJ + j] = F16 ? acc[ta][tb][e] * unscale : acc[ta][tb][e];
+        if (i < MI && j < MJ) {
+          if constexpr (RS)
+            out[i * MJ + j] = acc[ta][tb][e] * ldexpf(1.f, -min(img_exp(xb[i]), 120)) * uj;
+          else
+            out[i * MJ + j] = F16 ? acc[ta][tb][e] * unscale : acc[ta][tb][e];
+        }
       }
     }
 }
@@ -942,8 +963,9 @@ static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, c
                           int64_t sy, int64_t MJ, const float* W, int64_t sw, int64_t N, int32_t batch, float alpha,
                           int32_t mode, float* out, int64_t ldo, int64_t so, void* workspace,
                           size_t workspace_bytes, mgp_stream_t stream, const float* xb, const float* yb,
-                          const float* wb) {
+                          const float* wb, bool rs = false) {
   const bool f16 = xb != nullptr;
+  if (rs && (W || !f16)) return MGP_ERR_UNSUPPORTED;
   if (!X) return -1;
   if (ldx < N || ldx % 4) return -2;
   if (batch > 1 && sx % 4) return -3;
@@ -975,6 +997,13 @@ static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, c
   float* ws = (float*)workspace;
   const int64_t bstride = MI * MJ, zstride = (int64_t)batch * MI * MJ;
   const dim3 grid((unsigned)(tiles * batch * nsplit));
+  if (rs && mode != 0)
+    hipLaunchKernelGGL((gram_x6_kernel<true, false, true, true>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy,
+                       MJ, W, sw, N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride, xb, yb, wb);
+  else if (rs)
+    hipLaunchKernelGGL((gram_x6_kernel<false, false, true, true>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy,
+                       MJ, W, sw, N, nper, nbj, tiles, (int)batch, nsplit, ws, bstride, zstride, xb, yb, wb);
+  else {
 #define MGP_GRAM_X6(TRI, WT, F16)                                                                              \
   if ((mode != 0) == TRI && (W != nullptr) == WT && f16 == F16)                                               \
     hipLaunchKernelGGL((gram_x6_kernel<TRI, WT, F16>), grid, dim3(768), 0, s, X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, \
@@ -988,6 +1017,7 @@ static int gram_x6_launch(const float* X, int64_t ldx, int64_t sx, int64_t MI, c
   MGP_GRAM_X6(false, true, true)
   MGP_GRAM_X6(false, false, true)
 #undef MGP_GRAM_X6
+  }
   int st = launch_status();
   if (st) return st;
   hipLaunchKernelGGL(gram_x6_reduce_kernel, dim3((unsigned)((MJ + 31) / 32), (unsigned)((MI + 31) / 32), (unsigned)batch),
@@ -1013,6 +1043,16 @@ extern "C" int mgp_gram_f16(const float* X, int64_t ldx, int64_t sx, int64_t MI,
   if (W && !w_bound) return -20;
   return gram_x6_launch(X, ldx, sx, MI, Y, ldy, sy, MJ, W, sw, N, batch, alpha, mode, out, ldo, so, workspace,
                         workspace_bytes, stream, x_bound, y_bound, w_bound);
+}
+
+// mgp_gram_f16 (unweighted) with per-row bounds xb[MI], yb[MJ] instead of two scalars
+// (gram_x6_kernel<., false, true, true>; the conditional backward's g_Lm gram).
+int gram_f16_rowscaled(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ldy, int64_t MJ, int64_t N,
+                       float alpha, int32_t mode, float* out, int64_t ldo, const float* xb, const float* yb,
+                       void* workspace, size_t workspace_bytes, mgp_stream_t stream) {
+  if (!xb || !yb) return MGP_ERR_UNSUPPORTED;
+  return gram_x6_launch(X, ldx, 0, MI, Y, ldy, 0, MJ, nullptr, 0, N, 1, alpha, mode, out, ldo, MI * ldo, workspace,
+                        workspace_bytes, stream, xb, yb, nullptr, true);
 }
 
 // mgp_gram_f16 (weighted) with X given as its row image (mgp_split_rows_f16 of X

@@ -69,6 +69,18 @@ __device__ __forceinline__ float lane_xor16(float v) {
 // max over the 64 lanes of a wave, every lane gets it: DPP within rows of 16 (quad
 // swaps, half-row and row mirrors pair the groups already reduced), then the
 // permlane swaps across rows (no LDS round trips)
+// max over each 32-lane half of a wave (every lane of the half gets it)
+__device__ __forceinline__ float half_max_f32(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));
+  };
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0xB1>{}));   // quad_perm [1, 0, 3, 2]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x4E>{}));   // quad_perm [2, 3, 0, 1]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x141>{}));  // row_half_mirror
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x140>{}));  // row_mirror
+  return fmaxf(v, lane_xor16(v));
+}
+
 __device__ __forceinline__ float wave_max_f32(float v) {
   auto dpp = [](float x, auto ctrl) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));

@@ -333,10 +333,6 @@ using ic = std::integral_constant<int, V>;
 // 438 us; K4 +2.5 %, K5 unchanged -- so only there).
 // BH: called as bh(b, mk) on k-step mk's B fragments right before their MFMAs
 // (trsm_bwd16_kernel's per-column rescale of the gA image); NoBHook: nothing.
-#ifndef MGP_BH_EARLY
-#define MGP_BH_EARLY 0
-#endif
-constexpr bool kBhEarly = MGP_BH_EARLY;  // the hook on the next k-step's fragments, after this one's MFMAs
 struct NoBHook {
   template <class B>
   __device__ __forceinline__ void operator()(B&, int) const {}
@@ -438,7 +434,6 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
   u32x4v st[NPL];
   load_t(st, mk_begin);
   load_b(b0, mk_begin);
-  if constexpr (kBhEarly) bhook(b0, mk_begin);
   store_t(0, st);
   __syncthreads();
   // two k-steps per iteration: LDS buffers and fragment sets alternate
@@ -448,12 +443,11 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     load_t(st, mk + 1);
     load_b(b1, mk + 1);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!kBhEarly) bhook(b0, mk);
+    bhook(b0, mk);
     if constexpr (X8)
       compute_x8(0, b0, ilo, ihi, std::false_type{});
     else
       compute(0, b0, ilo, ihi);
-    if constexpr (kBhEarly) bhook(b1, mk + 1);   // beside k-step mk's MFMAs
     __builtin_amdgcn_sched_barrier(0);
     store_t(1, st);
     __syncthreads();
@@ -461,12 +455,11 @@ __device__ __forceinline__ void x6_mainloop(floatx16 (&acc)[4][NC], bf16x8 (*sL)
     load_t(st, m2);
     load_b(b0, m2);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!kBhEarly) bhook(b1, mk + 1);
+    bhook(b1, mk + 1);
     if constexpr (X8)
       compute_x8(1, b1, ilo, ihi, std::true_type{});
     else
       compute(1, b1, ilo, ihi);
-    if constexpr (kBhEarly) bhook(b0, m2);
     __builtin_amdgcn_sched_barrier(0);
     store_t(0, st);
     __syncthreads();
@@ -909,7 +902,8 @@ __global__ __launch_bounds__(256) void grad_a_prep_kernel(const float* __restric
                                                           const float* __restrict__ Gv, int64_t ldg, int64_t M,
                                                           int64_t N, int K, int nns, const float* __restrict__ bound,
                                                           float* __restrict__ gA0, int64_t ldo,
-                                                          bf16x8* __restrict__ img, float* __restrict__ part, int rbs, int qvec) {
+                                                          bf16x8* __restrict__ img, float* __restrict__ part, int rbs, int qvec,
+                                                          float* __restrict__ amax = nullptr) {
   __shared__ __attribute__((aligned(16))) float sg[KMAX + 1][128];  // G_mu rows, then sum_k Gv
   __shared__ __attribute__((aligned(16))) float sA[2][32][kPrepPitch];
   __shared__ float sp[2][4][32][KMAX];
@@ -972,6 +966,15 @@ __global__ __launch_bounds__(256) void grad_a_prep_kernel(const float* __restric
     const int64_t rb = rb0 + it;
     const int b = it & 1;
     load_rows(a, rb);
+    if (amax) {  // max |A[m][.]| over this slab per row -> amax[slab][m] (rowmax_fold_kernel)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float m =
+            half_max_f32(fmaxf(fmaxf(fabsf(a[i][0]), fabsf(a[i][1])), fmaxf(fabsf(a[i][2]), fabsf(a[i][3]))));
+        const int64_t row = 32 * rb + ct_r + 8 * i;
+        if ((tid & 31) == 0 && row < M) amax[(int64_t)blockIdx.x * M + row] = m;
+      }
+    }
     // (1) coalesced rows: gA0, the LDS tile
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1660,12 +1663,17 @@ constexpr int kTrsmBwd16MaxT = 32;  // row tiles (M <= 4096); larger M: trsm_bwd
 #define MGP_TRSM_BWD16 1
 #endif
 constexpr bool kTrsmBwd16 = MGP_TRSM_BWD16;
+#ifndef MGP_GLM_F16
+#define MGP_GLM_F16 1
+#endif
+constexpr bool kGlmF16 = MGP_GLM_F16;
 __global__ __launch_bounds__(256, 2) void trsm_bwd16_kernel(const bf16x8* __restrict__ gAfr,
                                                            const bf16x8* __restrict__ LIfr, uint32_t gafr_bytes,
                                                            uint32_t lifr_bytes, int nmk, int nmb, int nTn,
                                                            int64_t M, int64_t N, float* __restrict__ gKuf,
                                                            int64_t ldk, const float* __restrict__ cexp, int64_t ldc,
-                                                           const float* __restrict__ li_bound) {
+                                                           const float* __restrict__ li_bound,
+                                                           float* __restrict__ gmax) {
   __shared__ bf16x8 sL[2][4 * 3 * 64];
   __shared__ float sF[kTrsmBwd16MaxT][kX6BN];  // per (tile t' - t, column): 2^(E - cexp)
   int t, tn;
@@ -1719,7 +1727,44 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd16_kernel(const bf16x8* __rest
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][c][e] = acc[i][c][e] * u1 * u2;
   }
+  if (gmax) {  // max |gKuf[m][.]| over this wave's 64 columns per row -> gmax[4 tn + w][m]
+    float* dst = gmax + (int64_t)(4 * tn + w) * M;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float m = half_max_f32(fmaxf(fabsf(acc[i][0][e]), fabsf(acc[i][1][e])));
+        const int64_t row = 128 * (int64_t)t + 32 * i + acc_row(e, lane);
+        if ((lane & 31) == 0 && row < M) dst[row] = m;
+      }
+  }
   store_acc_f32(acc, gKuf, ldk, 128 * (int64_t)t, (int64_t)tn * kX6BN, M, N, nullptr);
+}
+
+// out[m] = max over p < np of part[p][m] (blockIdx.y = 0: A's slab partials into
+// out[0 .. M), 1: g_Kuf's wave partials into out[M .. 2M)).  Workgroup: 16 rows x 16
+// partial groups (a thread takes partials g, g + 16, ... eight loads in flight), LDS.
+__global__ __launch_bounds__(256) void rowmax_fold_kernel(const float* __restrict__ pa, int npa,
+                                                          const float* __restrict__ pg, int npg, int64_t M,
+                                                          float* __restrict__ out) {
+  __shared__ float sm[16][17];
+  const int r = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t m = (int64_t)blockIdx.x * 16 + r;
+  const float* p = blockIdx.y ? pg : pa;
+  const int np = blockIdx.y ? npg : npa;
+  float v = 0.f;
+  if (m < M) {
+#pragma unroll 8
+    for (int q = g; q < np; q += 16) v = fmaxf(v, p[(int64_t)q * M + m]);
+  }
+  sm[g][r] = v;
+  __syncthreads();
+  if (threadIdx.x < 16 && m < M) {
+    float x = sm[0][r];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) x = fmaxf(x, sm[k][r]);
+    out[blockIdx.y * M + m] = x;
+  }
 }
 
 // ------------------------------------------------------------------ K4 (x6)
@@ -2928,11 +2973,15 @@ extern "C" int mgp_gram(const float* X, int64_t ldx, int64_t MI, const float* Y,
                         int64_t N, float alpha, int32_t tri, float* out, int64_t ldo, void* workspace,
                         size_t workspace_bytes, mgp_stream_t stream);
 
+int gram_f16_rowscaled(const float* X, int64_t ldx, int64_t MI, const float* Y, int64_t ldy, int64_t MJ, int64_t N,
+                       float alpha, int32_t mode, float* out, int64_t ldo, const float* xb, const float* yb,
+                       void* workspace, size_t workspace_bytes, mgp_stream_t stream);  // gram.hip
+
 constexpr int kRowSumChunks = 32;  // column chunks of row_sums_kernel
 
 namespace {
 struct CondBwdWs {  // workspace carve-up (256-B aligned pieces)
-  size_t sfr, ga0, rimg, qpart, gafr, lifr, P, LT, part, bnd, cexp, gram, total;
+  size_t sfr, ga0, rimg, qpart, gafr, lifr, P, LT, part, bnd, cexp, rmax, rpart, gram, total;
 };
 size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
@@ -2953,6 +3002,9 @@ CondBwdWs cond_bwd_layout(int64_t M, int64_t N, int32_t K) {
   w.part = o; o += al256((size_t)K * kRowSumChunks * 8);  // row_sums partials
   w.bnd = o;  o += 256;  // split-f16 bounds: max |Gv|, max |LinvT| (MGP_TRSM_BWD16)
   w.cexp = o; o += al256((size_t)((M + 127) / 128) * ldn * 4);  // gA image scales per (row tile, column)
+  w.rmax = o; o += al256((size_t)2 * M * 4);  // row maxima of A and g_Kuf (the f16 g_Lm gram)
+  // their partials: per slab of 128 n (grad_a_prep), per 64 columns (trsm_bwd16)
+  w.rpart = o; o += al256((size_t)(mgp_rows_f16_ksteps(N) / 8 + 1 + (N + 63) / 64 + 4) * M * 4);
   w.gram = o;
   size_t g = mgp_gram_x6_workspace_bytes(M, M, N, K, 2);
   g = g > mgp_gram_x6_workspace_bytes(M, M, M, K, 2) ? g : mgp_gram_x6_workspace_bytes(M, M, M, K, 2);
@@ -3139,19 +3191,26 @@ static int conditional_backward(
   const int nns = (int)mgp_rows_f16_ksteps(N);
   const int slabs = (nns + 7) / 8;
   const bool prep = f16 && lda % 4 == 0 && aligned16(A);  // else grad_a_base, split_rows_f16, gram_narrow
+  // g_Lm on f16 products with exact per-row scales (MGP_GLM_F16): the row maxima of A
+  // (grad_a_prep) and of g_Kuf (trsm_bwd16) by atomics
+  const bool glm16 = kGlmF16 && bwd16 && prep;
+  float* rmaxA = (float*)(ws + L.rmax);
+  float* rmaxG = rmaxA + M;
+  float* rpartA = glm16 ? (float*)(ws + L.rpart) : nullptr;
+  float* rpartG = glm16 ? rpartA + (int64_t)slabs * M : nullptr;
   if (prep) {
     const int rbs = kPrepRB;
     const dim3 grid((unsigned)slabs, (unsigned)((M + 32 * rbs - 1) / (32 * rbs)));
     const int qvec = (ldq % 4 == 0 && K % 4 == 0 && aligned16(q_mu)) ? 1 : 0;
     if (K <= 4)
       hipLaunchKernelGGL(grad_a_prep_kernel<4>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, nns,
-                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec);
+                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec, rpartA);
     else if (K <= 8)
       hipLaunchKernelGGL(grad_a_prep_kernel<8>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, nns,
-                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec);
+                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec, rpartA);
     else
       hipLaunchKernelGGL(grad_a_prep_kernel<16>, grid, dim3(256), 0, s, A, lda, q_mu, ldq, Gmu, Gv, ldg, M, N, K, nns,
-                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec);
+                         a_bound, gA0, ldn, rimg, qpart, rbs, qvec, rpartA);
     if ((st = launch_status())) return st;
   } else {
     const int rows = 128;
@@ -3193,7 +3252,7 @@ static int conditional_backward(
   if (bwd16)
     hipLaunchKernelGGL(trsm_bwd16_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)gAfr,
                        (const bf16x8*)LIfr, (uint32_t)img, (uint32_t)mgp_x6_lower_bytes(M, 1), nmk, nmb, nTn, M, N,
-                       g_Kuf, ldk, (const float*)cexp, ldn, (const float*)li_bound);
+                       g_Kuf, ldk, (const float*)cexp, ldn, (const float*)li_bound, rpartG);
   else
   hipLaunchKernelGGL(trsm_bwd_kernel, dim3((unsigned)(nT * nTn)), dim3(256), 0, s, (const bf16x8*)gAfr,
                      (const bf16x8*)LIfr, (uint32_t)img, (uint32_t)mgp_x6_lower_bytes(M, 1), nmk, nmb, nTn, M, N, g_Kuf,
@@ -3227,8 +3286,19 @@ static int conditional_backward(
   //    both modes: it feeds the near-cancelling Z / lengthscale / variance gradients
   //    through the Cholesky backward (split-f16 operands measured 3.6e-4 normwise on a
   //    lengthscale gradient where float32 autograd is 2.2e-4)
-  st = mgp_gram_x6(g_Kuf, ldk, 0, M, A, lda, 0, M, nullptr, 0, N, 1, -1.f, 1, g_Lm, ldgl, M * ldgl, gws, gwsb,
-                   stream);
+  //    (the C path with MGP_GLM_F16: f16 products, every row of g_Kuf and of A split at
+  //    its own exact scale -- the global-bound split was what lost the accuracy)
+  if (glm16) {
+    hipLaunchKernelGGL(rowmax_fold_kernel, dim3((unsigned)((M + 15) / 16), 2), dim3(256), 0, s, rpartA, slabs,
+                       rpartG, 4 * nTn, M, rmaxA);
+    if ((st = launch_status())) return st;
+  }
+  if (glm16)
+    st = gram_f16_rowscaled(g_Kuf, ldk, M, A, lda, M, N, -1.f, 1, g_Lm, ldgl, (const float*)rmaxG,
+                            (const float*)rmaxA, gws, gwsb, stream);
+  else
+    st = mgp_gram_x6(g_Kuf, ldk, 0, M, A, lda, 0, M, nullptr, 0, N, 1, -1.f, 1, g_Lm, ldgl, M * ldgl, gws, gwsb,
+                     stream);
   if (st) return st;
   if (prep) {  // g_q_mu from step 2's partials
     hipLaunchKernelGGL(prep_fold_kernel, dim3((unsigned)((M * K + 15) / 16)), dim3(256), 0, s, qpart, slabs, M, K,
