@@ -450,7 +450,9 @@ int mgp_conditional_backward_f16c(const void* Afr, size_t afr_bytes, const float
 /* The q_sqrt-only part of mgp_conditional_backward_f16c -- L_k's image (scale l_bound)
  * and the transposed triangles L_k^T -- into prep (mgp_conditional_backward_prep_bytes),
  * e.g. on a side stream while the forward runs, and the backward on it (two launches
- * fewer on its stream, the same results).  Prep: -1 .. -7 q_sqrt, ldqs, strideq, M, K,
+ * fewer on its stream, the same results).  t_bound (may be NULL): max |LinvT| as K3's
+ * bounded L^-T images carry it (their trailer), so the backward needs no reduction of
+ * its own for Linv's split-f16 image.  Prep: -1 .. -7 q_sqrt, ldqs, strideq, M, K,
  * l_bound, prep; prepped: as _f16c, plus -33 prep NULL, -34 prep_bytes. */
 size_t mgp_conditional_backward_prep_bytes(int64_t M, int32_t K);
 int mgp_conditional_backward_prep_f16c(const float* q_sqrt, int64_t ldqs, int64_t strideq, int64_t M, int32_t K,
@@ -463,7 +465,8 @@ int mgp_conditional_backward_f16c_prepped(const void* Afr, size_t afr_bytes, con
                                           int64_t strideg, float* g_Kuf, int64_t ldk, float* g_Lm, int64_t ldgl,
                                           double* g_var, void* workspace, size_t workspace_bytes, const void* Cfr,
                                           size_t cfr_bytes, const float* colmax, const float* l_bound,
-                                          const void* prep, size_t prep_bytes, mgp_stream_t stream);
+                                          const void* prep, size_t prep_bytes, const float* t_bound,
+                                          mgp_stream_t stream);
 
 /* Reverse mode of Lm = chol(Kuu) (models.py:141): gKuu = sym(Lm^-T Phi(Lm^T gL) Lm^-1),
  * Phi = lower triangle with halved diagonal, in float64 from the float32 L,

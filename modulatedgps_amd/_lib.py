@@ -131,7 +131,7 @@ SIGNATURES = {
                                                             c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                                                             c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64,
                                                             c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr,
-                                                            c_size, c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
+                                                            c_size, c_ptr, c_ptr, c_ptr, c_size, c_ptr, c_ptr]),
     "mgp_c_images_bytes": (c_size, [c_i64, c_i64, c_i32]),
     "mgp_colnorm_max": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_i32, c_ptr, c_ptr]),
     "mgp_expert_conditional_f16c": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64,

@@ -1743,11 +1743,12 @@ __global__ __launch_bounds__(256, 2) void trsm_bwd16_kernel(const bf16x8* __rest
 
 // out[m] = max over p < np of part[p][m] (blockIdx.y = 0: A's slab partials into
 // out[0 .. M), 1: g_Kuf's wave partials into out[M .. 2M)).  Workgroup: 16 rows x 16
-// partial groups (a thread takes partials g, g + 16, ... eight loads in flight), LDS.
-__global__ __launch_bounds__(256) void rowmax_fold_kernel(const float* __restrict__ pa, int npa,
-                                                          const float* __restrict__ pg, int npg, int64_t M,
-                                                          float* __restrict__ out) {
-  __shared__ float sm[16][17];
+// partial groups (a thread takes partials g, g + 64, ... eight loads in flight), LDS
+// (16 rows x 16 groups: 21 us per launch at c3; 64 groups: the loads' latency shared).
+__global__ __launch_bounds__(1024) void rowmax_fold_kernel(const float* __restrict__ pa, int npa,
+                                                           const float* __restrict__ pg, int npg, int64_t M,
+                                                           float* __restrict__ out) {
+  __shared__ float sm[64][17];
   const int r = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int64_t m = (int64_t)blockIdx.x * 16 + r;
   const float* p = blockIdx.y ? pg : pa;
@@ -1755,14 +1756,14 @@ __global__ __launch_bounds__(256) void rowmax_fold_kernel(const float* __restric
   float v = 0.f;
   if (m < M) {
 #pragma unroll 8
-    for (int q = g; q < np; q += 16) v = fmaxf(v, p[(int64_t)q * M + m]);
+    for (int q = g; q < np; q += 64) v = fmaxf(v, p[(int64_t)q * M + m]);
   }
   sm[g][r] = v;
   __syncthreads();
   if (threadIdx.x < 16 && m < M) {
     float x = sm[0][r];
 #pragma unroll
-    for (int k = 1; k < 16; ++k) x = fmaxf(x, sm[k][r]);
+    for (int k = 1; k < 64; ++k) x = fmaxf(x, sm[k][r]);
     out[blockIdx.y * M + m] = x;
   }
 }
@@ -3088,7 +3089,7 @@ static int conditional_backward(
     float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
     float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, mgp_stream_t stream,
     bool f16, bool x8 = false, const void* Cfr = nullptr, size_t cfr_bytes = 0, const float* colmax = nullptr,
-    const float* l_bound = nullptr, const void* qprep = nullptr) {
+    const float* l_bound = nullptr, const void* qprep = nullptr, const float* t_bound = nullptr) {
   if (!Afr) return -1;
   if (afr_bytes < mgp_x6_cols_bytes(M, N)) return -2;
   if (!A) return -3;
@@ -3140,7 +3141,8 @@ static int conditional_backward(
   const bool cpath = f16 && !x8 && Cfr;  // B-b from the forward's C_k images
   // B-d on split-f16 images (trsm_bwd16_kernel): the C path, M <= 4096
   const bool bwd16 = kTrsmBwd16 && cpath && nT <= kTrsmBwd16MaxT;
-  float* li_bound = (float*)(ws + L.bnd) + 1;
+  // max |LinvT| given (t_bound: the forward's L^-T image bound from K3) or formed here
+  float* li_bound = t_bound ? const_cast<float*>(t_bound) : (float*)(ws + L.bnd) + 1;
   float* cexp = (float*)(ws + L.cexp);
   if (cpath) {
     if (!colmax || !l_bound) return -32;
@@ -3152,7 +3154,7 @@ static int conditional_backward(
     if (!qprep)
       hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
                          ldqs, strideq, M, nmb, nmk, nfrag, Sfr, l_bound);
-    if (bwd16) {  // Linv's split-f16 image at max |LinvT| (its upper triangle)
+    if (bwd16 && !t_bound) {  // Linv's split-f16 image at max |LinvT| (its upper triangle)
       if ((st = hip_status(hipMemsetAsync(li_bound, 0, sizeof(float), s)))) return st;
       launch_absmax<2>(LinvT, ldl, (int64_t)0, M, M, M, li_bound, s);
     }
@@ -3289,7 +3291,7 @@ static int conditional_backward(
   //    (the C path with MGP_GLM_F16: f16 products, every row of g_Kuf and of A split at
   //    its own exact scale -- the global-bound split was what lost the accuracy)
   if (glm16) {
-    hipLaunchKernelGGL(rowmax_fold_kernel, dim3((unsigned)((M + 15) / 16), 2), dim3(256), 0, s, rpartA, slabs,
+    hipLaunchKernelGGL(rowmax_fold_kernel, dim3((unsigned)((M + 15) / 16), 2), dim3(1024), 0, s, rpartA, slabs,
                        rpartG, 4 * nTn, M, rmaxA);
     if ((st = launch_status())) return st;
   }
@@ -3397,14 +3399,14 @@ extern "C" int mgp_conditional_backward_f16c_prepped(
     float* g_q_mu, int64_t ldgq, float* g_q_sqrt, int64_t ldgs, int64_t strideg, float* g_Kuf, int64_t ldk,
     float* g_Lm, int64_t ldgl, double* g_var, void* workspace, size_t workspace_bytes, const void* Cfr,
     size_t cfr_bytes, const float* colmax, const float* l_bound, const void* prep, size_t prep_bytes,
-    mgp_stream_t stream) {
+    const float* t_bound, mgp_stream_t stream) {
   if (!Cfr) return -30;
   if (!prep) return -33;
   if (prep_bytes < mgp_conditional_backward_prep_bytes(M, K)) return -34;
   if (!aligned16(prep)) return MGP_ERR_ALIGN;
   return conditional_backward(Afr, afr_bytes, A, lda, q_sqrt, ldqs, strideq, q_mu, ldq, LinvT, ldl, Gmu, Gv, ldg, M,
                               N, K, g_q_mu, ldgq, g_q_sqrt, ldgs, strideg, g_Kuf, ldk, g_Lm, ldgl, g_var, workspace,
-                              workspace_bytes, stream, true, false, Cfr, cfr_bytes, colmax, l_bound, prep);
+                              workspace_bytes, stream, true, false, Cfr, cfr_bytes, colmax, l_bound, prep, t_bound);
 }
 
 // Afr from mgp_trsm_stats_f16x8 with the f32 A (all three planes): S_k A on f16 hi

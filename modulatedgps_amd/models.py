@@ -62,6 +62,7 @@ _RBF_NO_FILL = True  # the batched RBF backward overwrites gZ / g_ls (False: zer
 # training: the q_sqrt-only launches of the C-images backward (L_k's image, L_k^T) on the
 # side stream beside K3 (mgp_conditional_backward_prep_f16c; False: inside the backward)
 _COND_PREP = True
+_T_BOUND = True   # the C-images backward takes max |LinvT| from K3's bounded L^-T images (A/B: False)
 
 # The training step keeps each layer's C_k = L_k^T A images for the backward
 # (mgp_conditional_backward_f16c) while both layers' sets fit in this fraction of the
@@ -654,6 +655,7 @@ class SMGP(SGP):
         # split-f16 L^-T images: K3 folds their scale bound (max |LinvT|) into its
         # writes of the inverse, so the split needs no reduction launches
         bounded = b["x6"] and "Tfr_a" in b and "LinvT2" in b and fmt == "f16"
+        b["lt_bounded"] = bounded   # the backward takes max |LinvT| from the Tfr trailers
         sched = step_schedule() if (b["x6"] and "Tfr_a" in b) else "overlap"
         # schedule k1_in_k3: both layers' K1 as a side job of K3's step launches (batched K3)
         k1_in_k3 = (sched == "k1_in_k3" and "LinvT2" in b and self.pred_layer.kernel._x(X) is X
@@ -992,10 +994,11 @@ class SMGP(SGP):
                     cimg = (b["Cfr_" + L], b["colmax_" + L],
                             ops.image_bound(b["Lfr_" + L], M, K=layer.num_latent_gps))
                 prep = b["cprep_" + L] if cimg is not None and b.get("cprep_done") else None
+                tb = ops.image_bound(b["Tfr_" + L], M, K=1) if prep is not None and b.get("lt_bounded") and _T_BOUND else None
                 return ops.conditional_backward_x6(b["Afr_" + L], b["A32_" + L], layer.q_sqrt,
                                                    layer.q_mu, b["LinvT_" + L], G[gi], G[gi + 1], M, N,
                                                    workspace=ws, fmt=forward_image_format(True),
-                                                   c_images=cimg, prep=prep)
+                                                   c_images=cimg, prep=prep, t_bound=tb)
 
         def tail_backward(L, name, layer, g):
             with _Stage(timing, "chol_bwd"):

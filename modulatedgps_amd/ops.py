@@ -805,7 +805,7 @@ def conditional_backward_prep(q_sqrt, l_bound, out=None):
 
 
 def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None, workspace=None, fmt="x6",
-                            cross=None, c_images=None, prep=None):
+                            cross=None, c_images=None, prep=None, t_bound=None):
     """Backward of one layer's conditional (see include/mgp_hip.h): returns dict of
     g_q_mu [M, K], g_q_sqrt [K, M, M], g_Kuf [M, N], g_Lm [M, M], g_var (float64 [1]).
     fmt: format of A's image Afr ("f16": mgp_conditional_backward_f16; with cross "f8",
@@ -841,8 +841,8 @@ def conditional_backward_x6(Afr, A, q_sqrt, q_mu, LinvT, Gmu, Gv, M, N, out=None
         entry = "mgp_conditional_backward_f16c"
         args += [Cfr.data_ptr(), Cfr.numel(), colmax.data_ptr(), l_bound.data_ptr()]
         if prep is not None:   # from conditional_backward_prep(q_sqrt, l_bound) of the same q_sqrt
-            entry += "_prepped"
-            args += [prep.data_ptr(), prep.numel()]
+            entry += "_prepped"   # t_bound: max |LinvT| (e.g. image_bound of K3's bounded L^-T image)
+            args += [prep.data_ptr(), prep.numel(), t_bound.data_ptr() if t_bound is not None else None]
     elif prep is not None:
         raise ValueError("prep needs c_images (the C-images backward)")
     _lib.call(entry, *args, _stream())

@@ -195,6 +195,13 @@ def test_conditional_backward_c_images(device, N, M, K, D, ls, pattern):
     for key in g:
         if torch.is_tensor(g[key]):
             assert torch.equal(g[key], g_p[key]), key
+    # ... and with max |LinvT| handed in (t_bound, as the training step takes it from K3)
+    tb = torch.triu(LinvT[0][:, :M]).abs().max().reshape(1).contiguous()
+    g_t = ops.conditional_backward_x6(Ahr, A, qs, qmu, LinvT[0], Gmu, Gv, M, N, fmt="f16", cross="f16",
+                                      c_images=(Cfr, colmax, lb), prep=prep, t_bound=tb)
+    for key in g:
+        if torch.is_tensor(g[key]):
+            assert torch.equal(g[key], g_t[key]), key
 
 
 @pytest.mark.parametrize("M,D,ls", [(64, 2, 0.8), (200, 3, 1.0), (1024, 8, 1.0)])

@@ -165,5 +165,5 @@ def test_conditional_backward_prep_entries_check_arguments():
     wsb = lib.mgp_conditional_backward_workspace_bytes(M, N, K)
     cb = lambda cfr=c, pr=c, nb=pb: lib.mgp_conditional_backward_f16c_prepped(
         c, 1 << 30, c, 128, c, M, M * M, c, K, c, M, c, c, 128, M, N, K, c, K, c, M, M * M, c, 128, c, M, c, c, wsb,
-        cfr, 1 << 30, c, c, pr, nb, None)
+        cfr, 1 << 30, c, c, pr, nb, None, None)
     assert cb(cfr=None) == -30 and cb(pr=None) == -33 and cb(nb=pb - 1) == -34

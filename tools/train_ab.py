@@ -31,6 +31,9 @@ def main():
     if "noprep" in sys.argv[4:]:   # the C-images backward's q_sqrt launches inside it (before the prep)
         from modulatedgps_amd import models
         models._COND_PREP = False
+    if "notb" in sys.argv[4:]:   # max |LinvT| reduced inside the backward (before the K3 bound hand-over)
+        from modulatedgps_amd import models
+        models._T_BOUND = False
     if "adamper" in sys.argv[4:]:   # one Adam launch per parameter block (before round 5's set)
         from modulatedgps_amd import training
         training._ADAM_SET = False
