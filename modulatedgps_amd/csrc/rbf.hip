@@ -134,6 +134,11 @@ static int rbf_launch(const float* X, int64_t ldx, const float* Z, int64_t ldz, 
 // stride -- the strided dword loads cost the address unit 8x the cycles and
 // bounded this kernel.
 constexpr int kRbfRows = 2;  // rows of Z per wave
+#ifndef MGP_RBF_PACKED
+#define MGP_RBF_PACKED 1
+#endif
+constexpr bool kRbfPacked = MGP_RBF_PACKED;
+typedef float floatx2v __attribute__((ext_vector_type(2)));
 // one workgroup's rows (blockIdx.x) over the points [nb, ne); part: this chunk's [M][NS]
 template <int DMAX, bool VEC>
 __device__ __forceinline__ void rbf_bwd_rows_body(const float* __restrict__ X, int64_t ldx,
@@ -176,6 +181,35 @@ __device__ __forceinline__ void rbf_bwd_rows_body(const float* __restrict__ X, i
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) g[r] = (m0 + r < M) ? gK[(m0 + r) * ldg + n] : 0.f;
+    if constexpr (kRbfPacked && DMAX % 2 == 0) {
+      // coordinate pairs on packed f32 VALU ops (v_pk_add / v_pk_mul / v_pk_fma_f32):
+      // half the instructions of the per-coordinate terms
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        floatx2v dx[DMAX / 2], qv = {0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < DMAX / 2; ++p) {
+          dx[p] = floatx2v{x[2 * p], x[2 * p + 1]} - floatx2v{z[r][2 * p], z[r][2 * p + 1]};
+          qv = floatx2v{hc2[2 * p], hc2[2 * p + 1]} * dx[p] * dx[p] + qv;
+        }
+        const float wv = g[r] * (var * __expf(qv[0] + qv[1]));
+        acc[r][0] += wv;
+        const floatx2v w2 = {wv, wv};
+#pragma unroll
+        for (int p = 0; p < DMAX / 2; ++p) {
+          const floatx2v t = w2 * dx[p];
+          floatx2v a1 = {acc[r][1 + 2 * p], acc[r][2 + 2 * p]};
+          floatx2v a2 = {acc[r][1 + DMAX + 2 * p], acc[r][2 + DMAX + 2 * p]};
+          a1 += t;
+          a2 = t * dx[p] + a2;
+          acc[r][1 + 2 * p] = a1[0];
+          acc[r][2 + 2 * p] = a1[1];
+          acc[r][1 + DMAX + 2 * p] = a2[0];
+          acc[r][2 + DMAX + 2 * p] = a2[1];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float dx[DMAX], q = 0.f;
