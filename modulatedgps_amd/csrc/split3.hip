@@ -690,6 +690,11 @@ __device__ __forceinline__ void x6_mainloop16(floatx4v (&acc)[8][4], bf16x8 (*sL
 // (the B-layout of the images K4 writes); a fragment's lane position takes
 // 8 rows from two lanes of the 16x16 accumulator layout (one exchange across the lane halves).
 // One item (workgroup index b of a launch of `grid` items) of the split-f16 K5.
+// C_k images (training) with non-temporal stores (MGP_C_NT)
+#ifndef MGP_C_NT
+#define MGP_C_NT 1
+#endif
+constexpr bool kCntStores = MGP_C_NT;
 template <bool COUT>
 __device__ __forceinline__ void expert_cond16_item(bf16x8 (*sL)[4 * 2 * 3 * 64], int b, int grid,
                                                    const bf16x8* __restrict__ Afr, const bf16x8* __restrict__ Lfr,
@@ -725,7 +730,20 @@ __device__ __forceinline__ void expert_cond16_item(bf16x8 (*sL)[4 * 2 * 3 * 64],
           v[r] = x0 * cmul;
           v[4 + r] = x1 * cmul;
         }
-        store_split_f16(Ck + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, 1.f);
+        bf16x8* dst = Ck + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos;
+        if constexpr (kCntStores) {  // read back only by the backward, long after: past L2
+          halfx8 h, l;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const _Float16 hi = (_Float16)v[j];
+            h[j] = hi;
+            l[j] = (_Float16)(v[j] - (float)hi);
+          }
+          __builtin_nontemporal_store(__builtin_bit_cast(bf16x8, h), dst);
+          __builtin_nontemporal_store(__builtin_bit_cast(bf16x8, l), dst + 64);
+        } else {
+          store_split_f16(dst, v, 1.f);
+        }
       }
   }
   // sum over the 128 rows of C^2 per column: 8 blocks x 4 registers, then the 4 lane groups
