@@ -11,9 +11,11 @@ both KLs) over one batch of synthetic input already resident in HBM, with
 fresh in-kernel Philox noise per step.  Workload (N = 1): BASELINE config 3,
 N = 65536, M = 1024, K = 8, D = 8, fp32, per GPU.  Multi-GPU: data-parallel
 over N, one process per GPU (`--gpus N` without torchrun starts the N ranks
-itself).  `--scaling weak` (default): every rank holds its own 65536-point
-shard of the global batch; `--scaling strong`: BASELINE config c4, c3's
-N = 65536 split over the ranks.  Kuu/Cholesky/KL are replicated; ONE RCCL
+itself).  `--scaling strong` (default): BASELINE config c4, c3's N = 65536
+split over the ranks (N / world points per GPU, one whole-config ELBO per
+step); `--scaling weak`: every rank holds its own 65536-point shard of the
+global batch.  `--config c4r` is c4's per-rank shape (N = 8192) on one GPU,
+the single-GPU bound of the 8-GPU point.  Kuu/Cholesky/KL are replicated; ONE RCCL
 all-reduce of the data-term scalar per step.  `--layout expert`: the
 north_star layout (experts sharded, one all_to_all).  Timing: W warmup steps,
 then the K timed steps as `--repeats` blocks (default 5 x 50), each bracketed by
@@ -38,6 +40,7 @@ CONFIGS = {
     # name: (N per GPU, M, K, D, lengthscale, S)
     "c2": (8192, 256, 4, 2, 0.15, 25),
     "c3": (65536, 1024, 8, 8, 1.0, 25),
+    "c4r": (8192, 1024, 8, 8, 1.0, 25),   # c4's per-rank shard: c3's N over 8 GPUs
     "c5": (262144, 2048, 16, 16, 2.0, 25),
 }
 PEAK_F32_MFMA = 157.3e12      # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
@@ -56,9 +59,9 @@ def parse():
     ap.add_argument("--repeats", type=int, default=5,
                     help="the timed steps are split into this many blocks, each bracketed by barrier + "
                          "synchronize; value = the median block rate (SURVEY §8d: median of 5 repeats)")
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
-                    help="multi-GPU data layout: 'weak' = N points per GPU (the default); 'strong' = BASELINE "
-                         "config c4, the config's N sharded over the ranks (N / world per GPU)")
+    ap.add_argument("--scaling", default="strong", choices=("weak", "strong"),
+                    help="multi-GPU data layout: 'strong' (the default) = BASELINE config c4, the config's N "
+                         "sharded over the ranks (N / world per GPU); 'weak' = N points per GPU")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--planes", type=int, default=3, choices=(1, 2, 3),
                     help="bf16 planes per operand in K5 (3: f32-accurate x6, the default; 2 / 1: the "
@@ -486,7 +489,10 @@ def main():
         modes = k5_modes_leg(elbo_step, args, fmt)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, tuple(args.cpu_sample))
+        sizes = tuple(args.cpu_sample)
+        if cfg[0] < max(sizes):   # c4r / c2: sample at and below the config's own N
+            sizes = (cfg[0] // 4, cfg[0])
+        cpu = cpu_baseline(cfg, sizes)
     step_flops = 2 * (2.0 * M ** 3 / 3.0 + (K + 1.0) * M * M * N + N * M * (3 * D + 4.0))
     if rank == 0:
         out = {
@@ -494,7 +500,9 @@ def main():
                        f"ELBO steps/sec (N={CONFIGS[args.config][0]}, M={M}, K={K}); Kuf HBM GB/s vs roofline"),
             "value": value, "unit": "ELBO steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong" if (expert or strong) else "weak", "vs_baseline": None,
+            # N = 1: both layouts are the same run; it is reported under the chosen series
+            "scaling": "strong" if (expert or strong or (world == 1 and args.scaling == "strong")) else "weak",
+            "vs_baseline": None,
             "repeats": len(blocks), "steps_per_repeat": [n for n, _ in blocks], "block_rates": block_rates,
             "dtype": (("f32 (split-f16 + e4m3 cross terms)" if f16x8 else "f32 (split-f16, 22-bit operands)")
                       if f16 else {3: "f32 (split-bf16 x6, f32-exact operands)", 2: "f32/bf16x3 mixed",

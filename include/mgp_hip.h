@@ -155,13 +155,14 @@ int mgp_trsm_stats(const float* LinvT, int64_t ldl, const float* Kuf, int64_t ld
  * tail of GPflow base_conditional (models.py:141-143; Knn = var from
  * models.py:133).  q_sqrt: [K][M][ldqs] at element stride strideq.
  * fmean, fvar: [K][ldf] (expert-major; ldf >= N).  Workspace (per-row-tile
- * partial sums): mgp_expert_workspace_bytes(M, N, K). */
+ * partial sums): mgp_expert_workspace_bytes(M, N, K).  (Exact-f32 MFMA products;
+ * the default-format entry of this operation is mgp_expert_conditional, below.) */
 size_t mgp_expert_workspace_bytes(int64_t M, int64_t N, int32_t K);
-int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
-                           int64_t strideq, const float* stats, int64_t lds,
-                           const float* variance, int64_t M, int64_t N, int32_t K, float* fmean,
-                           float* fvar, int64_t ldf, void* workspace, size_t workspace_bytes,
-                           mgp_stream_t stream);
+int mgp_expert_conditional_f32(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
+                               int64_t strideq, const float* stats, int64_t lds,
+                               const float* variance, int64_t M, int64_t N, int32_t K, float* fmean,
+                               float* fvar, int64_t ldf, void* workspace, size_t workspace_bytes,
+                               mgp_stream_t stream);
 
 /* ---------------------------------------------------------------- K5, split-bf16
  * The same K-expert conditional on the bf16 matrix cores at f32 accuracy:
@@ -174,7 +175,7 @@ int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int
  *   mgp_split_cols_x6:  A [M][lda] -> Afr (mgp_x6_cols_bytes(M, N) bytes);
  *       on the ELBO path K4 (mgp_trsm_stats_x6) writes Afr directly.
  * mgp_expert_conditional_x6 then produces fmean/fvar exactly as
- * mgp_expert_conditional.  Images must be < 4 GiB.  Workspace:
+ * mgp_expert_conditional_f32.  Images must be < 4 GiB.  Workspace:
  * mgp_expert_x6_workspace_bytes(M, N, K). */
 size_t mgp_x6_lower_bytes(int64_t M, int32_t K);    /* also the LinvT image: K = 1 */
 size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
@@ -697,6 +698,58 @@ int mgp_adam_step_set(int32_t n, float* const* theta, float* const* u, const voi
                       const int32_t* grad_is_double, const int64_t* ldg, float* const* m1, float* const* m2,
                       const int64_t* rows, const int64_t* cols, const int64_t* ld, float lr, float beta1,
                       float beta2, float eps, int64_t t, float grad_sign, mgp_stream_t stream);
+
+
+/* ---------------------------------------------------------------- the §8(b) front
+ * One entry per reference operation in the default formats: what a
+ * binding from another host language needs.  They are thin hosts over the kernels
+ * above (csrc/front.hip); the format-specific entries above are the expert surface
+ * the Python host uses for its fused, stream-overlapped ELBO step.  Every workspace
+ * is sized by mgp_workspace_bytes(op, M, N, K) (0 = none needed; for
+ * MGP_OP_RBF_BACKWARD pass D as K) and must be 16-B aligned. */
+enum {
+  MGP_OP_RBF_KUU_JITTER = 1,
+  MGP_OP_RBF_KUF = 2,
+  MGP_OP_POTRF_LOWER = 3,
+  MGP_OP_TRSM_LLN = 4,
+  MGP_OP_EXPERT_CONDITIONAL = 5,
+  MGP_OP_GAUSS_KL_WHITE = 6,
+  MGP_OP_ELBO_TERMS = 7,
+  MGP_OP_ELBO_TERMS_BACKWARD = 8,
+  MGP_OP_CONDITIONAL_BACKWARD = 9,
+  MGP_OP_CHOL_BACKWARD = 10,
+  MGP_OP_RBF_BACKWARD = 11
+};
+size_t mgp_workspace_bytes(int32_t op, int64_t M, int64_t N, int32_t K);
+/* Kuu = K(Z, Z) + jitter I in float32 (covariances.Kuu, models.py:135); same as
+ * mgp_rbf_kuu.  The ELBO path builds Kuu in float64 inside the factorisation
+ * (mgp_kuu_potrf_trtri): a float32 Kuu carries cond(Kuu) * 2^-24 into L. */
+int mgp_rbf_kuu_jitter(const float* Z, int64_t ldz, int64_t M, int32_t D, const float* variance,
+                       const float* lengthscales, int32_t n_ls, float jitter, float* Kuu, int64_t ldk,
+                       mgp_stream_t stream);
+/* In place: A [M][lda] (lower triangle read) <- L = chol(A), zeros above the
+ * diagonal; LinvT (nullable, [M][ldl]) <- (L^-1)^T, the form mgp_trsm_lln takes
+ * L in.  Factorised in float64 (K3).  info (device int32) = 0 or the 1-based column
+ * of the first non-positive pivot (tf.linalg.cholesky at models.py:141 raises
+ * there).  lda, ldl % 4 == 0. */
+int mgp_potrf_lower(float* A, int64_t lda, int64_t M, float* LinvT, int64_t ldl, int32_t* info,
+                    void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+/* In place: B [M][ldb] <- L^-1 B, the triangular_solve(Lm, Kmn, lower=True) of
+ * base_conditional (models.py:141-143), with L given as LinvT = (L^-1)^T from
+ * mgp_potrf_lower (K4 as a triangular GEMM on exact three-plane bf16 images:
+ * f32-accurate for any right-hand side). */
+int mgp_trsm_lln(const float* LinvT, int64_t ldl, int64_t M, float* B, int64_t ldb, int64_t N,
+                 void* workspace, size_t workspace_bytes, mgp_stream_t stream);
+/* The K-expert whitened conditional from A = L^-1 Kuf (models.py:141-143):
+ *   fmean[k][n] = sum_m A[m,n] q_mu[m,k]
+ *   fvar[k][n]  = var - sum_m A[m,n]^2 + sum_m' (sum_{m>=m'} L_k[m,m'] A[m,n])^2
+ * with L_k = band_part(q_sqrt[k], -1, 0), in the default split-f16 format (K5 on
+ * f16 MFMAs, 22-bit operands).  q_mu [M][ldq >= K]; q_sqrt [K][M][ldqs] at element
+ * stride strideq; fmean, fvar [K][ldf] (expert-major).  K <= 32. */
+int mgp_expert_conditional(const float* A, int64_t lda, const float* q_mu, int64_t ldq,
+                           const float* q_sqrt, int64_t ldqs, int64_t strideq, const float* variance,
+                           int64_t M, int64_t N, int32_t K, float* fmean, float* fvar, int64_t ldf,
+                           void* workspace, size_t workspace_bytes, mgp_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -65,9 +65,17 @@ SIGNATURES = {
     "mgp_trsm_stats": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                       c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "mgp_expert_workspace_bytes": (c_size, [c_i64, c_i64, c_i32]),
-    "mgp_expert_conditional": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr,
-                                              c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
-                                              c_ptr]),
+    "mgp_expert_conditional_f32": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr,
+                                                  c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size,
+                                                  c_ptr]),
+    # the SURVEY §8(b) front (csrc/front.hip)
+    "mgp_workspace_bytes": (c_size, [c_i32, c_i64, c_i64, c_i32]),
+    "mgp_rbf_kuu_jitter": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_i32, ctypes.c_float,
+                                          c_ptr, c_i64, c_ptr]),
+    "mgp_potrf_lower": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+    "mgp_trsm_lln": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_size, c_ptr]),
+    "mgp_expert_conditional": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64,
+                                              c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "mgp_trsm_stats_x6": (ctypes.c_int, [c_ptr, c_size, c_ptr, c_size, c_i64, c_i64, c_ptr, c_i64, c_i32,
                                          c_ptr, c_size, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "mgp_kl_grad": (ctypes.c_int, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32, ctypes.c_double, c_ptr,

@@ -31,6 +31,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "kuf_image.hpp"
@@ -1387,11 +1388,23 @@ extern "C" size_t mgp_x6_cols_bytes(int64_t M, int64_t N);
 // Share of the image blocks per step launch j: proportional to the CUs the launch's tile
 // workgroups leave idle (one workgroup per CU: the step kernel's LDS), at least an eighth
 // of the CUs each.
-static void kuf_side_split(int nb, int batch, int64_t total, std::vector<int64_t>& beg, std::vector<int>& nwg) {
-  int cus = 0, dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    cus = 256;
+// CU count of the device the stream runs on, cached per device (the attribute query
+// costs a driver call on every K3 launch otherwise).
+static int stream_device_cus(hipStream_t s) {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev < 0 || dev >= 64) dev = 0;
+  int cus = cache[dev].load(std::memory_order_relaxed);
+  if (cus > 0) return cus;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  cache[dev].store(cus, std::memory_order_relaxed);
+  return cus;
+}
+
+static void kuf_side_split(int nb, int batch, int64_t total, std::vector<int64_t>& beg, std::vector<int>& nwg,
+                           hipStream_t s) {
+  const int cus = stream_device_cus(s);
   const int steps = nb - 1;
   std::vector<double> idle(steps);
   double sum = 0.0;
@@ -1406,7 +1419,9 @@ static void kuf_side_split(int nb, int batch, int64_t total, std::vector<int64_t
     acc += idle[j];
     beg[j + 1] = j + 1 == steps ? total : std::min<int64_t>(total, (int64_t)(total * (acc / sum) + 0.5));
     const int64_t cnt = beg[j + 1] - beg[j];
-    nwg[j] = (int)std::min<int64_t>((cnt + 1) / 2, (int64_t)idle[j]);
+    // at least one workgroup for a step that was given image blocks (idle[j] can be
+    // < 1 on a device or partition with fewer than 8 CUs)
+    nwg[j] = cnt > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>((cnt + 1) / 2, (int64_t)idle[j])) : 0;
   }
 }
 
@@ -1434,7 +1449,7 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
       a.kfr[b] = (bf16x8*)kj->Kfr[b];
       a.kbound[b] = (float*)((char*)kj->Kfr[b] + mgp_x6_cols_bytes(a.M, kj->N) - 256);  // image trailer
     }
-    if (a.nb >= 2) kuf_side_split(a.nb, batch, batch * a.kblocks, kbeg, knwg);
+    if (a.nb >= 2) kuf_side_split(a.nb, batch, batch * a.kblocks, kbeg, knwg, s);
   }
   hipLaunchKernelGGL(chol_prep, dim3(a.nb * a.nb + 1, batch), block, 0, s, a);
   int st = launch_status();

@@ -158,6 +158,13 @@ __device__ __forceinline__ void kuf_image_block(const KufImageArgs& a, int64_t b
           v[j] = __builtin_amdgcn_exp2f(-acc[8 * half + j]) * mult;
           if constexpr (RAGGED)
             if (m0 + 32 * i + acc_row(8 * half + j, lane) >= a.M) v[j] = 0.f;
+          // the split below must see v as the rounded f32 value: without this the
+          // compiler contracts the multiply into the hi / lo conversions
+          // (v_fma_mix{lo,hi}_f16 on the unrounded product beside v_cvt_pk_f16_f32 of
+          // the rounded one), which left the lo plane inconsistent with hi whenever
+          // mult is not a power of two (kernel variance 0.1: Kuf image off by half an
+          // f16 ulp of hi, 3e-4 of the maximum, tests/diag_f16_images.py)
+          asm volatile("" : "+v"(v[j]));
         }
         store_fragment<F16, POL>(a.Kfr + ((nb * a.nmk + 2 * mb + half) * 3) * 64 + lane, v);
       }

@@ -527,7 +527,7 @@ static int launch_expert(const float* A, int64_t lda, const float* q_sqrt, int64
   return mgp_launch_cond_finalize(stats, lds, nTm, part, ldp, nTm, variance, N, K, fmean, fvar, ldf, s);
 }
 
-extern "C" int mgp_expert_conditional(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
+extern "C" int mgp_expert_conditional_f32(const float* A, int64_t lda, const float* q_sqrt, int64_t ldqs,
                                       int64_t strideq, const float* stats, int64_t lds,
                                       const float* variance, int64_t M, int64_t N, int32_t K,
                                       float* fmean, float* fvar, int64_t ldf, void* workspace,

@@ -4,23 +4,20 @@ Drop-in counterparts of MixtureGPs/models.py (same class names, constructor
 arguments and method names).  The SMGP ELBO hot path
 (SMGP._build_likelihood, models.py:69-79) runs as:
 
-  per layer (pred, assign):                         reference call site
-    K2 mgp_rbf_kuu          Kuu + jitter I          models.py:135
-    K3 mgp_potrf_trtri      L, L^-1 (both layers    models.py:141 (cholesky)
-                            batched in one sweep)
-    K1 mgp_rbf_kuf          Kuf [M, N]              models.py:139
-    (default "x6" mode: K1 writes Kuf as a split-bf16 image, K4/K5 run on the
-     bf16 matrix cores with f32 accuracy -- csrc/split3.hip)
-    K1 mgp_rbf_kuf_x6       Kuf image               models.py:139
-       mgp_split_upper_x6 / mgp_split_lower_x6   images of L^-T and tril(q_sqrt)
-    K4 mgp_trsm_stats_x6    A image + stats         models.py:141-143 (triangular_solve, A^T q_mu)
-    K5 mgp_expert_conditional_x6  fmean, fvar [K, N]  models.py:141-143 (LTA, fvar)
-    (forward evaluations, config expert_format "f16" = the default: the same chain
-     on split-f16 images, K1 mgp_rbf_kuf_f16, mgp_split_upper_f16 /
-     mgp_split_lower_f16, K4 mgp_trsm_stats_f16, K5 mgp_expert_conditional_f16)
-    (config.set_conditional_mode("f32"): K1 mgp_rbf_kuf + K4 mgp_trsm_stats +
-     K5 mgp_expert_conditional on the exact-f32 MFMA instead)
-    K7 mgp_gauss_kl_white   KL                      models.py:79 (prior_kl)
+  both layers (pred, assign) at once, default split-f16 format:   reference call site
+    K2+K3 mgp_kuu_potrf_trtri_kuf   Kuu + jitter I built in     models.py:135, 141 (cholesky)
+                                    float64, L and L^-1; the
+                                    step launches also write
+    K1                              both layers' Kuf images     models.py:139
+          mgp_split_upper_f16_bounded_batch   L^-T images
+          mgp_qsqrt_images_kl_f16_batch       tril(q_sqrt) images + K7 KL   models.py:79, 141-143
+    K4 mgp_trsm_stats_f16_batch     A image + stats             models.py:141-143 (triangular_solve, A^T q_mu)
+    K5 mgp_expert_conditional_f16_batch  fmean, fvar [K, N]     models.py:141-143 (LTA, fvar)
+    (config expert_format "x6": the same chain on exact split-bf16 images, six bf16
+     products per f32 product -- mgp_rbf_kuf_x6, mgp_split_upper_x6 / _lower_x6,
+     mgp_trsm_stats_x6, mgp_expert_conditional_x6 -- csrc/split3.hip;
+     config.set_conditional_mode("f32"): mgp_rbf_kuf + mgp_trsm_stats +
+     mgp_expert_conditional_f32 on the exact-f32 MFMA)
   K6 mgp_elbo_terms         sum_n lse_s(...)        models.py:55-67,73-76
   mgp_elbo_combine          ELBO scalar             models.py:76,79
 
@@ -681,7 +678,11 @@ class SMGP(SGP):
             pf, pa = self.pred_layer, self.assign_layer
             # split-f16: both layers' tril(q_sqrt) images and KL terms in three launches
             # (mgp_qsqrt_images_kl_f16_batch) instead of five per layer, beside K3's chain
-            q_batch = _QS_BATCH and fmt == "f16" and pf.q_mu.shape == pa.q_mu.shape and "Lfr_f" in b
+            # (the batch entry also needs equal q_mu leading dimensions and q_sqrt ld / stride(0),
+            # else the per-layer launches run)
+            q_batch = (_QS_BATCH and fmt == "f16" and pf.q_mu.shape == pa.q_mu.shape and "Lfr_f" in b
+                       and pf.q_mu.stride() == pa.q_mu.stride()
+                       and pf.q_sqrt.stride() == pa.q_sqrt.stride())
 
             def side_work():
                 for L, layer in layers:

@@ -372,7 +372,7 @@ def expert_conditional(A, q_sqrt, stats, variance, fmean=None, fvar=None, worksp
     nbytes = _lib.load().mgp_expert_workspace_bytes(M, N, K)
     if workspace is None or workspace.numel() < nbytes:
         workspace = _ws(nbytes, dev)
-    _lib.call("mgp_expert_conditional", A.data_ptr(), _ld(A), q_sqrt.data_ptr(), _ld(q_sqrt),
+    _lib.call("mgp_expert_conditional_f32", A.data_ptr(), _ld(A), q_sqrt.data_ptr(), _ld(q_sqrt),
               q_sqrt.stride(0), stats.data_ptr(), _ld(stats), variance.data_ptr(), M, N, K,
               fmean.data_ptr(), fvar.data_ptr(), _ld(fmean), workspace.data_ptr(),
               workspace.numel(), _stream())
@@ -706,9 +706,19 @@ class AdamSet:
 
     def step(self, grads, t, lr, beta1=0.9, beta2=0.999, eps=1e-7, grad_sign=-1.0):
         """grads: one 2-D gradient per block, in order (float32 or float64)."""
-        for gr, s in zip(grads, self.shapes):
-            if gr.shape[-1] != s[1]:
-                raise ValueError("gradient / parameter shape mismatch")
+        if len(grads) != self.n:
+            raise ValueError(f"AdamSet.step takes {self.n} gradients, got {len(grads)}")
+        dev = self._keep[0][0].device
+        for j, (gr, s) in enumerate(zip(grads, self.shapes)):
+            # the kernel reads rows x cols at the gradient's leading dimension: every block must
+            # match its parameter's shape exactly, be float32 / float64, row-contiguous and on
+            # the parameters' device
+            if tuple(gr.shape) != s:
+                raise ValueError(f"gradient {j}: shape {tuple(gr.shape)} != parameter shape {s}")
+            if gr.dtype not in (torch.float32, torch.float64):
+                raise ValueError(f"gradient {j}: dtype {gr.dtype} (float32 or float64 expected)")
+            if gr.numel() and (gr.stride(-1) != 1 or gr.device != dev):
+                raise ValueError(f"gradient {j}: must be row-contiguous on {dev}")
         _lib.call("mgp_adam_step_set", self.n, self.theta, self.u, self._P(*[gr.data_ptr() for gr in grads]),
                   self._I32(*[int(gr.dtype == torch.float64) for gr in grads]), self._I64(*[_ld(gr) for gr in grads]),
                   self.m1, self.m2, self.rows, self.cols, self.ld, float(lr), float(beta1), float(beta2), float(eps),

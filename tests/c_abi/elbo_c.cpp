@@ -8,6 +8,7 @@
 // q_mu[M][K], q_sqrt[K][M][M]; then lik_var[K], z[S][N][K], u[S][N][K].
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -66,10 +67,13 @@ void* dev_bytes(size_t n) {
 
 int main(int argc, char** argv) {
   // --batched: both layers' K4 and K5 through mgp_trsm_stats_f16_batch /
-  // mgp_expert_conditional_f16_batch (per-layer images), else one call per layer
+  // mgp_expert_conditional_f16_batch (per-layer images), else one call per layer;
+  // --front: the SURVEY §8(b) names only (mgp_rbf_kuu_jitter, mgp_potrf_lower,
+  // mgp_rbf_kuf, mgp_trsm_lln, mgp_expert_conditional, mgp_gauss_kl_white)
   const bool batched = argc == 3 && std::string(argv[2]) == "--batched";
-  if (argc != 2 && !batched) {
-    std::fprintf(stderr, "usage: %s problem.bin [--batched]\n", argv[0]);
+  const bool front = argc == 3 && std::string(argv[2]) == "--front";
+  if (argc != 2 && !batched && !front) {
+    std::fprintf(stderr, "usage: %s problem.bin [--batched | --front]\n", argv[0]);
     return 1;
   }
   std::FILE* f = std::fopen(argv[1], "rb");
@@ -112,9 +116,31 @@ int main(int argc, char** argv) {
     dqs[l] = to_device(qs[l].data(), M, M, ldm, K);  // [K][M][ldm]
   }
 
-  // K2 + K3: Kuu of both layers (float64) and its Cholesky + inverse in one batched sweep
   float* LinvT = (float*)dev_bytes(sizeof(float) * 2 * M * ldm);
   int32_t* info = (int32_t*)dev_bytes(2 * sizeof(int32_t));
+  float *fmean[2], *fvar[2];
+  double* kl = (double*)dev_bytes(2 * sizeof(double));
+  if (front) {
+    size_t wsb = 0;
+    for (int32_t op : {MGP_OP_POTRF_LOWER, MGP_OP_TRSM_LLN, MGP_OP_EXPERT_CONDITIONAL, MGP_OP_GAUSS_KL_WHITE})
+      wsb = std::max(wsb, mgp_workspace_bytes(op, M, N, K));
+    void* ws = dev_bytes(wsb);
+    float* Kuu = (float*)dev_bytes(sizeof(float) * M * ldm);
+    float* A = (float*)dev_bytes(sizeof(float) * M * ldn);
+    for (int l = 0; l < 2; ++l) {
+      fmean[l] = (float*)dev_bytes(sizeof(float) * K * ldn);
+      fvar[l] = (float*)dev_bytes(sizeof(float) * K * ldn);
+      float* lt = LinvT + l * M * ldm;
+      CHECK_MGP(mgp_rbf_kuu_jitter(dZ[l], D, M, (int32_t)D, dvar[l], dls[l], 1, 1e-6f, Kuu, ldm, s));
+      CHECK_MGP(mgp_potrf_lower(Kuu, ldm, M, lt, ldm, info + l, ws, wsb, s));
+      CHECK_MGP(mgp_rbf_kuf(dX, D, dZ[l], D, N, M, (int32_t)D, dvar[l], dls[l], 1, A, ldn, s));
+      CHECK_MGP(mgp_trsm_lln(lt, ldm, M, A, ldn, N, ws, wsb, s));
+      CHECK_MGP(mgp_expert_conditional(A, ldn, dqmu[l], K, dqs[l], ldm, M * ldm, dvar[l], M, N, K, fmean[l], fvar[l],
+                                       ldn, ws, wsb, s));
+      CHECK_MGP(mgp_gauss_kl_white(dqmu[l], K, dqs[l], ldm, M * ldm, M, K, kl + l, ws, wsb, s));
+    }
+  } else {
+  // K2 + K3: Kuu of both layers (float64) and its Cholesky + inverse in one batched sweep
   const size_t cwb = mgp_chol_workspace_bytes(M, 2);
   void* cws = dev_bytes(cwb);
   const float* Zs[2] = {dZ[0], dZ[1]};
@@ -131,8 +157,7 @@ int main(int argc, char** argv) {
   const size_t kwb = mgp_kl_workspace_bytes(M, K);
   void* kws = dev_bytes(kwb);
   void *Kfr[2], *Afr[2], *Tfr[2], *Lfr[2], *xws[2];
-  float *stats[2], *fmean[2], *fvar[2];
-  double* kl = (double*)dev_bytes(2 * sizeof(double));
+  float* stats[2];
   for (int l = 0; l < 2; ++l) {
     Kfr[l] = dev_bytes(colb);
     Afr[l] = dev_bytes(colb);
@@ -165,6 +190,8 @@ int main(int argc, char** argv) {
     CHECK_MGP(mgp_expert_conditional_f16_batch(2, cA, colb, cL, lowb, st, ldn, v, M, N, K, fmean, fvar, ldn, xws, xwb,
                                                nullptr, 0, nullptr, s));
   }
+
+  }   // (fused chain)
 
   // K6 with the explicit noise, then the scalar ELBO
   const size_t ewb = mgp_elbo_workspace_bytes(N);

@@ -69,3 +69,20 @@ def decode_cols_image(img, M, N):
     out = np.zeros((Mp, Np))
     out[np.broadcast_to(rows, f.shape), np.broadcast_to(cols, f.shape)] = f
     return out[:M, :N]
+
+
+def decode_cols_f16(img, M, N, bound):
+    """Split-f16 column image (planes 0 / 1 = fp16 hi / lo of x 2^e, e = 13 - ilogb(bound);
+    modulatedgps_amd/csrc/mgp_common.hpp) -> float64 [M, N] = (hi + lo) 2^-e."""
+    Mp, Np = -(-M // 128) * 128, -(-N // 256) * 256
+    nb, nmk = Np // 32, Mp // 16
+    u = img.detach().cpu().numpy().view(np.float16)[: nb * nmk * 3 * 64 * 8].reshape(nb, nmk, 3, 64, 8)
+    e = 13 - int(np.floor(np.log2(bound)))
+    f = (u[:, :, 0].astype(np.float64) + u[:, :, 1].astype(np.float64)) * 2.0 ** -e
+    lane, j = np.arange(64), np.arange(8)
+    kp = (j[None, :] & 3) + 8 * (j[None, :] >> 2) + 4 * (lane[:, None] >> 5)
+    rows = 16 * np.arange(nmk)[None, :, None, None] + kp[None, None]
+    cols = 32 * np.arange(nb)[:, None, None, None] + (lane & 31)[None, None, :, None]
+    out = np.zeros((Mp, Np))
+    out[np.broadcast_to(rows, f.shape), np.broadcast_to(cols, f.shape)] = f
+    return out[:M, :N]

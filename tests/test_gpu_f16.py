@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from oracle import cpu_ref as R
-from tests.helpers import build_model, dev_noise, load_golden, normwise, params_from_golden, to_np
+from tests.helpers import build_model, decode_cols_f16, dev_noise, load_golden, normwise, params_from_golden, to_np
 
 pytestmark = pytest.mark.gpu
 
@@ -285,3 +285,65 @@ def test_split_upper_bounded_batch_bit_identical(device, M):
     torch.cuda.synchronize()
     for b in range(2):
         assert torch.equal(got[b], ref[b])
+
+
+@pytest.mark.parametrize("var", [0.1, 0.3, 0.5])
+def test_kuf_f16_image_any_variance(device, var):
+    """K1's split-f16 Kuf image at kernel variances that are not powers of two (the
+    per-lane multiplier var * 2^e then rounds), by its own launch (mgp_rbf_kuf_f16) and
+    as the side job of K3's step launches (mgp_kuu_potrf_trtri_kuf, the ELBO step's
+    default; bit-identical to it): hi + lo at f32 class against float64 Kuf.
+    Regression (round 6): the compiler had contracted that multiply into the hi / lo
+    conversions (v_fma_mix*_f16 beside v_cvt_pk_f16_f32 of the rounded product), so lo
+    did not belong to the stored hi -- at variance 0.1 the image was 2.3e-6 off
+    normwise and 3e-4 of the maximum (f32 class: 2.7e-7), which made the assignment
+    layer's fmean / fvar 7x less accurate than x6 (its kernel variance is 0.1) and the
+    training gradient of that layer up to 12x worse than float32 autograd."""
+    from modulatedgps_amd import ops
+    N, M, D = 4096, 256, 8
+    X, _, p = R.synthetic_problem(N, M, 1, D, 1.0, state="init", S=1)
+    Z = p.pred["Z"]
+    X32, Z32 = X.astype(np.float32), Z.astype(np.float32)
+    Xd, Zd = _t(X32, device), _t(Z32, device)
+    vt = torch.tensor([var], dtype=torch.float32, device=device)
+    lt = torch.tensor([1.0], dtype=torch.float32, device=device)
+    ref = R.rbf_K(Z32.astype(np.float64), X32.astype(np.float64), float(np.float32(var)), 1.0)
+    img = ops.rbf_kuf_x6(Xd, Zd, vt, lt, fmt="f16")
+    side = torch.zeros_like(img)
+    ops.kuu_potrf_trtri([Zd], [vt], [lt], 1e-6, kuf=(Xd, [side], "f16"))
+    torch.cuda.synchronize()
+    assert torch.equal(img, side)
+    bound = float(ops.image_bound(img, M, N=N).cpu())
+    assert bound == pytest.approx(float(np.float32(var)))
+    got = decode_cols_f16(img, M, N, bound)
+    assert normwise(got, ref) < 5e-7
+    assert np.abs(got - ref).max() < 2e-6 * np.abs(ref).max()
+
+
+def test_conditionals_f16_any_variance(device):
+    """Both layers' (fmean, fvar) of the split-f16 chain at the synthetic problem's
+    kernel variances (pred 0.5, assign 0.1) against float64: the assignment layer as
+    accurate as the prediction layer and as the x6 chain (round-6 regression of the
+    K1 split above: assign fmean 7.6e-6 normwise at config-3 shapes, now 1.0e-6)."""
+    from modulatedgps_amd import config
+    N, M, K, D = 8192, 512, 4, 8
+    X, _, p = R.synthetic_problem(N, M, K, D, 1.0, state="perturbed", S=1)
+    errs = {}
+    for fmt in ("f16", "x6"):
+        old = config.expert_format()
+        config.set_expert_format(fmt)
+        try:
+            model = build_model(p, device)
+            got = [to_np(c)[:, :N] for c in model.conditionals(_t(X, device))]
+        finally:
+            config.set_expert_format(old)
+        for name, L, gm, gv in (("pred", p.pred, got[0], got[1]), ("assign", p.assign, got[2], got[3])):
+            f32 = lambda v: np.asarray(v, np.float64).astype(np.float32).astype(np.float64)
+            fm, fv = R.svgp_predict_f_dedup(f32(X), f32(L["Z"]), f32(L["variance"]), f32(L["lengthscales"]),
+                                            f32(L["q_mu"]), f32(L["q_sqrt"]))
+            errs[fmt, name] = (normwise(gm, fm.T), normwise(gv, fv.T))
+    print(errs)
+    for name in ("pred", "assign"):
+        for i in range(2):
+            assert errs["f16", name][i] < 3e-6
+            assert errs["f16", name][i] < 2.5 * errs["x6", name][i]

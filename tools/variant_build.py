@@ -1,6 +1,6 @@
 """Build a variant of libmgp_hip.so with extra -D flags on one source, for A/B timing
 on the GPU box via MGP_HIP_LIB (the in-tree library is left alone).
-    python tools/variant_build.py NAME split3.hip -DFOO=1 ...   -> var/NAME.so"""
+    python tools/variant_build.py NAME split3.hip -DFOO=1 ...   -> abvar/NAME.so (travels to the box)"""
 import os
 import subprocess
 import sys
@@ -10,7 +10,7 @@ from modulatedgps_amd import build as B  # noqa: E402
 
 name, src, flags = sys.argv[1], sys.argv[2], sys.argv[3:]
 B.build()
-out_dir = os.path.join(B.ROOT, "var")
+out_dir = os.path.join(B.ROOT, "abvar")
 os.makedirs(out_dir, exist_ok=True)
 obj = os.path.join(out_dir, name + "_" + src.replace(".hip", ".o"))
 subprocess.run([B.HIPCC, *B.CXXFLAGS, *flags, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
