@@ -1056,7 +1056,10 @@ constexpr int kElboLanes = 4;
 // variance gradients, differences of large Kuf / Kuu terms through the Cholesky
 // backward, amplify that reordering past their test bound at small M (measured:
 // assign.variance 9.6e-4 vs 6.8e-4 at N = 1000, M = 25, K = 3, D = 1).
-constexpr int kElboBwdLanes = 1;
+#ifndef MGP_K6B_LANES
+#define MGP_K6B_LANES 1
+#endif
+constexpr int kElboBwdLanes = MGP_K6B_LANES;
 static int64_t elbo_fwd_blocks(int64_t N, int lanes) { return (N * lanes + kElboThreads - 1) / kElboThreads; }
 
 extern "C" size_t mgp_elbo_workspace_bytes(int64_t N) {

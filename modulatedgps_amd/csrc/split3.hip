@@ -1455,6 +1455,17 @@ __device__ __forceinline__ void static_for(F&& f) {
 #define MGP_GAC_NC 1
 #endif
 constexpr int kGacPD = MGP_GAC_PD, kGacNC = MGP_GAC_NC;
+// the split-f16 C-images backward on grad_a_c16_kernel (0: grad_a_c_kernel; A/B)
+#ifndef MGP_GAC16
+#define MGP_GAC16 1
+#endif
+constexpr bool kGac16 = MGP_GAC16;
+// grad_a_c16_kernel's row-tile groups per workgroup (1; 2: two row tiles at once, measured
+// slower -- 3.0 vs 1.78 ms per launch for 3.2 vs 8.1 GB fetched, r06k_gac16_train_ab.log)
+#ifndef MGP_GAC16_G
+#define MGP_GAC16_G 1
+#endif
+constexpr int kGac16G = MGP_GAC16_G;
 
 template <int PD, int NC>
 __global__ __launch_bounds__(256, 2) void grad_a_c_kernel(const bf16x8* __restrict__ Ltfr, uint32_t lt_bytes,
@@ -1614,6 +1625,245 @@ __global__ __launch_bounds__(256, 2) void grad_a_c_kernel(const bf16x8* __restri
       // column block nb + c as (128-column tile, wave) of the one-block store
       grad_a_c_store(acc, c, t, (int)((nb + c) / 4), (int)((nb + c) % 4), lane, nmk, M, N, gA0, ld0, gAfr, gexp,
                      ldc);
+    }
+  }
+}
+
+// B-b from the C images on 16x16x32 MFMAs (round 6; replaces grad_a_c_kernel in the
+// split-f16 training step): the same sum gA = 2 sum_k L_k (C_k diag(Gv_k)) + gA0 and the
+// same per-(tile, column) exponent image, but with K5's main-loop shape instead of
+// grad_a_c's 32x32x16 one -- wave tile 128 rows x 64 columns (8 x 4 blocks of 16 x 16),
+// one LDS barrier per 32-deep k-step PAIR (96 MFMAs per wave) instead of per 16-deep
+// k-step (12 MFMAs), and half the LDS bytes per MFMA (each staged L_k fragment feeds
+// four column blocks instead of one).  grad_a_c measured 54-57 % MFMA busy with an
+// LDS read per 1.5 MFMAs; K5's shape runs at ~80 %.
+// Item = (row-tile pair (nT - 1 - p, p), 256-column tile tn), both passes as grad_a_c.
+// The pair stream of a pass (row tile t): blocks of 4 pairs (8 k-steps) outer (the
+// second pass runs them downwards, as grad_a_c, so the workgroups of a column tile
+// stay in step on one XCD), experts inner; after an expert's 4 pairs the accumulator
+// goes to units of the next expert's column weight (grad_a_c's rescale: one f32
+// rounding per switch relative to the running sum, |g| clamped below at 2^-40 of the
+// column's largest).  The column weights (K x 256) and their clamps sit in LDS.
+// Zero blocks of the diagonal tile are zero-filled in the L_k image (no masks).
+constexpr int kGac16KMax = 16;
+// G = 1 (the default): two passes per 256-thread workgroup, as above.  G = 2 (measured,
+// not kept): a 512-thread workgroup takes the row tiles (2j + 1, 2j) of a column tile AT
+// ONCE, one per 4-wave group, over one stream of blocks ascending, so that both groups
+// read the same C_k fragments between the same barriers.  With G = 1 the row-tile
+// workgroups of a column tile share the C_k strips only through L2 when they happen to
+// be in step (8.1 GB fetched per launch for 2.1 GB of images, profiles/
+// r06i_pmc_cond_bwd_f16c.json); G = 2 fetches 3.2 GB but runs 3.0 ms instead of 1.78
+// (one 8-wave workgroup per CU, a barrier over both groups, the short tile's group idle
+// through the long tile's extra blocks) -- the fetched bytes are not what bounds it.
+template <int G>
+__global__ __launch_bounds__(256 * G, 2 / G) void grad_a_c16_kernel(const bf16x8* __restrict__ Ltfr, uint32_t lt_bytes,
+                                                            const bf16x8* __restrict__ Cfr, int64_t cexp,
+                                                            uint32_t c_bytes, int nmk, int nTn, int K, int64_t M,
+                                                            int64_t N, const float* __restrict__ Gv, int64_t ldg,
+                                                            const float* __restrict__ gA0, int64_t ld0,
+                                                            bf16x8* __restrict__ gAfr,
+                                                            const float* __restrict__ l_bound,
+                                                            const float* __restrict__ a_bound,
+                                                            const float* __restrict__ colmax,
+                                                            float* __restrict__ gexp, int64_t ldc) {
+  __shared__ bf16x8 sL[G][2][4 * 2 * 2 * 64];
+  __shared__ float sG[kGac16KMax * 256];
+  const int nT = nmk / 8, nmb = nmk / 2;
+  const int nI = G == 1 ? (nT + 1) / 2 : (nT + 1) / 2;   // items per column tile
+  int p, tn;
+  col_major_item(blockIdx.x, nI, nTn, p, tn);
+  const int grp = G == 2 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
+  // G = 1: passes over row tiles t1 = nT - 1 - p, then t2 = p (t1 == t2: the middle tile of
+  // an odd nT, alone).  G = 2: one pass over blocks 0 .. th, th = min(2p + 1, nT - 1);
+  // group 0 owns row tile th, group 1 row tile 2p (none when th == 2p)
+  const int th = G == 2 ? (2 * p + 1 < nT ? 2 * p + 1 : nT - 1) : 0;
+  const int own2 = grp == 0 ? th : (2 * p < th ? 2 * p : -1);
+  const int tid = threadIdx.x & 255, lane = tid & 63, li = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float unscale =
+      ldexpf(1.f, -(img_exp(*l_bound) + img_exp(*colmax * *a_bound * 1.0009765625f)));
+  // column weights of the tile (column tid), clamped from below at 2^-40 of the column's largest
+  if (grp == 0) {
+    const int64_t n = 256 * (int64_t)tn + tid;
+    float gmax = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float x = n < N ? Gv[(int64_t)k * ldg + n] : 0.f;
+      sG[k * 256 + tid] = x;
+      gmax = fmaxf(gmax, fabsf(x));
+    }
+    const float gmin = fmaxf(gmax * 0x1p-40f, 0x1p-126f);
+    for (int k = 0; k < K; ++k) {
+      const float x = sG[k * 256 + tid];
+      sG[k * 256 + tid] = __builtin_copysignf(fmaxf(fabsf(x), gmin), x);
+    }
+  }
+  // T staging (x6_mainloop16, NPL 2): unit e = tid + 256 s: sub-tile e / 256, k-step
+  // (e / 128) % 2 of the pair, plane (e / 64) % 2
+  uint32_t vT[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int e = tid + 256 * s, i = e / 256, kk = (e / 128) % 2, pl = (e / 64) % 2;
+    vT[s] = (uint32_t)((((i * nmk + kk) * 3 + pl) * 64 + (e & 63)) * 16);
+  }
+  const uint32_t vB = (uint32_t)((((q >> 1) * 3) * 64 + li + 32 * (q & 1)) * 16);
+  const uint32_t sB0 = (uint32_t)((8 * tn + 2 * w) * nmk) * 3u * kFragBytes;
+  const int aoff = (q >> 1) * 64 * 2 + li + 32 * (q & 1);
+  const int col0 = 64 * w + li;   // this lane's column of block cb: col0 + 16 cb (within the tile)
+  bf16x8 (*sLg)[4 * 2 * 2 * 64] = sL[grp];
+  __syncthreads();   // sG
+  for (int pass = 0; pass < (G == 1 ? (nT - 1 - p != p ? 2 : 1) : 1); ++pass) {
+    const int trun = G == 1 ? (pass ? p : nT - 1 - p) : th;   // the stream's blocks 0 .. trun
+    const int t = G == 1 ? trun : own2;                      // this group's row tile (-1: none)
+    const bool desc = G == 1 && pass;                        // G = 1, second pass: blocks downwards
+    const int S = K * 4 * (trun + 1);                        // pairs of the stream (even)
+    // pair s_ of the stream -> (expert k, pair ks, block b)
+    auto at = [&](int s_, int& k, int& ks) {
+      const int bi = s_ / (4 * K), r = s_ % (4 * K);
+      k = r >> 2;
+      ks = 4 * (desc ? trun - bi : bi) + (r & 3);
+    };
+    auto active = [&](int s_) {   // uniform per group: this group's tile needs the pair
+      if (G == 1) return true;
+      const int bi = s_ / (4 * K);
+      return bi <= t;
+    };
+    auto load_t = [&](u32x4v (&st)[4], int s_) {
+      if (!active(s_)) return;
+      int k, ks;
+      at(s_, k, ks);
+      const uint32_t o = (uint32_t)(((int64_t)k * nmb + 4 * t) * nmk + 2 * ks) * 3u * kFragBytes;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) st[u] = __builtin_amdgcn_raw_buffer_load_b128(img_rsrc(Ltfr, lt_bytes), vT[u], o, 0);
+    };
+    auto load_b = [&](bf16x8 (&b)[4][3], int s_) {
+      if (!active(s_)) return;
+      int k, ks;
+      at(s_, k, ks);
+      const __amdgpu_buffer_rsrc_t rB = img_rsrc(Cfr + (int64_t)k * cexp, c_bytes);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          b[cb][pl] = ld_frag(rB, vB, sB0 + (uint32_t)(cb >> 1) * (uint32_t)nmk * 3u * kFragBytes +
+                                          (uint32_t)((2 * ks) * 3 + pl) * kFragBytes + (uint32_t)(16 * (cb & 1)) * 16u);
+    };
+    auto store_t = [&](int buf, const u32x4v (&st)[4], int s_) {
+      if (!active(s_)) return;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) reinterpret_cast<u32x4v*>(sLg[buf])[tid + 256 * u] = st[u];
+    };
+    floatx4v acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[i][c] = floatx4v{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int buf, const bf16x8 (&b)[4][3], int s_) {
+      if (!active(s_)) return;
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib) {
+        const int base = (ib >> 1) * 128 * 2 + 16 * (ib & 1) + aoff;
+        bf16x8 a[3];
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) a[pl] = sLg[buf][base + 64 * pl];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[ib][cb] = mfma16_fmt<2, true>(a, b[cb], acc[ib][cb]);
+      }
+    };
+    // after expert k's 4 pairs of a block: to units of expert (k + 1) % K's weight
+    auto rescale = [&](int s_) {
+      if (!active(s_)) return;
+      const int k = (s_ % (4 * K)) >> 2, kn = k + 1 < K ? k + 1 : 0;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const float r = sG[k * 256 + col0 + 16 * cb] / sG[kn * 256 + col0 + 16 * cb];
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) acc[ib][cb] *= r;
+      }
+    };
+    bf16x8 b0[4][3], b1[4][3];
+    u32x4v st[4];
+    load_t(st, 0);
+    load_b(b0, 0);
+    store_t(0, st, 0);
+    __syncthreads();
+#pragma nounroll
+    for (int s_ = 0; s_ < S; s_ += 2) {
+      load_t(st, s_ + 1);
+      load_b(b1, s_ + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0, b0, s_);
+      __builtin_amdgcn_sched_barrier(0);
+      store_t(1, st, s_ + 1);
+      __syncthreads();
+      const int s2 = s_ + 2 < S ? s_ + 2 : S - 1;  // after the last pair: harmless reload
+      load_t(st, s2);
+      load_b(b0, s2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1, b1, s_ + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if ((s_ & 3) == 2) rescale(s_ + 1);   // pair s_ + 1 ended the expert's block
+      store_t(0, st, s2);
+      __syncthreads();
+    }
+    if (t < 0) continue;   // (G = 2: a group without a row tile; uniform per group, no barrier below)
+    // acc is in units of expert 0's weight (the wrap after the last block)
+    float gl[4], mx[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      gl[cb] = sG[col0 + 16 * cb] * unscale;
+      mx[cb] = 0.f;
+    }
+    // gA = 2 out + gA0 (rows >= M read 0 outside the resource), column maxima over the tile
+    const int64_t i0 = 128 * (int64_t)t;
+    const __amdgpu_buffer_rsrc_t r0 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)gA0, (short)0, (int)(uint32_t)(M * ld0 * 4), 0x00020000);
+    uint32_t ld32 = (uint32_t)ld0;
+    // (opaque per pass: otherwise the 128 per-lane epilogue offsets are hoisted out of the
+    // pass loop and spilled across the main loop)
+    asm volatile("" : "+s"(ld32));
+    const uint32_t soff = (uint32_t)((i0 * ld0 + 256 * (int64_t)tn) * 4);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int nl = col0 + 16 * cb;
+      const bool ok = 256 * (int64_t)tn + nl < N;
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t rl = (uint32_t)(16 * ib + 4 * q + e);
+          const float a0 =
+              __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r0, (rl * ld32 + (uint32_t)nl) * 4u, soff, 0));
+          const float v = ok ? fmaf(2.f, acc[ib][cb][e] * gl[cb], a0) : 0.f;
+          acc[ib][cb][e] = v;
+          mx[cb] = fmaxf(mx[cb], fabsf(v));
+        }
+      mx[cb] = fmaxf(mx[cb], lane_xor16(mx[cb]));
+      mx[cb] = fmaxf(mx[cb], lane_xor32(mx[cb]));
+      const int64_t n = 256 * (int64_t)tn + nl;
+      if (q == 0 && ok) gexp[t * ldc + n] = mx[cb] > 0.f ? (float)img_exp(mx[cb]) : kCexpZero;
+    }
+    // the split-f16 image at 2^e per column (two factors: e can pass 127): fragment
+    // (32-column block 8 tn + 2 w + c, k-step 8 t + ib) from the 16x16 blocks (ib, 2c)
+    // and (ib, 2c + 1) through one lane-half exchange (K4's epilogue)
+    const bool lo_half = lane < 32;
+    const int pos = lo_half ? li + 32 * q : 16 + li + 32 * (q - 2);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ex = img_exp(lo_half ? mx[2 * c] : mx[2 * c + 1]), ex1 = ex / 2;
+      const float sc1 = ldexpf(1.f, ex1), scale = ldexpf(1.f, ex - ex1);
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[ib][2 * c][r];
+          v[4 + r] = acc[ib][2 * c + 1][r];
+          lane_half_swap(v[r], v[4 + r]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= sc1;
+        store_split_f16(gAfr + ((((int64_t)8 * tn + 2 * w + c) * nmk + 8 * t + ib) * 3) * 64 + pos, v, scale);
+      }
     }
   }
 }
@@ -3247,7 +3497,13 @@ static int conditional_backward(
     if ((st = launch_status())) return st;
   }
   // 3. gA (image) = 2 sum_k (S_k A) diag(Gv_k) + gA0  (C path: 2 sum_k L_k C_k diag(Gv_k) + gA0)
-  if (cpath)
+  if (cpath && kGac16 && bwd16 && K <= kGac16KMax)
+    hipLaunchKernelGGL(grad_a_c16_kernel<kGac16G>, dim3((unsigned)((nT + 1) / 2 * nTn)), dim3(256 * kGac16G), 0, s,
+                       (const bf16x8*)Sfr,
+                       (uint32_t)lower_planes(M, K), (const bf16x8*)Cfr, (int64_t)(cols_planes(M, N) / 16),
+                       (uint32_t)cols_planes(M, N), nmk, nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, l_bound,
+                       (const float*)trailer(const_cast<void*>(Afr), cols_planes(M, N)), colmax, cexp, ldn);
+  else if (cpath)
     hipLaunchKernelGGL((grad_a_c_kernel<kGacPD, kGacNC>), dim3((unsigned)((nT + 1) / 2 * (2 / kGacNC) * nTn)), dim3(256), 0, s,
                        (const bf16x8*)Sfr, (uint32_t)lower_planes(M, K), (const bf16x8*)Cfr,
                        (int64_t)(cols_planes(M, N) / 16), (uint32_t)cols_planes(M, N), nmk, (2 / kGacNC) * nTn, K, M, N, Gv, ldg, gA0, ldn, gAfr, l_bound,

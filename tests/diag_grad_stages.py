@@ -74,12 +74,12 @@ def layer_stage_grads(X, L, Gmu, Gv, dtype):
     torch.autograd.backward([fmean, fvar], [t(Gmu.T), t(Gv.T)])
     out = {"g_Kuf": Kuf.grad.double().numpy(), "g_Lm": np.tril(Lm.grad.double().numpy()),
            "g_q_mu": P["q_mu"].grad.double().numpy(), "g_q_sqrt": np.tril(P["q_sqrt"].grad.double().numpy())}
+    gK = Kuu.grad.double().numpy()
+    out["_tail"] = {"g_Kuu": 0.5 * (gK + gK.T)}
     if dtype == torch.float64:   # the tail references (not compared as stages)
-        gK = Kuu.grad.double().numpy()
-        tail = tail_f64(X, L, gKuf=out["g_Kuf"], gKuu=0.5 * (gK + gK.T))
+        tail = tail_f64(X, L, gKuf=out["g_Kuf"], gKuu=out["_tail"]["g_Kuu"])
         kuf_only = tail_f64(X, L, gKuf=out["g_Kuf"], gKuu=np.zeros_like(gK))
-        out["_tail"] = {"g_Kuu": 0.5 * (gK + gK.T), "g_ls": tail["g_ls"], "g_var_rbf": tail["g_var"],
-                        "g_ls_kuf": kuf_only["g_ls"]}
+        out["_tail"].update({"g_ls": tail["g_ls"], "g_var_rbf": tail["g_var"], "g_ls_kuf": kuf_only["g_ls"]})
     return out
 
 
@@ -198,8 +198,14 @@ def main():
             s64 = layer_stage_grads(X, L, G64[gm], G64[gv], torch.float64)
             s32 = layer_stage_grads(X, L, G64[gm], G64[gv], torch.float32)
             tail = s64.pop("_tail")
-            s32.pop("_tail", None)
+            t32 = s32.pop("_tail")
             rep["stages_f32_autograd"][name] = {k: normwise(s32[k], s64[k]) for k in s64}
+            # which float32 cotangent moves the lengthscale gradient (float64 tail on each mix)
+            rep["stages_f32_autograd"][name]["gKuu"] = normwise(t32["g_Kuu"], tail["g_Kuu"])
+            for lab, gf, gu in (("gls_f32Kuf_f32Kuu", s32["g_Kuf"], t32["g_Kuu"]),
+                                ("gls_f32Kuf_refKuu", s32["g_Kuf"], tail["g_Kuu"]),
+                                ("gls_refKuf_f32Kuu", s64["g_Kuf"], t32["g_Kuu"])):
+                rep["stages_f32_autograd"][name][lab] = normwise(tail_f64(X, L, gKuf=gf, gKuu=gu)["g_ls"], tail["g_ls"])
             s64.update(tail)
             rep["_stage_ref"][name] = s64
             print(f"stage oracle {name} {time.time() - t0:.0f}s", flush=True)
@@ -251,6 +257,12 @@ def main():
                         "rbf_gvar_own": normwise(rbf["rbf_gvar"][i].reshape(-1), tail["g_var"]),
                         "rbf_gls_ref": normwise(tail["g_ls"], rep["_stage_ref"][name]["g_ls"]),
                         "rbf_gvar_ref": normwise(tail["g_var"], rep["_stage_ref"][name]["g_var_rbf"]),
+                        "gls_hipKuf_refKuu": normwise(tail_f64(X, L, gKuf=rbf["rbf_gKuf"][i][:M, :N],
+                                                               gKuu=gKuu_ref)["g_ls"],
+                                                      rep["_stage_ref"][name]["g_ls"]),
+                        "gls_refKuf_hipKuu": normwise(tail_f64(X, L, gKuf=rep["_stage_ref"][name]["g_Kuf"],
+                                                               gKuu=rbf["rbf_gKuu"][i][:M, :M])["g_ls"],
+                                                      rep["_stage_ref"][name]["g_ls"]),
                         "gls_kuf_part_over_total": float(np.abs(rep["_stage_ref"][name]["g_ls_kuf"]).sum()
                                                          / max(np.abs(rep["_stage_ref"][name]["g_ls"]).sum(), 1e-300))}
         finally:

@@ -308,7 +308,9 @@ def test_kuf_f16_image_any_variance(device, var):
     vt = torch.tensor([var], dtype=torch.float32, device=device)
     lt = torch.tensor([1.0], dtype=torch.float32, device=device)
     ref = R.rbf_K(Z32.astype(np.float64), X32.astype(np.float64), float(np.float32(var)), 1.0)
-    img = ops.rbf_kuf_x6(Xd, Zd, vt, lt, fmt="f16")
+    # zero-filled buffers: plane 2 of a split-f16 image is never written
+    img = torch.zeros(ops._lib.load().mgp_x6_cols_bytes(M, N), dtype=torch.uint8, device=device)
+    ops.rbf_kuf_x6(Xd, Zd, vt, lt, out=img, fmt="f16")
     side = torch.zeros_like(img)
     ops.kuu_potrf_trtri([Zd], [vt], [lt], 1e-6, kuf=(Xd, [side], "f16"))
     torch.cuda.synchronize()

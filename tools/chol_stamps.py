@@ -95,6 +95,33 @@ for j in range(steps - 1):
         continue
     d = [s[k + 1] - s[k] for k in range(5)]
     print(j, *d, "|", s[5] - s[0], "| entry->start", s[0] - s[7], " start->loads issued", s[6] - s[0])
+# MFMA busy per role (round 6): the analytic f64 MFMA count of the
+# workgroup (tools/k3_mfma_count.py: 64 pipe cycles per v_mfma_f64_16x16x4) over its own
+# stamped shader cycles on the CU's 4 SIMDs -- the look-ahead workgroup (the factorisation
+# chain, VALU panel sweeps) apart from the pair workgroups (the trailing-update / forward-
+# substitution GEMMs, north_star's "panel GEMMs")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import k3_mfma_count as KC  # noqa: E402
+nb = M // 64
+print("MFMA busy per role (analytic MFMAs x 64 cycles / (4 SIMDs x stamped cycles)):")
+print("step  look-ahead(cyc, busy)  pair row nb-1 #0 (cyc, MFMAs, busy)")
+la_b, pr_b = [], []
+for j in range(steps - 1):
+    s = st[j]
+    la_cyc = s[7] - s[0]
+    q = [pb[j * 8 + k] for k in range(8)]
+    i, nt, nupd = nb - 1, nb, (nb - 1) - j
+    pm = KC.PAIR_P + sum((KC.DIAG if j + 1 + e == i else KC.UPD) if e < nupd else
+                         (KC.FWD if e - nupd < j else KC.FWD_DIAG) for e in range(min(2, nt)))
+    pc = q[5] - q[0] if q[0] and q[5] else 0
+    lb = KC.LOOKAHEAD * 64 / (4 * la_cyc) if la_cyc > 0 else float("nan")
+    pbz = pm * 64 / (4 * pc) if pc > 0 else float("nan")
+    la_b.append((KC.LOOKAHEAD * 64, 4 * la_cyc))
+    if pc:
+        pr_b.append((pm * 64, 4 * pc))
+    print(f"{j:2d}  {la_cyc:7d} {lb:6.3f}   {pc:7d} {pm:5d} {pbz:6.3f}")
+tot = lambda v: sum(a for a, _ in v) / max(1, sum(b for _, b in v))
+print(f"cycle-weighted: look-ahead {tot(la_b):.3f}  pair workgroups {tot(pr_b):.3f}")
 p = st[63]
 if p[0]:
     print(f"prep tile (0, 0): build {p[1] - p[0]}  factor {p[2] - p[1]}  write {p[3] - p[2]} shader cycles; "
