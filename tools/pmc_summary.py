@@ -109,12 +109,19 @@ def main(root, out, groups=("SQ_WAVE_CYCLES", "FETCH_SIZE", "WRITE_SIZE", "TCC_H
             else:
                 e["effective_clock_ghz"] = None
                 e["clock_note"] = "dispatch < 0.3 ms: GRBM_GUI_ACTIVE outlasts the kernel, no clock derived"
+        if avg.get("SQ_WAVE_CYCLES"):   # wave-cycle buckets (issuing / waiting on a dependency or pipe / parked)
+            wc = avg["SQ_WAVE_CYCLES"]
+            e["wave_cycles_issuing"] = avg.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
+            e["wave_cycles_wait_inst"] = avg.get("SQ_WAIT_INST_ANY", 0.0) / wc
+            e["wave_cycles_wait_any"] = avg.get("SQ_WAIT_ANY", 0.0) / wc
+        if avg.get("SQ_INSTS_LDS"):
+            e["lds_bank_conflict_cycles_per_lds_inst"] = avg.get("SQ_LDS_BANK_CONFLICT", 0.0) / avg["SQ_INSTS_LDS"]
         if "SQ_INSTS_VALU_MFMA_MOPS_F64" in avg:
             e["f64_mfma_count"] = avg["SQ_INSTS_VALU_MFMA_MOPS_F64"] / 4.0
             if e.get("mfma_busy_cycles") and e["f64_mfma_count"] > 0:
                 e["mfma_busy_cycles_per_f64_mfma"] = e["mfma_busy_cycles"] / e["f64_mfma_count"]
         summary[k] = e
-    json.dump({"source": "rocprofv3 --pmc passes of tools/pmc_pass.sh (tools/bench_kernels.py, c3)",
+    json.dump({"source": os.environ.get("PMC_SOURCE", "rocprofv3 --pmc passes of tools/pmc_pass.sh (tools/bench_kernels.py, c3)"),
                "corrections": "bytes_read = 2 * FETCH_SIZE KiB (gfx950 wide-read undercount), "
                               "bytes_written = WRITE_SIZE KiB",
                "kernels": summary}, open(out, "w"), indent=1)
