@@ -24,6 +24,12 @@ CXXFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-I", INCLUD
             "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
 
+# per-source flags: chol.hip's step launches take their hot scalar arguments first, and the
+# dispatch preloads up to 16 argument dwords into SGPRs (gfx950 kernel-argument preload),
+# so a K3 step's first tile loads wait for no kernel-argument fetch
+FILE_FLAGS = {"chol.hip": ["-mllvm", "-amdgpu-kernarg-preload-count=16"]}
+
+
 def _sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
@@ -42,7 +48,7 @@ def _compile(src, hdr_time, verbose, extra):
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
     if _mtime(obj) >= max(_mtime(src), hdr_time) and not extra:
         return obj
-    cmd = [HIPCC, *CXXFLAGS, *extra, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CXXFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstddef>
 #include <vector>
 
 #include "kuf_image.hpp"
@@ -818,6 +819,19 @@ __device__ __forceinline__ void write_diag(const CholArgs& a, int b, int j, cons
 }
 
 // ------------------------------------------------------------------ prep launch
+// MGP_K3_PREP_NT: the prep's Kuu tiles and zero fills stored non-temporal (fewer dirty L2
+// lines for the write-back at the prep's end, in front of the first step launch)
+#ifndef MGP_K3_PREP_NT
+#define MGP_K3_PREP_NT 0
+#endif
+template <class T>
+__device__ __forceinline__ void prep_store(T* p, T v) {
+#if MGP_K3_PREP_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
   __shared__ double s1[CB * LDT], s2[CB * LDT], col[CB];
   __shared__ double sil[32];
@@ -845,7 +859,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     if (a.A || a.D > 32) {
       for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
         const int r = idx >> 6, c = idx & 63;
-        dst[(int64_t)r * ld + c] = elem(r0 + r, c0 + c);
+        prep_store(dst + (int64_t)r * ld + c, elem(r0 + r, c0 + c));
       }
       return;
     }
@@ -873,7 +887,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
         v = varb * exp(-0.5 * sacc);
         if (gr == gc) v += a.jitter;
       }
-      dst[(int64_t)r * ld + c] = v;
+      prep_store(dst + (int64_t)r * ld + c, v);
     }
     __syncthreads();
   };
@@ -908,7 +922,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_prep(CholArgs a) {
     for (int idx = threadIdx.x; idx < CB * CB; idx += kCholThreads) {
       const int r = idx >> 6, c = idx & 63;
       const int64_t gr = r0 + r, gc = c0 + c;
-      if (gr < a.M && gc < a.M) dst[gr * a.ldl + gc] = 0.f;
+      if (gr < a.M && gc < a.M) prep_store(dst + gr * a.ldl + gc, 0.f);
     }
   }
 }
@@ -966,6 +980,20 @@ __global__ __launch_bounds__(kCholThreads) void chol_last_step(CholArgs a, int j
   }
 }
 
+// ------------------------------------------------------------------ step launch arguments
+// chol_step_pair's leading scalar arguments are the ones its first tile loads need (the
+// workspace, its strides, the step and the pair count); they come ahead of the CholArgs
+// block so that the dispatch preloads them into SGPRs (chol.hip is compiled with
+// -amdgpu-kernarg-preload-count, modulatedgps_amd/build.py).  Every other field is read
+// from the kernel-argument segment behind the tile loads.  The layout below mirrors the
+// kernel's parameter list (kernel arguments follow their natural alignment in order),
+// giving the offset of the CholArgs block for the side job's dynamic-index reads.
+struct StepPairKernargs {
+  double* ws; int64_t strideWS, Mp; int nb, j, batch, Pb;
+  CholArgs a;
+};
+constexpr size_t kStepArgsOffset = offsetof(StepPairKernargs, a);
+
 // ------------------------------------------------------------------ Kuf side job
 #ifndef MGP_KUF_SIDE_POLICY
 #define MGP_KUF_SIDE_POLICY 1   // the side job's image stores (kuf_image.hpp img_store): non-temporal
@@ -991,7 +1019,8 @@ __device__ __forceinline__ void kuf_side_blocks(const CholArgs& a, int w, int64_
     // dynamic index (`a` is the by-value kernel argument at its offset 0; indexing `a`
     // itself would copy the whole struct to scratch)
     typedef const CholArgs __attribute__((address_space(4))) KernargCholArgs;
-    const KernargCholArgs& ag = *(const KernargCholArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const KernargCholArgs& ag = *(const KernargCholArgs*)(
+        (const char __attribute__((address_space(4)))*)__builtin_amdgcn_kernarg_segment_ptr() + kStepArgsOffset);
     const KufImageArgs ka = {a.kx, a.kldx, ag.Z[b], a.ldz, a.kN, a.M, a.D, ag.var[b], ag.ls[b], ag.n_ls[b],
                              a.knmk, a.krow_blocks, ag.kfr[b], ag.kbound[b]};
     const int64_t bid = item - b * a.kblocks;
@@ -1050,22 +1079,29 @@ __host__ __device__ inline int step_pair_count(int nb, int j) {  // per batch en
 // does not straddle two) share the panel tiles W_lj, B_jc there.  No idle workgroups.
 // Workgroups past batch (1 + Pb) (when the launch carries a Kuf side job): kuf_side_job
 // over the image blocks [k0, k1), nkwg of them.
-__global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j, int batch, int Pb, int64_t k0,
+__global__ __launch_bounds__(kPairThreads) void chol_step_pair(double* pws, int64_t pstrideWS, int64_t pMp, int pnb,
+                                                               int j, int batch, int Pb, CholArgs ain, int64_t k0,
                                                                int64_t k1, int nkwg) {
   __shared__ double s1[CB * LDT], sD[CB * LDT], s2[2][CB * LDT], col[CB];
+  CholArgs a = ain;   // (fields read in place; the hot ones from the preloaded arguments)
+  a.ws = pws;
+  a.strideWS = pstrideWS;
+  a.Mp = pMp;
+  a.nb = pnb;
   if ((int)blockIdx.x >= batch * (1 + Pb)) {   // uniform per workgroup
     kuf_side_job(a, (int)blockIdx.x - batch * (1 + Pb), k0, k1, nkwg, reinterpret_cast<float*>(s1),
                  reinterpret_cast<float*>(sD));
     return;
   }
   ENTRYTIME(t_entry);
-  // the kernel arguments every workgroup reads, loaded at entry as one batch of scalar
-  // loads behind one wait (the compiler had placed each at its first use: three dependent
-  // scalar-cache round trips before the first tile load)
-  asm volatile("" ::"s"(a.ws), "s"(a.strideWS), "s"(a.Mp), "s"(a.M), "s"(a.nb), "s"(a.L), "s"(a.LinvT),
-               "s"(a.ldl), "s"(a.strideL), "s"(a.info), "s"(j), "s"(batch), "s"(Pb));
-  asm volatile("" ::"s"(a.lt_absmax[0]), "s"(a.lt_absmax[1]), "s"(a.lt_absmax[2]), "s"(a.lt_absmax[3]),
-               "s"(a.lt_absmax[4]), "s"(a.lt_absmax[5]), "s"(a.lt_absmax[6]), "s"(a.lt_absmax[7]));
+  // the other kernel arguments a workgroup reads, as one batch of scalar loads whose wait
+  // sits behind the tile loads' issue (the compiler had placed each load at its first use:
+  // dependent kernel-argument round trips, ~1 us each, in front of the first tile load)
+  auto kernargs_in = [&]() {
+    asm volatile("" ::"s"(a.M), "s"(a.L), "s"(a.LinvT), "s"(a.ldl), "s"(a.strideL), "s"(a.info));
+    asm volatile("" ::"s"(a.lt_absmax[0]), "s"(a.lt_absmax[1]), "s"(a.lt_absmax[2]), "s"(a.lt_absmax[3]),
+                 "s"(a.lt_absmax[4]), "s"(a.lt_absmax[5]), "s"(a.lt_absmax[6]), "s"(a.lt_absmax[7]));
+  };
   const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));  // tile group
   const int wg = blockIdx.x;
   // workgroup -> (batch entry, tile row, pair of the row): step_pair_count
@@ -1114,6 +1150,7 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
     } else {
       tile_fetch(r2, Wt(i, i), CB);
     }
+    kernargs_in();
     if (act) {
       tile_put(s1, r1);
       tile_put(sD, rD);
@@ -1164,6 +1201,7 @@ __global__ __launch_bounds__(kPairThreads) void chol_step_pair(CholArgs a, int j
   const double* srcu = (upd && l != i) ? Wt(i, l) : fwd ? Bt(i, c) : nullptr;
   if (src2) tile_fetch(r2, src2, CB);
   if (srcu) row_from_global(u, srcu, CB);
+  kernargs_in();
 #ifdef MGP_DBG_STAMPS
   __builtin_amdgcn_sched_barrier(0);
   PAIRSTAMP(pst, j, 6);  // every load issued
@@ -1473,8 +1511,9 @@ static int chol_run(CholArgs& a, int batch, void* workspace, size_t workspace_by
       const int Pb = step_pair_count(a.nb, j);
       const bool side = !kbeg.empty() && knwg[j] > 0;
       const int nkwg = side ? knwg[j] : 0;
-      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb) + nkwg), dim3(kPairThreads), 0, s, a, j, batch, Pb,
-                         side ? kbeg[j] : (int64_t)0, side ? kbeg[j + 1] : (int64_t)0, nkwg);
+      hipLaunchKernelGGL(chol_step_pair, dim3(batch * (1 + Pb) + nkwg), dim3(kPairThreads), 0, s, a.ws, a.strideWS,
+                         a.Mp, a.nb, j, batch, Pb, a, side ? kbeg[j] : (int64_t)0, side ? kbeg[j + 1] : (int64_t)0,
+                         nkwg);
     } else {
       hipLaunchKernelGGL(chol_last_step, dim3(a.nb, batch), block, 0, s, a, j);
     }

@@ -261,10 +261,11 @@ __device__ __forceinline__ bf16x8 ld_frag(__amdgpu_buffer_rsrc_t r, uint32_t vof
 
 // Item b -> (row tile t heavy-first, column tile tn, expert k); the K experts of
 // a column tile are 8 block ids apart (one XCD) when nTn % 8 == 0.
-// TN_OUTER (K5 writing the C_k images, training): per XCD, one column tile at a
-// time with all its row tiles (heavy first) and experts, so A's column slab is
-// fetched about once instead of once per row tile (C-writing K5 1.60 -> 1.51 ms;
-// without the C writes the row-tile-outer order is faster, 1.33 vs 1.36 ms).
+// TN_OUTER: per XCD, one column tile at a time with all its row tiles (heavy first)
+// and experts, so A's column slab is fetched about once instead of once per row tile
+// (the 32x32x16 C-writing K5 of round 2: 1.60 -> 1.51 ms; without the C writes the
+// row-tile-outer order was faster, 1.33 vs 1.36 ms).  The 16x16x32 kernels use the
+// row-tile-outer order for both (MGP_K5C_TN_OUTER).
 template <bool TN_OUTER = false>
 __device__ __forceinline__ void x6_item(int b, int nTn, int K, int& t, int& tn, int& k, int grid = -1) {
   if (TN_OUTER && nTn % 8 == 0) {
@@ -695,6 +696,13 @@ __device__ __forceinline__ void x6_mainloop16(floatx4v (&acc)[8][4], bf16x8 (*sL
 #define MGP_C_NT 1
 #endif
 constexpr bool kCntStores = MGP_C_NT;
+// C-writing K5 (training) in the column-tile-outer item order (x6_item TN_OUTER): measured
+// against the forward's row-tile-outer order on the 16x16x32 kernel, training step 14.18-14.22
+// vs 14.11-14.18 ms (profiles/r06o_train_ab.log) -- so the row-tile-outer order (0) is kept
+#ifndef MGP_K5C_TN_OUTER
+#define MGP_K5C_TN_OUTER 0
+#endif
+constexpr bool kK5cTnOuter = MGP_K5C_TN_OUTER;
 template <bool COUT>
 __device__ __forceinline__ void expert_cond16_item(bf16x8 (*sL)[4 * 2 * 3 * 64], int b, int grid,
                                                    const bf16x8* __restrict__ Afr, const bf16x8* __restrict__ Lfr,
@@ -704,7 +712,7 @@ __device__ __forceinline__ void expert_cond16_item(bf16x8 (*sL)[4 * 2 * 3 * 64],
                                                    const float* __restrict__ l_bound, bf16x8* __restrict__ Cfr,
                                                    int64_t cexp, const float* __restrict__ colmax) {
   int t, tn, k;
-  x6_item<COUT>(b, nTn, K, t, tn, k, grid);
+  x6_item<COUT && kK5cTnOuter>(b, nTn, K, t, tn, k, grid);
   const int nTp = nmb / 4;
   const int lane = threadIdx.x & 63, li = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

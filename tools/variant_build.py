@@ -13,7 +13,7 @@ B.build()
 out_dir = os.path.join(B.ROOT, "abvar")
 os.makedirs(out_dir, exist_ok=True)
 obj = os.path.join(out_dir, name + "_" + src.replace(".hip", ".o"))
-subprocess.run([B.HIPCC, *B.CXXFLAGS, *flags, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
+subprocess.run([B.HIPCC, *B.CXXFLAGS, *B.FILE_FLAGS.get(src, []), *flags, "-c", os.path.join(B.CSRC, src), "-o", obj], check=True)
 objs = [os.path.join(B.BUILD, f) for f in sorted(os.listdir(B.BUILD))
         if f.endswith(".o") and f != src.replace(".hip", ".o")]
 subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out_dir, name + ".so"),
