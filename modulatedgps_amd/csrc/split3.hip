@@ -703,6 +703,10 @@ constexpr bool kCntStores = MGP_C_NT;
 #define MGP_K5C_TN_OUTER 0
 #endif
 constexpr bool kK5cTnOuter = MGP_K5C_TN_OUTER;
+#ifndef MGP_K5_TN_OUTER
+#define MGP_K5_TN_OUTER 0   // the forward K5's item order (0: row tile outer)
+#endif
+constexpr bool kK5TnOuter = MGP_K5_TN_OUTER;
 template <bool COUT>
 __device__ __forceinline__ void expert_cond16_item(bf16x8 (*sL)[4 * 2 * 3 * 64], int b, int grid,
                                                    const bf16x8* __restrict__ Afr, const bf16x8* __restrict__ Lfr,
@@ -712,7 +716,7 @@ __device__ __forceinline__ void expert_cond16_item(bf16x8 (*sL)[4 * 2 * 3 * 64],
                                                    const float* __restrict__ l_bound, bf16x8* __restrict__ Cfr,
                                                    int64_t cexp, const float* __restrict__ colmax) {
   int t, tn, k;
-  x6_item<COUT && kK5cTnOuter>(b, nTn, K, t, tn, k, grid);
+  x6_item<COUT ? kK5cTnOuter : kK5TnOuter>(b, nTn, K, t, tn, k, grid);
   const int nTp = nmb / 4;
   const int lane = threadIdx.x & 63, li = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

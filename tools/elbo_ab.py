@@ -1,7 +1,7 @@
 """Timed c3 ELBO steps of the library in MGP_HIP_LIB (default: the in-tree one),
 for A/B runs of kernel variants in separate processes: ms per step for `rounds`
 blocks of `steps` steps, and the ELBO at a fixed Philox key (bit-identity check).
-Usage: python tools/elbo_ab.py [rounds] [steps] [label]"""
+Usage: python tools/elbo_ab.py [rounds] [steps] [label]   (MGP_AB_CONFIG=c4r: another bench config)"""
 import os
 import sys
 import time
@@ -23,7 +23,7 @@ def main():
         from modulatedgps_amd import models
         models._QS_BATCH = False
     dev = torch.device("cuda", 0)
-    cfg = bench.CONFIGS["c3"]
+    cfg = bench.CONFIGS[os.environ.get("MGP_AB_CONFIG", "c3")]   # e.g. c4r: c4's per-rank shape
     X_np, Y_np, layers = bench.synthetic(cfg, 0, dev)
     model = bench.build_model(cfg, layers, dev, num_data=cfg[0])
     X = torch.from_numpy(X_np).to(dev)
