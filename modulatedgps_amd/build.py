@@ -79,6 +79,55 @@ def build(verbose=False, extra_flags=()):
     return LIB
 
 
+ASAN_BUILD = os.path.join(PKG, "_build_asan")
+ASAN_LIB = os.path.join(ASAN_BUILD, "libmgp_hip_asan.so")
+
+
+def asan_runtime():
+    """The clang AddressSanitizer runtime the host-ASan library links against (preloaded
+    into the Python process that loads it), or None."""
+    base = "/opt/rocm/lib/llvm/lib/clang"
+    if not os.path.isdir(base):
+        return None
+    for v in sorted(os.listdir(base), reverse=True):
+        p = os.path.join(base, v, "lib", "linux", "libclang_rt.asan-x86_64.so")
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def build_asan(verbose=False):
+    """libmgp_hip.so with its HOST code built under AddressSanitizer (-Xarch_host
+    -fsanitize=address; the gfx950 device code is the same, GPU sanitizers are not used) into
+    modulatedgps_amd/_build_asan/ -- for the CPU tests of the C-ABI's host paths
+    (tests/test_host_asan.py).  Not the product library."""
+    os.makedirs(ASAN_BUILD, exist_ok=True)
+    srcs = _sources()
+    hdr_time = max([_mtime(h) for h in _headers()] + [0.0])
+    flags = ["-O1", "-g", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-I", INCLUDE, "-I", CSRC,
+             "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+    def one(src):
+        obj = os.path.join(ASAN_BUILD, os.path.basename(src).replace(".hip", ".o"))
+        if _mtime(obj) >= max(_mtime(src), hdr_time):
+            return obj
+        cmd = [HIPCC, *flags, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc (asan) failed for {src}:\n{r.stdout}\n{r.stderr}")
+        return obj
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(one, srcs))
+    if _mtime(ASAN_LIB) < max(_mtime(o) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-fsanitize=address", "-shared-libasan",
+               "-o", ASAN_LIB + ".tmp", *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link (asan) failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(ASAN_LIB + ".tmp", ASAN_LIB)
+    return ASAN_LIB
+
+
 C_ABI_SRC = os.path.join(ROOT, "tests", "c_abi", "elbo_c.cpp")
 C_ABI_BIN = os.path.join(ROOT, "tests", "c_abi", "elbo_c")
 
