@@ -219,7 +219,8 @@ def test_trsm_stats_f16_batch_bit_identical(device, N, M, K, with_a):
             assert torch.equal(As[b][:, :N], ref[b][2][:, :N])
 
 
-@pytest.mark.parametrize("N,M,K,train", [(65536, 1024, 8, False), (8192, 256, 4, True), (3000, 200, 3, True)])
+@pytest.mark.parametrize("N,M,K,train", [(65536, 1024, 8, False), (8192, 256, 4, True), (3000, 200, 3, True),
+                                         (2800, 200, 3, False), (2800, 130, 2, True)])   # odd column-tile counts
 def test_expert_conditional_f16_batch_bit_identical(device, N, M, K, train):
     """mgp_expert_conditional_f16_batch (both layers' K5 in one launch, forward or with
     the training C_k images) gives the same fmean / fvar / C_k bits as one
