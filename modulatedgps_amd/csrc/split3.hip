@@ -76,9 +76,9 @@ __global__ __launch_bounds__(256) void split_tri_kernel(const float* __restrict_
                                                         int64_t stride, int64_t M, int nmb, int nmk,
                                                         int64_t nfrag, bf16x8* __restrict__ img,
                                                         const float* __restrict__ bound = nullptr) {
-  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f >= nfrag) return;
-  split_tri_frag<LOWER, TRANS, FULL>(src, ld, stride, M, nmb, nmk, f, threadIdx.x & 63, img, bound);
+  // (a grid of fewer than nfrag / 4 workgroups walks the fragments with a stride)
+  for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nfrag; f += (int64_t)gridDim.x * 4)
+    split_tri_frag<LOWER, TRANS, FULL>(src, ld, stride, M, nmb, nmk, f, threadIdx.x & 63, img, bound);
 }
 
 // ------------------------------------------------------------------ tril(q_sqrt) work of two layers
@@ -98,23 +98,37 @@ struct QLayer {
   float* bmax;      // [nblk] block maxima
 };
 
+// The tril(q_sqrt) work runs on the side stream beside K3's chain: with MGP_QS_GRID > 0 its
+// two wide launches (the KL partials and the image split) walk their blocks / fragments in a
+// grid-stride loop over at most MGP_QS_GRID workgroups per layer, so that they hold fewer CUs
+// while the chain's step launches dispatch (same per-block and per-fragment work: the same bits;
+// 256 against the full grids: ELBO step 3.186-3.234 vs 3.229-3.238 ms and c4r 0.696-0.700 vs
+// 0.702-0.706 ms on one box, even on another, profiles/r06v_qsqrt_side_grid_ab.log, r06w_*;
+// 16 or 64 put the side work on the critical path).
+#ifndef MGP_QS_GRID
+#define MGP_QS_GRID 256
+#endif
+constexpr int kQsGrid = MGP_QS_GRID;
+
 __global__ __launch_bounds__(256) void kl_absmax2_kernel(QLayer l0, QLayer l1, int64_t ldq, int64_t ldqs,
-                                                         int64_t strideq, int64_t M, int K, int nrb) {
+                                                         int64_t strideq, int64_t M, int K, int nrb, int nblk) {
   __shared__ double scratch[16];
   __shared__ float smax[4];
   const QLayer& l = blockIdx.y ? l1 : l0;
-  const int blk = blockIdx.x;
-  const KlPartial r = kl_partials_thread(l.q_mu, ldq, l.q_sqrt, ldqs, strideq, M, K, nrb, blk, threadIdx.x, 256);
-  const float m = wave_max_f32(r.amax);
-  if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = m;
-  const double a = block_sum<double>((double)r.tr, scratch);   // (its barriers publish smax)
-  const double b = block_sum<double>((double)r.ld, scratch);
-  const double c = block_sum<double>((double)r.mh, scratch);
-  if (threadIdx.x == 0) {
-    l.part[3 * blk + 0] = a;
-    l.part[3 * blk + 1] = b;
-    l.part[3 * blk + 2] = c;
-    l.bmax[blk] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // (uniform per workgroup)
+    const KlPartial r = kl_partials_thread(l.q_mu, ldq, l.q_sqrt, ldqs, strideq, M, K, nrb, blk, threadIdx.x, 256);
+    const float m = wave_max_f32(r.amax);
+    if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = m;
+    const double a = block_sum<double>((double)r.tr, scratch);   // (its barriers publish smax)
+    const double b = block_sum<double>((double)r.ld, scratch);
+    const double c = block_sum<double>((double)r.mh, scratch);
+    if (threadIdx.x == 0) {
+      l.part[3 * blk + 0] = a;
+      l.part[3 * blk + 1] = b;
+      l.part[3 * blk + 2] = c;
+      l.bmax[blk] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    }
+    __syncthreads();   // smax / scratch reused by the next block
   }
 }
 
@@ -142,10 +156,9 @@ __global__ __launch_bounds__(1024) void kl_final2_kernel(QLayer l0, QLayer l1, i
 
 __global__ __launch_bounds__(256) void split_lower2_kernel(QLayer l0, QLayer l1, int64_t ldqs, int64_t strideq,
                                                            int64_t M, int nmb, int nmk, int64_t nfrag) {
-  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f >= nfrag) return;
   const QLayer& l = blockIdx.y ? l1 : l0;
-  split_tri_frag<true>(l.q_sqrt, ldqs, strideq, M, nmb, nmk, f, threadIdx.x & 63, l.Lfr, l.bound);
+  for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nfrag; f += (int64_t)gridDim.x * 4)
+    split_tri_frag<true>(l.q_sqrt, ldqs, strideq, M, nmb, nmk, f, threadIdx.x & 63, l.Lfr, l.bound);
 }
 
 // split_tri_kernel<false> (the split-f16 L^-T images) for two matrices at src and
@@ -2983,8 +2996,9 @@ extern "C" int mgp_qsqrt_images_kl_f16_batch(int32_t batch, const float* const* 
   }
   hipStream_t st = (hipStream_t)stream;
   const int nrb = (int)((M + kKlRows - 1) / kKlRows);
-  hipLaunchKernelGGL(kl_absmax2_kernel, dim3((unsigned)nblk, (unsigned)batch), dim3(256), 0, st, l[0], l[1], ldq,
-                     ldqs, strideq, M, K, nrb);
+  const int64_t kgrid = kQsGrid > 0 && nblk > kQsGrid ? kQsGrid : nblk;
+  hipLaunchKernelGGL(kl_absmax2_kernel, dim3((unsigned)kgrid, (unsigned)batch), dim3(256), 0, st, l[0], l[1], ldq,
+                     ldqs, strideq, M, K, nrb, (int)nblk);
   int rc = launch_status();
   if (rc) return rc;
   hipLaunchKernelGGL(kl_final2_kernel, dim3((unsigned)batch), dim3(1024), 0, st, l[0], l[1], (int)nblk,
@@ -2994,7 +3008,8 @@ extern "C" int mgp_qsqrt_images_kl_f16_batch(int32_t batch, const float* const* 
   const int64_t Mp = x6_mp(M);
   const int nmb = (int)(Mp / 32), nmk = (int)(Mp / 16);
   const int64_t nfrag = (int64_t)K * nmb * nmk;
-  hipLaunchKernelGGL(split_lower2_kernel, dim3((unsigned)((nfrag + 3) / 4), (unsigned)batch), dim3(256), 0, st, l[0],
+  const int64_t sgrid = kQsGrid > 0 && (nfrag + 3) / 4 > kQsGrid ? kQsGrid : (nfrag + 3) / 4;
+  hipLaunchKernelGGL(split_lower2_kernel, dim3((unsigned)sgrid, (unsigned)batch), dim3(256), 0, st, l[0],
                      l[1], ldqs, strideq, M, nmb, nmk, nfrag);
   return launch_status();
 }
@@ -3669,6 +3684,8 @@ extern "C" int mgp_conditional_backward_prep_f16c(const float* q_sqrt, int64_t l
   const int nmk = (int)(Mp / 16), nmb = (int)(Mp / 32);
   const int64_t nfrag = (int64_t)K * nmb * nmk;
   float* LT = (float*)((char*)prep + al256(mgp_x6_lower_bytes(M, K)));
+  // (full grids: the capped grid-stride form of the ELBO's q_sqrt launches measured slower here,
+  // training step 14.02-14.11 vs 13.98-14.01 ms, profiles/r06w_side_grid_ab.log)
   hipLaunchKernelGGL((split_tri_kernel<false, true>), dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, s, q_sqrt,
                      ldqs, strideq, M, nmb, nmk, nfrag, (bf16x8*)prep, l_bound);
   hipLaunchKernelGGL(tril_transpose_kernel, dim3((unsigned)((M + 31) / 32), (unsigned)((M + 31) / 32), (unsigned)K),
