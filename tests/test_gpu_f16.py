@@ -178,7 +178,8 @@ def test_mfma_shape_switches(device):
     assert normwise(to_np(fvc), to_np(fv)) < 1e-6
 
 
-@pytest.mark.parametrize("N,M,K,with_a", [(65536, 1024, 8, False), (8192, 256, 4, True), (3000, 200, 3, True)])
+@pytest.mark.parametrize("N,M,K,with_a", [(65536, 1024, 8, False), (8192, 256, 4, True), (3000, 200, 3, True),
+                                           (8192, 1024, 8, False)])   # c4's per-rank shape: unpaired items
 def test_trsm_stats_f16_batch_bit_identical(device, N, M, K, with_a):
     """mgp_trsm_stats_f16_batch (both layers' K4 in one launch) writes the same A
     images, statistics and f32 A bits as one mgp_trsm_stats_f16 call per layer,
