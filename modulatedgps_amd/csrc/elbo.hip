@@ -18,6 +18,8 @@
 //     a streaming reduction over the packed lower triangle of each L_k.
 #include <math.h>
 
+#include <algorithm>
+
 #include "mgp_common.hpp"
 #include "qsqrt_jobs.hpp"
 
@@ -1061,22 +1063,45 @@ constexpr int kElboLanes = 4;
 #endif
 constexpr int kElboBwdLanes = MGP_K6B_LANES;
 static int64_t elbo_fwd_blocks(int64_t N, int lanes) { return (N * lanes + kElboThreads - 1) / kElboThreads; }
+// The forward's lanes per point by N: 4 from N = 65536 (c3: 262144 threads), 8 or 16 below,
+// so that a small per-rank N (c4's 8192) still gives the latency-bound sample chain
+// 2^17 - 2^18 threads (MGP_K6_ADAPTIVE_LANES = 0: 4 always).
+#ifndef MGP_K6_ADAPTIVE_LANES
+#define MGP_K6_ADAPTIVE_LANES 1
+#endif
+static int elbo_fwd_lanes(int64_t N) {
+  if (!MGP_K6_ADAPTIVE_LANES) return kElboLanes;
+  return N >= 65536 ? 4 : N >= 32768 ? 8 : 16;
+}
 
 extern "C" size_t mgp_elbo_workspace_bytes(int64_t N) {
-  const int64_t nb = elbo_fwd_blocks(N, kElboLanes);
+  const int64_t nb = elbo_fwd_blocks(N, std::max(kElboLanes, elbo_fwd_lanes(N)));
   return (size_t)(nb > 0 ? nb : 1) * sizeof(double);
 }
 
 template <int KM, bool MOD, bool MC>
-static void launch_elbo_terms(int nb, hipStream_t s, const float* mu_f, const float* var_f, const float* mu_a,
-                              const float* var_a, int64_t ldf, const float* Y, const float* lik_var,
-                              const float* lik_var_a, int64_t N, int K, int S, float inv_tau, float jitter,
-                              const float* noise_z, const float* noise_u, uint32_t k0, uint32_t k1,
+static void launch_elbo_terms(int nb, int lanes, hipStream_t s, const float* mu_f, const float* var_f,
+                              const float* mu_a, const float* var_a, int64_t ldf, const float* Y,
+                              const float* lik_var, const float* lik_var_a, int64_t N, int K, int S, float inv_tau,
+                              float jitter, const float* noise_z, const float* noise_u, uint32_t k0, uint32_t k1,
                               int64_t n_offset, double* partials, float mc_a, float mc_b) {
-  constexpr int L = MC ? 1 : kElboLanes;
-  hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC, L>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
-                     var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1, n_offset,
-                     partials, mc_a, mc_b);
+  if constexpr (MC) {
+    hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC, 1>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
+                       var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1,
+                       n_offset, partials, mc_a, mc_b);
+  } else if (lanes == 16) {
+    hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC, 16>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
+                       var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1,
+                       n_offset, partials, mc_a, mc_b);
+  } else if (lanes == 8) {
+    hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC, 8>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f, mu_a,
+                       var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1,
+                       n_offset, partials, mc_a, mc_b);
+  } else {
+    hipLaunchKernelGGL((elbo_terms_kernel<KM, MOD, MC, kElboLanes>), dim3(nb), dim3(kElboThreads), 0, s, mu_f, var_f,
+                       mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, inv_tau, jitter, noise_z, noise_u, k0, k1,
+                       n_offset, partials, mc_a, mc_b);
+  }
 }
 
 // mc: the pred likelihood is MultiClass(K)/RobustMax(eps) with mc_a = log(1 - eps),
@@ -1089,14 +1114,16 @@ static int elbo_terms_run(const float* mu_f, const float* var_f, const float* mu
                           float mc_a = 0.f, float mc_b = 0.f) {
   if (!workspace || workspace_bytes < mgp_elbo_workspace_bytes(N)) return MGP_ERR_WORKSPACE;
   double* partials = (double*)workspace;
-  const int nb = (int)elbo_fwd_blocks(N, mc ? 1 : kElboLanes);
+  const int lanes = mc ? 1 : elbo_fwd_lanes(N);
+  const int nb = (int)elbo_fwd_blocks(N, lanes);
   const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
   if (nb > 0) {
 #define MGP_ELBO_CASE(KM)                                                                               \
   if (K <= KM) {                                                                                         \
     auto f = lik_var_a ? (mc ? launch_elbo_terms<KM, true, true> : launch_elbo_terms<KM, true, false>)   \
                        : (mc ? launch_elbo_terms<KM, false, true> : launch_elbo_terms<KM, false, false>); \
-    f(nb, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, jitter, noise_z,  \
+    f(nb, lanes, s, mu_f, var_f, mu_a, var_a, ldf, Y, lik_var, lik_var_a, N, K, S, 1.f / tau, jitter,    \
+      noise_z,                                                                                           \
       noise_u, k0, k1, n_offset, partials, mc_a, mc_b);                                                  \
   } else
     MGP_ELBO_CASE(1) MGP_ELBO_CASE(2) MGP_ELBO_CASE(4) MGP_ELBO_CASE(8) MGP_ELBO_CASE(16)
